@@ -1,0 +1,216 @@
+/* include/rt_mi355x.h — C ABI of the MI355X (gfx950) per-pixel ray path.
+ *
+ * Drop-in boundary for the reference's render entry point
+ *     void render(size_t numTriangles, int W, int H, const Camera cam, const Vec3 missColor,
+ *                 int max_depth, int spp, const BVHNode* nodes, const AABB* aabbs,
+ *                 const Triangle* triangles, const int32_t* triObjectIds,
+ *                 const Material* objectMaterials, int numObjectMaterials,
+ *                 const Light* lights, int numLights, bool diffuse_bounce, Vec3* output);
+ * (HW2/HW2/GPUandCPU/include/query.h:13-29, defined at include/query.cu:79-167) and of the
+ * host pieces around it that the reference keeps in C++ (scene JSON + OBJ loading,
+ * camera setup, CPU LBVH build, ppm_p6 writer).  Plain C types, plain pointers and sizes;
+ * every function returns RT_OK (0) or a negative RT_ERR_* code and never throws;
+ * rt_last_error() returns the calling thread's last message.
+ *
+ * Structs marked "layout = reference" are byte-for-byte the reference's POD types, so a
+ * caller holding the reference's arrays passes them unchanged.
+ */
+#ifndef RT_MI355X_H
+#define RT_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum {
+    RT_OK = 0,
+    RT_ERR_ARG = -1,          /* bad argument / malformed arrays */
+    RT_ERR_IO = -2,           /* file could not be opened / written */
+    RT_ERR_PARSE = -3,        /* OBJ / JSON / PPM syntax */
+    RT_ERR_HIP = -4,          /* HIP runtime error (message in rt_last_error) */
+    RT_ERR_NOMEM = -5,
+    RT_ERR_NODEVICE = -6,     /* no gfx950 device / code object not loadable */
+    RT_ERR_UNSUPPORTED = -7   /* input outside what the kernels handle (see rt_last_error) */
+};
+
+/* ---- reference POD types ------------------------------------------------------------ */
+typedef struct { float x, y, z; } rt_vec3;                       /* layout = reference: Vec3, G/include/vec3.h:299-304 */
+typedef struct {                                                  /* layout = reference: BVHNode, G/include/bvh.h:7-13 */
+    uint32_t parent_idx, left_idx, right_idx, object_idx;         /* object_idx == 0xFFFFFFFF: internal */
+} rt_bvh_node;
+typedef struct { rt_vec3 min_corner, max_corner; } rt_aabb;      /* layout = reference: AABB, G/include/bvh.h:28-52 */
+typedef struct { rt_vec3 v0, v1, v2, n0, n1, n2; } rt_triangle;  /* layout = reference: Triangle, G/include/MeshOBJ.h:42-67 */
+typedef struct {                                                  /* layout = reference: Material, G/include/material.h:6-21 */
+    rt_vec3 albedo; float kd;
+    rt_vec3 specular_color; float ks; float shininess;
+    float kr;
+    rt_vec3 emission;
+} rt_material;
+typedef struct { rt_vec3 position, color; int32_t intensity; } rt_light; /* layout = reference: Light, G/include/scene.h:21-25 */
+
+/* Derived pinhole basis of the reference Camera (G/include/camera.h:208-216): the fields
+ * render() reads.  Fill with rt_camera_init (same float/double arithmetic as
+ * Camera::initialize, camera.h:72-94). */
+typedef struct {
+    rt_vec3 center, pixel00_loc, pixel_delta_u, pixel_delta_v;
+    int32_t pixel_width, pixel_height;
+} rt_camera;
+
+/* Reference Material() defaults (material.h:8-19). */
+void rt_material_default(rt_material* m);
+
+/* Camera(pos, lookAt, up, focal_length_mm, sensor_height_mm, width, height)
+ * (G/include/camera.h:13-28).  hw1 != 0 follows HW1/include/camera.h (error instead of
+ * clamping width/height < 1). */
+int rt_camera_init(rt_camera* cam, const float pos[3], const float look_at[3], const float up[3],
+                   double focal_length_mm, double sensor_height_mm, int width, int height, int hw1);
+
+/* jittered_samples(spp, seed) (G/include/antialias.h:12-27): std::mt19937 +
+ * uniform_real_distribution<float>; centered != 0 subtracts 0.5 (G/), 0 keeps [0,1) (HW1).
+ * out: 2*spp floats. */
+int rt_jittered_samples(int spp, uint32_t seed, int centered, float* out);
+
+/* ---- host scene: the reference's loaders + CPU LBVH (G/src/main.cu:104-317) -------- */
+typedef struct rt_host_scene rt_host_scene;
+
+typedef struct {
+    /* settings (G/include/scene.h:15-19), miss colour, camera, counts */
+    int32_t max_depth, spp, diffuse_bounce;
+    rt_vec3 miss_color;
+    rt_vec3 cam_position, cam_look_at, cam_up;
+    double focal_length_mm, sensor_height_mm;
+    int32_t pixel_width, pixel_height;
+    uint64_t num_triangles, num_vertices;
+    int32_t num_materials, num_lights, num_objects_loaded;
+    int32_t bvh_max_stack;   /* DFS stack depth the traversal of this tree needs */
+    int32_t bvh_height;
+} rt_scene_info;
+
+typedef struct {  /* views into rt_host_scene storage (valid until rt_host_scene_free) */
+    const rt_bvh_node* nodes;        /* 2P-1 */
+    const rt_aabb* aabbs;            /* 2P-1 */
+    const rt_triangle* triangles;    /* P, packed as G/src/main.cu:388-404 */
+    const int32_t* tri_object_ids;   /* P */
+    const rt_material* materials;    /* num_materials */
+    const rt_light* lights;          /* num_lights (fallback light added as main.cu:328-336) */
+    const rt_vec3* positions;        /* num_vertices (transformed) */
+    const rt_vec3* normals;          /* num_vertices or NULL */
+    const uint32_t* indices;         /* 3P */
+} rt_scene_arrays;
+
+/* Scene JSON (G/include/scene.h:242-393) + every mesh object: LoadOBJ_ToMesh
+ * (G/include/MeshOBJ.h:260-427), applyObjectTransform (G/src/main.cu:57-96), AppendMesh
+ * (MeshOBJ.h:429-466); then calculateAABBs + CPU buildBVH (G/include/bvh.cu:60-89,209-317).
+ * Relative mesh paths resolve like G/src/main.cu:119-147 with project_dir (NULL =
+ * dirname(dirname(dirname(scene)))). */
+int rt_host_scene_load_json(const char* scene_path, const char* project_dir, rt_host_scene** out);
+/* OBJ path list without JSON (G/src/main.cu:151-157): default material/camera/settings. */
+int rt_host_scene_load_objs(const char* const* obj_paths, int n, rt_host_scene** out);
+int rt_host_scene_info(const rt_host_scene* s, rt_scene_info* out);
+int rt_host_scene_arrays(const rt_host_scene* s, rt_scene_arrays* out);
+void rt_host_scene_free(rt_host_scene* s);
+
+/* CPU LBVH over caller arrays (leaf AABBs from indexed triangles), reference algorithm:
+ * nodes/aabbs must hold 2P-1 entries. */
+int rt_build_bvh(const rt_vec3* positions, size_t num_vertices, const uint32_t* indices,
+                 size_t num_triangles, rt_bvh_node* nodes, rt_aabb* aabbs);
+
+/* HW1 mesh: LoadOBJ_ToMeshSOA (HW1/src/MeshOBJ.cpp:143-281). */
+typedef struct rt_mesh rt_mesh;
+typedef struct {
+    const rt_vec3* positions; const rt_vec3* normals; const uint32_t* indices;
+    uint64_t num_vertices, num_triangles; int32_t has_normals, has_uvs;
+} rt_mesh_view;
+int rt_mesh_load_obj_hw1(const char* path, rt_mesh** out);
+int rt_mesh_view_get(const rt_mesh* m, rt_mesh_view* out);
+void rt_mesh_free(rt_mesh* m);
+
+/* ---- ppm_p6 (HW1/ppm_p6_lib/include/ppm_p6.hpp:46-85) ------------------------------- */
+typedef struct { int32_t maxval, clamp, gamma2, flip_y; } rt_ppm_options;  /* defaults 255,1,1,0 */
+void rt_ppm_options_default(rt_ppm_options* o);
+/* rgb: W*H*3 floats, row 0 = top.  Writes "P6\n<W> <H>\n<maxval>\n" + samples. */
+int rt_ppm_write(const char* path, const float* rgb, int width, int height, const rt_ppm_options* opt);
+/* Same bytes into memory: needs 32 + W*H*3*(maxval<256 ? 1 : 2) bytes; *written = size. */
+int rt_ppm_encode(const float* rgb, int width, int height, const rt_ppm_options* opt,
+                  uint8_t* buf, size_t cap, size_t* written);
+/* read_p6 (ppm_p6.cpp:303-372): rgb_out may be NULL to query W/H first. */
+int rt_ppm_read(const char* path, float* rgb_out, size_t cap_floats, int* width, int* height, int* maxval);
+
+/* ---- the hot path: device-resident scene + HIP render ---------------------------------- */
+typedef struct rt_scene rt_scene;
+
+/* Upload the reference arrays to `device`, validating them (indices in range, a proper
+ * binary tree rooted at 0) and repacking them into the gfx950 traversal layout. */
+int rt_scene_create(int device, size_t num_triangles, const rt_bvh_node* nodes, const rt_aabb* aabbs,
+                    const rt_triangle* triangles, const int32_t* tri_object_ids,
+                    const rt_material* materials, int num_materials, const rt_light* lights,
+                    int num_lights, rt_scene** out);
+void rt_scene_destroy(rt_scene* s);
+int rt_scene_device(const rt_scene* s);
+size_t rt_scene_device_bytes(const rt_scene* s);
+
+enum {
+    RT_KERNEL_AUTO = 0,      /* the fastest parity-equivalent kernel */
+    RT_KERNEL_WAVE = 1,      /* wave-coherent masked DFS (shared per-wave stack) */
+    RT_KERNEL_LANE = 2       /* one private DFS stack per lane (baseline variant) */
+};
+
+typedef struct {
+    int32_t max_depth;        /* TraceRayIterative depth (query.h:156) */
+    int32_t spp;
+    int32_t diffuse_bounce;
+    rt_vec3 miss_color;
+    const float* jitter;      /* host, 2*spp floats; NULL = rt_jittered_samples(spp, 42, 1) */
+    /* Image sharding: rows are cut into bands of band_rows; this call renders bands b with
+     * b % band_count == band_index, written contiguously (band order) into the output
+     * ("strip" layout).  band_count <= 1 renders the whole frame in row-major order. */
+    int32_t band_rows, band_index, band_count;
+    int32_t kernel;           /* RT_KERNEL_* */
+} rt_render_opts;
+void rt_render_opts_default(rt_render_opts* o);
+
+/* Rows covered by (band_rows, band_index, band_count) for an H-row image. */
+int rt_shard_rows(int height, int band_rows, int band_index, int band_count);
+
+/* Render into device memory on `hip_stream` (hipStream_t; NULL = the null stream), no
+ * host sync.  rgb_dev: rows*W*3 floats.  hit_idx_dev / hit_t_dev (optional, rows*W*spp):
+ * primary-ray triangle index (-1 = miss) and t per (pixel, sample). */
+int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt,
+                     float* rgb_dev, int32_t* hit_idx_dev, float* hit_t_dev, void* hip_stream);
+
+/* Synchronous convenience: render into host memory (rows*W*3 floats, + optional AOVs). */
+int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt,
+              float* rgb_host, int32_t* hit_idx_host, float* hit_t_host);
+
+/* The reference signature verbatim (query.h:13-29) over host arrays: uploads to device 0,
+ * renders on the GPU, writes W*H Vec3 to `output` (host).  Synchronous. */
+int rt_render_reference(size_t num_triangles, int W, int H, const rt_camera* cam, rt_vec3 miss_color,
+                        int max_depth, int spp, const rt_bvh_node* nodes, const rt_aabb* aabbs,
+                        const rt_triangle* triangles, const int32_t* tri_object_ids,
+                        const rt_material* materials, int num_materials, const rt_light* lights,
+                        int num_lights, int diffuse_bounce, rt_vec3* output);
+
+/* HW1 brute-force path on the GPU (HW1/src/render.cpp:72-116 semantics: every triangle,
+ * closest t >= 0 with the first index winning ties, HW1 shade).  Synchronous; host I/O. */
+int rt_render_hw1(int device, const rt_vec3* positions, const rt_vec3* normals,
+                  const uint32_t* indices, size_t num_triangles, const rt_camera* cam,
+                  rt_vec3 light_position, rt_vec3 light_color, int spp, const float* jitter,
+                  float* rgb_host, int32_t* hit_idx_host, float* hit_t_host);
+
+/* Timing of the last rt_render_device launch sequence on this scene, measured with HIP
+ * events on the stream the kernels ran on: total ms and the main kernel's ms. */
+int rt_last_timing(const rt_scene* s, float* total_ms, float* kernel_ms);
+
+int rt_device_count(int* n);
+const char* rt_last_error(void);
+int rt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_MI355X_H */

@@ -1,0 +1,164 @@
+"""ctypes binding of include/rt_mi355x.h (librt_mi355x.so, built in-tree by build.py).
+
+The library is loaded lazily on first use and never replaced by a Python/CPU fallback:
+if the shared object is missing or a render call finds no gfx950 device, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("RT_MI355X_LIB", PKG / "lib" / "librt_mi355x.so"))
+
+RT_OK = 0
+RT_ERR = {
+    -1: "RT_ERR_ARG", -2: "RT_ERR_IO", -3: "RT_ERR_PARSE", -4: "RT_ERR_HIP",
+    -5: "RT_ERR_NOMEM", -6: "RT_ERR_NODEVICE", -7: "RT_ERR_UNSUPPORTED",
+}
+RT_KERNEL_AUTO, RT_KERNEL_WAVE, RT_KERNEL_LANE = 0, 1, 2
+
+
+class RTError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{RT_ERR.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Vec3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+    def __iter__(self):
+        return iter((self.x, self.y, self.z))
+
+
+class BVHNode(C.Structure):
+    _fields_ = [("parent_idx", C.c_uint32), ("left_idx", C.c_uint32),
+                ("right_idx", C.c_uint32), ("object_idx", C.c_uint32)]
+
+
+class AABB(C.Structure):
+    _fields_ = [("min_corner", Vec3), ("max_corner", Vec3)]
+
+
+class Triangle(C.Structure):
+    _fields_ = [("v0", Vec3), ("v1", Vec3), ("v2", Vec3), ("n0", Vec3), ("n1", Vec3), ("n2", Vec3)]
+
+
+class Material(C.Structure):
+    _fields_ = [("albedo", Vec3), ("kd", C.c_float), ("specular_color", Vec3), ("ks", C.c_float),
+                ("shininess", C.c_float), ("kr", C.c_float), ("emission", Vec3)]
+
+
+class Light(C.Structure):
+    _fields_ = [("position", Vec3), ("color", Vec3), ("intensity", C.c_int32)]
+
+
+class CameraT(C.Structure):
+    _fields_ = [("center", Vec3), ("pixel00_loc", Vec3), ("pixel_delta_u", Vec3),
+                ("pixel_delta_v", Vec3), ("pixel_width", C.c_int32), ("pixel_height", C.c_int32)]
+
+
+class SceneInfo(C.Structure):
+    _fields_ = [("max_depth", C.c_int32), ("spp", C.c_int32), ("diffuse_bounce", C.c_int32),
+                ("miss_color", Vec3), ("cam_position", Vec3), ("cam_look_at", Vec3), ("cam_up", Vec3),
+                ("focal_length_mm", C.c_double), ("sensor_height_mm", C.c_double),
+                ("pixel_width", C.c_int32), ("pixel_height", C.c_int32),
+                ("num_triangles", C.c_uint64), ("num_vertices", C.c_uint64),
+                ("num_materials", C.c_int32), ("num_lights", C.c_int32),
+                ("num_objects_loaded", C.c_int32), ("bvh_max_stack", C.c_int32),
+                ("bvh_height", C.c_int32)]
+
+
+class SceneArrays(C.Structure):
+    _fields_ = [("nodes", C.c_void_p), ("aabbs", C.c_void_p), ("triangles", C.c_void_p),
+                ("tri_object_ids", C.c_void_p), ("materials", C.c_void_p), ("lights", C.c_void_p),
+                ("positions", C.c_void_p), ("normals", C.c_void_p), ("indices", C.c_void_p)]
+
+
+class MeshView(C.Structure):
+    _fields_ = [("positions", C.c_void_p), ("normals", C.c_void_p), ("indices", C.c_void_p),
+                ("num_vertices", C.c_uint64), ("num_triangles", C.c_uint64),
+                ("has_normals", C.c_int32), ("has_uvs", C.c_int32)]
+
+
+class PPMOptions(C.Structure):
+    _fields_ = [("maxval", C.c_int32), ("clamp", C.c_int32), ("gamma2", C.c_int32), ("flip_y", C.c_int32)]
+
+
+class RenderOpts(C.Structure):
+    _fields_ = [("max_depth", C.c_int32), ("spp", C.c_int32), ("diffuse_bounce", C.c_int32),
+                ("miss_color", Vec3), ("jitter", C.c_void_p), ("band_rows", C.c_int32),
+                ("band_index", C.c_int32), ("band_count", C.c_int32), ("kernel", C.c_int32)]
+
+
+P = C.c_void_p
+I = C.c_int
+SZ = C.c_size_t
+
+# name -> (restype, argtypes); every symbol declared in include/rt_mi355x.h
+SIGNATURES = {
+    "rt_material_default": (None, [P]),
+    "rt_camera_init": (I, [P, P, P, P, C.c_double, C.c_double, I, I, I]),
+    "rt_jittered_samples": (I, [I, C.c_uint32, I, P]),
+    "rt_host_scene_load_json": (I, [C.c_char_p, C.c_char_p, P]),
+    "rt_host_scene_load_objs": (I, [P, I, P]),
+    "rt_host_scene_info": (I, [P, P]),
+    "rt_host_scene_arrays": (I, [P, P]),
+    "rt_host_scene_free": (None, [P]),
+    "rt_build_bvh": (I, [P, SZ, P, SZ, P, P]),
+    "rt_mesh_load_obj_hw1": (I, [C.c_char_p, P]),
+    "rt_mesh_view_get": (I, [P, P]),
+    "rt_mesh_free": (None, [P]),
+    "rt_ppm_options_default": (None, [P]),
+    "rt_ppm_write": (I, [C.c_char_p, P, I, I, P]),
+    "rt_ppm_encode": (I, [P, I, I, P, P, SZ, P]),
+    "rt_ppm_read": (I, [C.c_char_p, P, SZ, P, P, P]),
+    "rt_scene_create": (I, [I, SZ, P, P, P, P, P, I, P, I, P]),
+    "rt_scene_destroy": (None, [P]),
+    "rt_scene_device": (I, [P]),
+    "rt_scene_device_bytes": (SZ, [P]),
+    "rt_render_opts_default": (None, [P]),
+    "rt_shard_rows": (I, [I, I, I, I]),
+    "rt_render_device": (I, [P, P, P, P, P, P, P]),
+    "rt_render": (I, [P, P, P, P, P, P]),
+    "rt_render_reference": (I, [SZ, I, I, P, Vec3, I, I, P, P, P, P, P, I, P, I, I, P]),
+    "rt_render_hw1": (I, [I, P, P, P, SZ, P, Vec3, Vec3, I, P, P, P, P]),
+    "rt_last_timing": (I, [P, P, P]),
+    "rt_device_count": (I, [P]),
+    "rt_last_error": (C.c_char_p, []),
+    "rt_abi_version": (I, []),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load librt_mi355x.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RTError(-6, f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != RT_OK:
+        msg = lib().rt_last_error()
+        raise RTError(rc, msg.decode() if msg else "")
+
+
+def ptr(a) -> int | None:
+    """Address of a numpy array / ctypes object (None passes NULL)."""
+    if a is None:
+        return None
+    if hasattr(a, "ctypes"):
+        return a.ctypes.data
+    return C.addressof(a)

@@ -1,0 +1,351 @@
+"""Python mirror of the reference's host interface for the per-pixel ray path.
+
+Names and argument meaning follow the reference (citations relative to the reference repo,
+G/ = HW2/HW2/GPUandCPU):
+
+* :class:`Camera`       — ``Camera(pos, lookAt, up, focal_length_mm, sensor_height_mm, w, h)``
+                          (G/include/camera.h:13-28).
+* :class:`HostScene`    — ``SceneIO::LoadSceneFromFile`` + the mesh/BVH pipeline of
+                          G/src/main.cu:104-317 (loaders, transforms, CPU LBVH).
+* :class:`DeviceScene`  — the scene arrays resident on one MI355X.
+* :func:`render`        — ``render(numTriangles, W, H, cam, missColor, max_depth, spp, nodes,
+                          aabbs, triangles, triObjectIds, objectMaterials, numObjectMaterials,
+                          lights, numLights, diffuse_bounce, output)`` (G/include/query.h:13-29).
+* :func:`render_hw1`    — the HW1 brute-force loop (HW1/src/render.cpp:72-116) on the GPU.
+* :func:`write_p6` / :func:`read_p6` — ppm_p6 (HW1/ppm_p6_lib/include/ppm_p6.hpp:46-85).
+
+All compute goes through librt_mi355x.so; there is no CPU render path here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import check, lib, ptr
+
+LIGHT_DTYPE = np.dtype([("position", "<f4", 3), ("color", "<f4", 3), ("intensity", "<i4")])
+assert LIGHT_DTYPE.itemsize == C.sizeof(L.Light) == 28
+assert C.sizeof(L.Material) == 52 and C.sizeof(L.Triangle) == 72 and C.sizeof(L.AABB) == 24
+
+
+def _v3(v) -> L.Vec3:
+    x, y, z = (float(c) for c in v)
+    return L.Vec3(x, y, z)
+
+
+def _f3(v) -> "C.Array":
+    return (C.c_float * 3)(*[float(c) for c in v])
+
+
+class Camera:
+    """Pinhole camera; ``hw1=True`` follows HW1/include/camera.h (rejects w, h < 1)."""
+
+    def __init__(self, pos=(0.0, 0.0, 0.0), look_at=(0.0, 1.0, 0.0), up=(0.0, 0.0, 1.0),
+                 focal_length_mm: float = 50.0, sensor_height_mm: float = 24.0,
+                 width: int = 100, height: int = 100, hw1: bool = False):
+        self.pos, self.look_at, self.up = tuple(pos), tuple(look_at), tuple(up)
+        self.focal_length_mm, self.sensor_height_mm = float(focal_length_mm), float(sensor_height_mm)
+        self.c = L.CameraT()
+        check(lib().rt_camera_init(C.byref(self.c), _f3(pos), _f3(look_at), _f3(up),
+                                   self.focal_length_mm, self.sensor_height_mm, int(width), int(height),
+                                   1 if hw1 else 0))
+
+    @property
+    def pixel_width(self) -> int:
+        return self.c.pixel_width
+
+    @property
+    def pixel_height(self) -> int:
+        return self.c.pixel_height
+
+    def basis(self) -> dict:
+        """center, pixel00_loc, pixel_delta_u, pixel_delta_v as float32 arrays."""
+        return {k: np.array(tuple(getattr(self.c, k)), np.float32)
+                for k in ("center", "pixel00_loc", "pixel_delta_u", "pixel_delta_v")}
+
+    def resized(self, width: int, height: int) -> "Camera":
+        return Camera(self.pos, self.look_at, self.up, self.focal_length_mm, self.sensor_height_mm,
+                      width, height)
+
+
+def jittered_samples(spp: int, seed: int = 42, centered: bool = True) -> np.ndarray:
+    """(spp, 2) float32 sub-pixel offsets (G/include/antialias.h:12-27; HW1 when not centered)."""
+    out = np.zeros((spp, 2), np.float32)
+    check(lib().rt_jittered_samples(int(spp), int(seed), 1 if centered else 0, ptr(out)))
+    return out
+
+
+def default_material() -> np.ndarray:
+    m = L.Material()
+    lib().rt_material_default(C.byref(m))
+    return np.frombuffer(bytes(m), np.float32).copy()
+
+
+class HostScene:
+    """A G/-dialect scene loaded and BVH-built on the host (arrays in the reference layouts)."""
+
+    def __init__(self, handle: int):
+        self._h = C.c_void_p(handle)
+        info = L.SceneInfo()
+        check(lib().rt_host_scene_info(self._h, C.byref(info)))
+        self.info = info
+        arr = L.SceneArrays()
+        check(lib().rt_host_scene_arrays(self._h, C.byref(arr)))
+        P = int(info.num_triangles)
+        NN = 2 * P - 1
+        nv = int(info.num_vertices)
+
+        def view(addr, dtype, shape):
+            if not addr:
+                return None
+            n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+            buf = (C.c_char * n).from_address(addr)
+            return np.frombuffer(buf, dtype).reshape(shape).copy()  # own the data
+
+        self.num_triangles = P
+        self.nodes = view(arr.nodes, np.uint32, (NN, 4))
+        self.aabbs = view(arr.aabbs, np.float32, (NN, 6))
+        self.triangles = view(arr.triangles, np.float32, (P, 18))
+        self.tri_object_ids = view(arr.tri_object_ids, np.int32, (P,))
+        self.materials = view(arr.materials, np.float32, (info.num_materials, 13))
+        self.lights = view(arr.lights, LIGHT_DTYPE, (info.num_lights,))
+        self.positions = view(arr.positions, np.float32, (nv, 3))
+        self.normals = view(arr.normals, np.float32, (nv, 3))
+        self.indices = view(arr.indices, np.uint32, (P, 3))
+
+    @classmethod
+    def load_json(cls, path, project_dir=None) -> "HostScene":
+        h = C.c_void_p()
+        check(lib().rt_host_scene_load_json(str(path).encode(),
+                                            None if project_dir is None else str(project_dir).encode(),
+                                            C.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def load_objs(cls, paths: Sequence) -> "HostScene":
+        enc = [str(p).encode() for p in paths]
+        arr = (C.c_char_p * len(enc))(*enc)
+        h = C.c_void_p()
+        check(lib().rt_host_scene_load_objs(C.cast(arr, C.c_void_p), len(enc), C.byref(h)))
+        return cls(h.value)
+
+    def camera(self, width: Optional[int] = None, height: Optional[int] = None) -> Camera:
+        i = self.info
+        return Camera(tuple(i.cam_position), tuple(i.cam_look_at), tuple(i.cam_up), i.focal_length_mm,
+                      i.sensor_height_mm, width or i.pixel_width, height or i.pixel_height)
+
+    @property
+    def settings(self) -> dict:
+        i = self.info
+        return {"max_depth": i.max_depth, "spp": i.spp, "diffuse_bounce": bool(i.diffuse_bounce),
+                "miss_color": tuple(i.miss_color)}
+
+    def close(self) -> None:
+        if self._h:
+            lib().rt_host_scene_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MeshHW1:
+    """LoadOBJ_ToMeshSOA (HW1/src/MeshOBJ.cpp:143-281)."""
+
+    def __init__(self, path):
+        h = C.c_void_p()
+        check(lib().rt_mesh_load_obj_hw1(str(path).encode(), C.byref(h)))
+        self._h = h
+        v = L.MeshView()
+        check(lib().rt_mesh_view_get(self._h, C.byref(v)))
+        nv, nt = int(v.num_vertices), int(v.num_triangles)
+        self.positions = np.frombuffer((C.c_char * (nv * 12)).from_address(v.positions), np.float32).reshape(nv, 3).copy()
+        self.normals = (np.frombuffer((C.c_char * (nv * 12)).from_address(v.normals), np.float32).reshape(nv, 3).copy()
+                        if v.normals else None)
+        self.indices = np.frombuffer((C.c_char * (nt * 12)).from_address(v.indices), np.uint32).reshape(nt, 3).copy()
+        self.num_triangles = nt
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().rt_mesh_free(self._h)
+        except Exception:
+            pass
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+class DeviceScene:
+    """Reference arrays uploaded to one device (rt_scene_create)."""
+
+    def __init__(self, num_triangles: int, nodes, aabbs, triangles, tri_object_ids=None,
+                 materials=None, lights=None, device: int = 0):
+        P = int(num_triangles)
+        self._keep = [_c(nodes, np.uint32), _c(aabbs, np.float32), _c(triangles, np.float32)]
+        objs = None if tri_object_ids is None else _c(tri_object_ids, np.int32)
+        mats = None if materials is None else _c(materials, np.float32).reshape(-1, 13)
+        lts = None if lights is None else np.ascontiguousarray(lights, dtype=LIGHT_DTYPE)
+        nmat = 0 if mats is None else mats.shape[0]
+        nl = 0 if lts is None else lts.shape[0]
+        h = C.c_void_p()
+        check(lib().rt_scene_create(int(device), P, ptr(self._keep[0]), ptr(self._keep[1]), ptr(self._keep[2]),
+                                    ptr(objs), ptr(mats), nmat, ptr(lts), nl, C.byref(h)))
+        self._h = h
+        self.num_triangles = P
+        self.device = device
+
+    @classmethod
+    def from_host(cls, hs: HostScene, device: int = 0) -> "DeviceScene":
+        return cls(hs.num_triangles, hs.nodes, hs.aabbs, hs.triangles, hs.tri_object_ids, hs.materials,
+                   hs.lights, device)
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    @property
+    def device_bytes(self) -> int:
+        return int(lib().rt_scene_device_bytes(self._h))
+
+    @staticmethod
+    def make_opts(spp: int = 1, max_depth: int = 1, diffuse_bounce: bool = True, miss_color=(0, 0, 0),
+                  jitter=None, band_rows: int = 8, band_index: int = 0, band_count: int = 1,
+                  kernel: int = L.RT_KERNEL_AUTO):
+        o = L.RenderOpts()
+        lib().rt_render_opts_default(C.byref(o))
+        o.spp, o.max_depth, o.diffuse_bounce = int(spp), int(max_depth), 1 if diffuse_bounce else 0
+        o.miss_color = _v3(miss_color)
+        jit = None
+        if jitter is not None:
+            jit = _c(jitter, np.float32).reshape(-1)
+            o.jitter = jit.ctypes.data
+        o.band_rows, o.band_index, o.band_count, o.kernel = int(band_rows), int(band_index), int(band_count), int(kernel)
+        return o, jit
+
+    def render(self, camera: Camera, spp: int = 1, max_depth: int = 1, diffuse_bounce: bool = True,
+               miss_color=(0, 0, 0), jitter=None, aov: bool = False, band_rows: int = 8,
+               band_index: int = 0, band_count: int = 1, kernel: int = L.RT_KERNEL_AUTO):
+        """Synchronous render to host: (rows, W, 3) float32 [+ (rows, W, spp) hit idx / t]."""
+        o, _jit = self.make_opts(spp, max_depth, diffuse_bounce, miss_color, jitter, band_rows, band_index,
+                                 band_count, kernel)
+        W = camera.pixel_width
+        rows = lib().rt_shard_rows(camera.pixel_height, o.band_rows, o.band_index, o.band_count)
+        if rows < 0:
+            raise L.RTError(-1, "bad band parameters")
+        rgb = np.zeros((rows, W, 3), np.float32)
+        hi = ht = None
+        if aov:
+            hi = np.zeros((rows, W, spp), np.int32)
+            ht = np.zeros((rows, W, spp), np.float32)
+        check(lib().rt_render(self._h, C.byref(camera.c), C.byref(o), ptr(rgb), ptr(hi), ptr(ht)))
+        return (rgb, hi, ht) if aov else rgb
+
+    def render_device(self, camera: Camera, opts, rgb_dev_ptr: int, hit_idx_ptr=None, hit_t_ptr=None,
+                      stream: Optional[int] = None) -> None:
+        check(lib().rt_render_device(self._h, C.byref(camera.c), C.byref(opts), rgb_dev_ptr, hit_idx_ptr,
+                                     hit_t_ptr, stream))
+
+    def last_timing(self):
+        tot, ker = C.c_float(), C.c_float()
+        check(lib().rt_last_timing(self._h, C.byref(tot), C.byref(ker)))
+        return tot.value, ker.value
+
+    def close(self) -> None:
+        if self._h:
+            lib().rt_scene_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def render(numTriangles, W, H, cam: Camera, missColor, max_depth, spp, nodes, aabbs, triangles,
+           triObjectIds, objectMaterials, numObjectMaterials, lights, numLights, diffuse_bounce, output):
+    """The reference entry point (G/include/query.h:13-29) with host arrays; fills ``output``
+    (H*W*3 float32, row-major, row 0 = top) like the CPU branch of query.cu:130-166."""
+    out = np.asarray(output)
+    if out.dtype != np.float32 or not out.flags.c_contiguous or out.size != W * H * 3:
+        raise ValueError("output must be a contiguous float32 array of W*H*3")
+    mats = _c(objectMaterials, np.float32).reshape(-1, 13)[:numObjectMaterials]
+    lts = np.ascontiguousarray(lights, dtype=LIGHT_DTYPE)[:numLights]
+    nd, ab, tr = _c(nodes, np.uint32), _c(aabbs, np.float32), _c(triangles, np.float32)
+    ob = None if triObjectIds is None else _c(triObjectIds, np.int32)
+    check(lib().rt_render_reference(int(numTriangles), int(W), int(H), C.byref(cam.c), _v3(missColor),
+                                    int(max_depth), int(spp), ptr(nd), ptr(ab), ptr(tr), ptr(ob), ptr(mats),
+                                    int(numObjectMaterials), ptr(lts), int(numLights),
+                                    1 if diffuse_bounce else 0, ptr(out)))
+    return out
+
+
+def render_hw1(positions, normals, indices, camera: Camera, light_position, light_color, spp: int = 1,
+               jitter=None, aov: bool = False, device: int = 0):
+    """HW1 brute-force path on the GPU: (H, W, 3) float32 [+ per-sample winning triangle / t]."""
+    pos, nrm, idx = _c(positions, np.float32), _c(normals, np.float32), _c(indices, np.uint32)
+    W, H = camera.pixel_width, camera.pixel_height
+    rgb = np.zeros((H, W, 3), np.float32)
+    hi = ht = None
+    if aov:
+        hi = np.zeros((H, W, spp), np.int32)
+        ht = np.zeros((H, W, spp), np.float32)
+    jit = None if jitter is None else _c(jitter, np.float32).reshape(-1)
+    check(lib().rt_render_hw1(int(device), ptr(pos), ptr(nrm), ptr(idx), idx.size // 3, C.byref(camera.c),
+                              _v3(light_position), _v3(light_color), int(spp), ptr(jit), ptr(rgb), ptr(hi),
+                              ptr(ht)))
+    return (rgb, hi, ht) if aov else rgb
+
+
+def build_bvh(positions, indices):
+    """CPU LBVH (G/include/bvh.cu:209-317) over an indexed mesh: (nodes (2P-1,4), aabbs (2P-1,6))."""
+    pos, idx = _c(positions, np.float32), _c(indices, np.uint32)
+    P = idx.size // 3
+    nodes = np.zeros((2 * P - 1, 4), np.uint32)
+    aabbs = np.zeros((2 * P - 1, 6), np.float32)
+    check(lib().rt_build_bvh(ptr(pos), pos.size // 3, ptr(idx), P, ptr(nodes), ptr(aabbs)))
+    return nodes, aabbs
+
+
+def _ppm_opts(maxval=255, clamp=True, gamma2=True, flip_y=False) -> L.PPMOptions:
+    return L.PPMOptions(int(maxval), 1 if clamp else 0, 1 if gamma2 else 0, 1 if flip_y else 0)
+
+
+def encode_p6(rgb, maxval=255, clamp=True, gamma2=True, flip_y=False) -> bytes:
+    a = _c(rgb, np.float32)
+    H, W = a.shape[0], a.shape[1]
+    o = _ppm_opts(maxval, clamp, gamma2, flip_y)
+    n = C.c_size_t()
+    check(lib().rt_ppm_encode(ptr(a), W, H, C.byref(o), None, 0, C.byref(n)))
+    buf = (C.c_uint8 * n.value)()
+    check(lib().rt_ppm_encode(ptr(a), W, H, C.byref(o), C.cast(buf, C.c_void_p), n.value, C.byref(n)))
+    return bytes(buf)
+
+
+def write_p6(path, rgb, maxval=255, clamp=True, gamma2=True, flip_y=False) -> None:
+    a = _c(rgb, np.float32)
+    o = _ppm_opts(maxval, clamp, gamma2, flip_y)
+    check(lib().rt_ppm_write(str(path).encode(), ptr(a), a.shape[1], a.shape[0], C.byref(o)))
+
+
+def read_p6(path) -> np.ndarray:
+    w, h, mv = C.c_int(), C.c_int(), C.c_int()
+    check(lib().rt_ppm_read(str(path).encode(), None, 0, C.byref(w), C.byref(h), C.byref(mv)))
+    out = np.zeros((h.value, w.value, 3), np.float32)
+    check(lib().rt_ppm_read(str(path).encode(), ptr(out), out.size, C.byref(w), C.byref(h), C.byref(mv)))
+    return out
+
+
+def device_count() -> int:
+    n = C.c_int()
+    rc = lib().rt_device_count(C.byref(n))
+    return n.value if rc == 0 else 0

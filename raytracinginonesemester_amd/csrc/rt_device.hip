@@ -1,0 +1,1073 @@
+// rt_device.hip — the hot path on gfx950: camera ray -> BVH traversal -> Möller–Trumbore
+// -> Lambert/Blinn-Phong with hard shadow rays (-> optional bounces), and the C-ABI
+// entry points that own device memory.
+//
+// Reference path (G/ = HW2/HW2/GPUandCPU): render() CPU branch include/query.cu:130-166,
+// TraceRayIterative query.h:156-220, SearchBVH query.h:224-311, ShadeDirect/IsInShadow
+// shader.h:44-110, EvaluateBRDF brdf.h:12-40, Camera::get_ray camera.h:49-53.
+//
+// Device layout (built from the reference arrays by rt_scene_create):
+//   inode[i]  64 B  children's AABBs + child refs of internal node i   (4 x float4)
+//   ibox[i]   32 B  internal node i's own AABB (pop-time re-tests)      (2 x float4)
+//   leaf[j]   64 B  v0, e1, e2, triangle index and the leaf's own AABB  (4 x float4)
+//   tnorm[t]  48 B  n0, n1, n2 of triangle t (read once per hit)        (3 x float4)
+// A child ref is an internal index, LEAF_BIT | leaf index, or NO_REF.
+//
+// Two traversal kernels, both bit-exact against the reference order:
+//  * WAVE: one DFS per wavefront over a shared stack held in four VGPRs (entry k in lane
+//    k, pushed with v_writelane, popped with v_readlane); each entry carries the 64-bit
+//    mask of lanes that pushed it.  The reference's order (push left then right, pop
+//    right first) is the same for every ray, so each lane sees exactly its own DFS as a
+//    subsequence and makes every box/triangle decision with the same bestT the reference
+//    would.  Node records are wave-uniform and come in through the scalar cache.
+//  * LANE: one private stack per lane (the reference's structure, kept for A/B).
+// Pop-time box re-tests are skipped when no lane's bestT changed since the push (the
+// re-test would repeat the push-time computation with the same inputs).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <algorithm>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rt_common.hpp"
+#include "rt_math.hpp"
+
+using namespace rtd;
+
+namespace {
+
+constexpr uint32_t LEAF_BIT = 0x80000000u;
+constexpr uint32_t NO_REF = 0xFFFFFFFFu;
+constexpr uint32_t VER_FORCE = 0xFFFFFFFFu;   // pop must re-test (root)
+constexpr int STACK_CAP = 64;                 // one entry per lane of the wave stack
+constexpr int BLOCK = 256;
+constexpr float kRayTMin = 1e-4f;             // query.h:233
+constexpr float RT_EPS = 1e-3f;               // shader.h:22
+
+struct DevMaterial {  // rt_material, read through a 4-byte aligned pointer
+    float albedo[3], kd, spec[3], ks, shininess, kr, emission[3];
+};
+struct DevLight {
+    float pos[3], color[3];
+    int32_t intensity;
+};
+
+struct SceneView {
+    const float4* __restrict__ inode;
+    const float4* __restrict__ ibox;
+    const float4* __restrict__ leaf;
+    const float4* __restrict__ tnorm;
+    const int32_t* __restrict__ objids;
+    const DevMaterial* __restrict__ mats;
+    const DevLight* __restrict__ lights;
+    int32_t num_tris, num_mats, num_lights;
+    uint32_t root_ref;
+    float root_box[6];
+};
+
+struct RenderParams {
+    SceneView sc;
+    f3 cam_center, cam_p00, cam_du, cam_dv;
+    int32_t W, H, spp, max_depth, diffuse_bounce;
+    f3 miss;
+    const float* __restrict__ jitter;  // 2*spp (device)
+    int32_t band_rows, band_index, band_count, rows;  // rows = local rows rendered
+    int32_t tile_w, tile_h, tiles_x, tiles_total;     // pixel tile per block
+    int32_t lane_samples;                             // 1: one sample per lane; else pixel loop
+    float* __restrict__ rgb;
+    int32_t* __restrict__ hit_idx;
+    float* __restrict__ hit_t;
+};
+
+// ---- wave primitives ------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+// v_writelane equivalent (no clang builtin on this toolchain): lane l takes v.
+__device__ __forceinline__ uint32_t wrlane(uint32_t v, uint32_t l, uint32_t old) {
+    return lane_id() == l ? v : old;
+}
+
+// ---- node accessors ---------------------------------------------------------------------
+struct Box {
+    float mn[3], mx[3];
+};
+
+__device__ __forceinline__ Box own_box(const SceneView& sc, uint32_t ref, bool is_root) {
+    Box b;
+    if (is_root) {
+        b.mn[0] = sc.root_box[0]; b.mn[1] = sc.root_box[1]; b.mn[2] = sc.root_box[2];
+        b.mx[0] = sc.root_box[3]; b.mx[1] = sc.root_box[4]; b.mx[2] = sc.root_box[5];
+    } else if (ref & LEAF_BIT) {
+        const float4* L = sc.leaf + 4 * (size_t)(ref & ~LEAF_BIT);
+        const float4 a = L[1], c = L[2], d = L[3];
+        b.mn[0] = a.w; b.mn[1] = c.w; b.mn[2] = d.x;
+        b.mx[0] = d.y; b.mx[1] = d.z; b.mx[2] = d.w;
+    } else {
+        const float4* B = sc.ibox + 2 * (size_t)ref;
+        const float4 lo = B[0], hi = B[1];
+        b.mn[0] = lo.x; b.mn[1] = lo.y; b.mn[2] = lo.z;
+        b.mx[0] = hi.x; b.mx[1] = hi.y; b.mx[2] = hi.z;
+    }
+    return b;
+}
+
+__device__ __forceinline__ bool box_test(const RayPre& r, const Box& b, float bestT) {
+    return box_hit(r, b.mn[0], b.mn[1], b.mn[2], b.mx[0], b.mx[1], b.mx[2], (double)kRayTMin, (double)bestT);
+}
+
+// Result of one closest-hit query.
+struct HitState {
+    float bestT;
+    int32_t slot;  // leaf index of the current best, -1 = none
+};
+
+// ---- WAVE traversal ---------------------------------------------------------------------
+// Every lane of the wave must call this (uniform control flow); `active` selects the
+// lanes that own a ray.  any_hit_dist > 0: shadow query — a lane stops as soon as its
+// bestT < dist (bestT only decreases, so the reference's final `hit && t < dist` is then
+// already true); the traversal order up to that point is the reference's.
+__device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre& r, bool active,
+                                              bool any_hit, float any_hit_dist, HitState& hs) {
+    const uint32_t lane = lane_id();
+    const uint64_t lane_bit = 1ull << lane;
+    uint64_t alive = ballot(active);
+    hs.bestT = FLT_MAX;
+    hs.slot = -1;
+    if (alive == 0) return;
+    uint32_t st_ref = 0, st_mlo = 0, st_mhi = 0, st_ver = 0;  // lane k holds entry k
+    int sp = 0;
+    uint32_t wave_ver = 0;
+    st_ref = wrlane(sc.root_ref, 0, st_ref);
+    st_mlo = wrlane((uint32_t)alive, 0, st_mlo);
+    st_mhi = wrlane((uint32_t)(alive >> 32), 0, st_mhi);
+    st_ver = wrlane(VER_FORCE, 0, st_ver);
+    sp = 1;
+    while (sp > 0) {
+        --sp;
+        const uint32_t ref = rdlane(st_ref, sp);
+        uint64_t mask = ((uint64_t)rdlane(st_mhi, sp) << 32) | rdlane(st_mlo, sp);
+        const uint32_t ver = rdlane(st_ver, sp);
+        mask &= alive;
+        if (mask == 0) continue;
+        bool act = (mask & lane_bit) != 0;
+        if (ver != wave_ver) {  // some lane's bestT changed since the push: pop-time re-test
+            const Box b = own_box(sc, ref, ver == VER_FORCE);
+            const bool pass = act && box_test(r, b, hs.bestT);
+            mask = ballot(pass);
+            act = pass;
+            if (mask == 0) continue;
+        }
+        if (ref & LEAF_BIT) {
+            const uint32_t slot = ref & ~LEAF_BIT;
+            const float4* L = sc.leaf + 4 * (size_t)slot;
+            const float4 a = L[0], b = L[1], c = L[2];
+            float t, u, v;
+            const bool h = act && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), kRayTMin,
+                                       hs.bestT, t, u, v);
+            if (h) {
+                hs.bestT = t;
+                hs.slot = (int32_t)slot;
+            }
+            const uint64_t hm = ballot(h);
+            if (hm != 0) {
+                ++wave_ver;
+                if (any_hit) alive &= ~ballot(h && t < any_hit_dist);
+            }
+            continue;
+        }
+        const float4* N = sc.inode + 4 * (size_t)ref;
+        const float4 q0 = N[0], q1 = N[1], q2 = N[2];
+        const uint4 q3 = *reinterpret_cast<const uint4*>(N + 3);
+        const uint32_t lref = q3.x, rref = q3.y;
+        if (lref != NO_REF) {
+            const bool pl = act && box_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, (double)kRayTMin, (double)hs.bestT);
+            const uint64_t ml = ballot(pl);
+            if (ml != 0) {
+                st_ref = wrlane(lref, sp, st_ref);
+                st_mlo = wrlane((uint32_t)ml, sp, st_mlo);
+                st_mhi = wrlane((uint32_t)(ml >> 32), sp, st_mhi);
+                st_ver = wrlane(wave_ver, sp, st_ver);
+                ++sp;
+            }
+        }
+        if (rref != NO_REF) {
+            const bool pr = act && box_hit(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, (double)kRayTMin, (double)hs.bestT);
+            const uint64_t mr = ballot(pr);
+            if (mr != 0) {
+                st_ref = wrlane(rref, sp, st_ref);
+                st_mlo = wrlane((uint32_t)mr, sp, st_mlo);
+                st_mhi = wrlane((uint32_t)(mr >> 32), sp, st_mhi);
+                st_ver = wrlane(wave_ver, sp, st_ver);
+                ++sp;
+            }
+        }
+    }
+}
+
+// ---- LANE traversal (private stack per lane; the reference's shape) ---------------------
+__device__ __forceinline__ void traverse_lane(const SceneView& sc, const RayPre& r, bool active,
+                                              bool any_hit, float any_hit_dist, HitState& hs) {
+    hs.bestT = FLT_MAX;
+    hs.slot = -1;
+    if (!active) return;
+    uint32_t st_ref[STACK_CAP];
+    uint32_t st_ver[STACK_CAP];
+    int sp = 0;
+    uint32_t ver = 0;
+    st_ref[0] = sc.root_ref;
+    st_ver[0] = VER_FORCE;
+    sp = 1;
+    while (sp > 0) {
+        --sp;
+        const uint32_t ref = st_ref[sp];
+        const uint32_t pv = st_ver[sp];
+        if (pv != ver) {
+            const Box b = own_box(sc, ref, pv == VER_FORCE);
+            if (!box_test(r, b, hs.bestT)) continue;
+        }
+        if (ref & LEAF_BIT) {
+            const uint32_t slot = ref & ~LEAF_BIT;
+            const float4* L = sc.leaf + 4 * (size_t)slot;
+            const float4 a = L[0], b = L[1], c = L[2];
+            float t, u, v;
+            if (mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), kRayTMin, hs.bestT, t, u, v)) {
+                hs.bestT = t;
+                hs.slot = (int32_t)slot;
+                ++ver;
+                if (any_hit && t < any_hit_dist) return;
+            }
+            continue;
+        }
+        const float4* N = sc.inode + 4 * (size_t)ref;
+        const float4 q0 = N[0], q1 = N[1], q2 = N[2];
+        const uint4 q3 = *reinterpret_cast<const uint4*>(N + 3);
+        if (q3.x != NO_REF &&
+            box_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, (double)kRayTMin, (double)hs.bestT)) {
+            st_ref[sp] = q3.x;
+            st_ver[sp] = ver;
+            ++sp;
+        }
+        if (q3.y != NO_REF &&
+            box_hit(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, (double)kRayTMin, (double)hs.bestT)) {
+            st_ref[sp] = q3.y;
+            st_ver[sp] = ver;
+            ++sp;
+        }
+    }
+}
+
+// any_hit (wave-uniform): shadow query, stop a lane once bestT < any_hit_dist.
+template <int MODE>
+__device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, bool active, bool any_hit,
+                                         float any_hit_dist, HitState& hs) {
+    if constexpr (MODE == RT_KERNEL_LANE) traverse_lane(sc, r, active, any_hit, any_hit_dist, hs);
+    else traverse_wave(sc, r, active, any_hit, any_hit_dist, hs);
+}
+
+// Full hit record of the winning leaf (intersectTriangle's tail, query.h:110-130).
+struct SurfHit {
+    f3 p, n;
+    int32_t tri;
+};
+
+__device__ __forceinline__ SurfHit resolve_hit(const SceneView& sc, const RayPre& r, int32_t slot) {
+    const float4* L = sc.leaf + 4 * (size_t)slot;
+    const float4 a = L[0], b = L[1], c = L[2];
+    const f3 v0 = mk(a.x, a.y, a.z), e1 = mk(b.x, b.y, b.z), e2 = mk(c.x, c.y, c.z);
+    float t = 0.f, u = 0.f, v = 0.f;
+    mt_g(r, v0, e1, e2, -FLT_MAX, FLT_MAX, t, u, v);  // same t/u/v as the accepting test
+    SurfHit s;
+    s.tri = __float_as_int(a.w);
+    const float4* Nn = sc.tnorm + 3 * (size_t)s.tri;
+    const float4 n0 = Nn[0], n1 = Nn[1], n2 = Nn[2];
+    hit_frame(r, e1, e2, mk(n0.x, n0.y, n0.z), mk(n1.x, n1.y, n1.z), mk(n2.x, n2.y, n2.z), t, u, v, s.p, s.n);
+    return s;
+}
+
+__device__ __forceinline__ DevMaterial material_of(const SceneView& sc, int32_t tri) {
+    // assignMaterialToHit (query.h:134-153) over Material() defaults (material.h:8-19)
+    DevMaterial m = {{0.8f, 0.8f, 0.8f}, 1.0f, {0.04f, 0.04f, 0.04f}, 0.0f, 32.0f, 0.0f, {0.f, 0.f, 0.f}};
+    if (sc.objids != nullptr && sc.mats != nullptr && tri >= 0 && tri < sc.num_tris) {
+        const int oid = sc.objids[tri];
+        if (oid >= 0 && oid < sc.num_mats) m = sc.mats[oid];
+    }
+    return m;
+}
+
+// EvaluateBRDF (brdf.h:12-40)
+__device__ __forceinline__ f3 eval_brdf(const DevMaterial& m, f3 N, f3 V, f3 L) {
+    const float NdotL = fmaxf(dot(N, L), 0.0f);
+    const float NdotV = fmaxf(dot(N, V), 0.0f);
+    if (NdotL <= 0.f || NdotV <= 0.f) return mk(0.f, 0.f, 0.f);
+    const float invPi = 0.31830988618f;
+    const f3 fd = scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), m.kd * invPi);
+    const f3 Hh = unit(add(L, V));
+    const float NdotH = fmaxf(dot(N, Hh), 0.0f);
+    const float inv2Pi = 0.15915494309f;
+    const float specNorm = (m.shininess + 2.0f) * inv2Pi;
+    const float specLobe = specNorm * powf(NdotH, m.shininess);
+    const f3 fs = scale(scale(mk(m.spec[0], m.spec[1], m.spec[2]), m.ks), specLobe);
+    return add(fd, fs);
+}
+
+// One camera sample through TraceRayIterative (query.h:156-220) + ShadeDirect (shader.h).
+// All lanes of a wave call it; `valid` marks lanes owning a sample.
+template <int MODE>
+__device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int32_t* prim_idx,
+                           float* prim_t) {
+    const SceneView& sc = P.sc;
+    // Camera::get_ray(float, float) (camera.h:49-53) with the jittered_samples offsets
+    const float jx = valid ? P.jitter[2 * s] : 0.f;
+    const float jy = valid ? P.jitter[2 * s + 1] : 0.f;
+    const float px = (float)x + jx, py = (float)y + jy;
+    const f3 pix = add(add(P.cam_p00, scale(P.cam_du, px)), scale(P.cam_dv, py));
+    RayPre ray = make_ray(P.cam_center, cam_unit(sub(pix, P.cam_center)));
+    uint32_t rng = make_rng_seed(x, y, s);
+
+    f3 radiance = mk(0.f, 0.f, 0.f);
+    f3 thr = mk(1.f, 1.f, 1.f);
+    bool alive = valid && P.max_depth > 0;
+    for (int depth = 0; depth < P.max_depth; ++depth) {
+        if (ballot(alive) == 0) break;
+        HitState hs;
+        traverse<MODE>(sc, ray, alive, false, 0.0f, hs);
+        const bool hit = alive && hs.slot >= 0;
+        SurfHit sh;
+        sh.tri = -1;
+        if (hit) sh = resolve_hit(sc, ray, hs.slot);
+        if (depth == 0 && valid) {
+            *prim_idx = hit ? sh.tri : -1;
+            *prim_t = hit ? hs.bestT : -1.0f;
+        }
+        if (alive && !hit) {
+            radiance = add(radiance, mul(thr, P.miss));
+            alive = false;
+        }
+        // ShadeDirect (shader.h:65-110)
+        DevMaterial m;
+        f3 N = mk(0.f, 0.f, 1.f), V = N, Lo = mk(0.f, 0.f, 0.f);
+        if (hit) {
+            m = material_of(sc, sh.tri);
+            N = unit(sh.n);
+            V = unit(sub(ray.o, sh.p));
+            Lo = add(Lo, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 0.05f));
+            Lo = add(Lo, mk(m.emission[0], m.emission[1], m.emission[2]));
+        }
+        for (int li = 0; li < sc.num_lights; ++li) {
+            const DevLight& lt = sc.lights[li];
+            const f3 lpos = mk(lt.pos[0], lt.pos[1], lt.pos[2]);
+            float NdotL = 0.f, dist = 0.f;
+            f3 L = mk(0.f, 0.f, 0.f);
+            bool need = false;
+            RayPre sray = ray;
+            if (hit) {
+                L = unit(sub(lpos, sh.p));
+                NdotL = fmaxf(dot(N, L), 0.0f);
+                if (NdotL > 0.0f) {
+                    // IsInShadow (shader.h:44-62)
+                    const f3 toL = sub(lpos, sh.p);
+                    dist = sqrtf(dot(toL, toL));
+                    if (dist > 0.0f) {
+                        need = true;
+                        sray = make_ray(add(sh.p, scale(N, RT_EPS)), divf(toL, dist));
+                    }
+                }
+            }
+            HitState shs;
+            traverse<MODE>(sc, sray, need, true, dist, shs);
+            const bool occluded = need && shs.slot >= 0 && shs.bestT < dist;
+            if (hit && NdotL > 0.0f && !occluded) {
+                const f3 f = eval_brdf(m, sh.n, V, L);
+                const f3 rad = scale(mk(lt.color[0], lt.color[1], lt.color[2]), (float)lt.intensity);
+                Lo = add(Lo, scale(mul(rad, f), NdotL));
+            }
+        }
+        if (hit) {
+            radiance = add(radiance, mul(thr, Lo));
+            // bounce (query.h:193-216); skipped after the last depth where it has no effect
+            if (depth + 1 < P.max_depth) {
+                const float kd = m.kd, kr = m.kr, total = kd + kr;
+                if (total <= 0.0f) {
+                    alive = false;
+                } else {
+                    const f3 Nb = unit(sh.n);
+                    const float xi = rng_next(rng);
+                    if (P.diffuse_bounce && xi < kd / total) {
+                        f3 dd = random_unit_vector(rng);
+                        if (!(dot(dd, Nb) > 0.0f)) dd = mk(-dd.x, -dd.y, -dd.z);
+                        ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), dd);
+                        const float nl = fmaxf(dot(Nb, dd), 0.0f);
+                        thr = mul(thr, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 2.0f * nl));
+                    } else {
+                        const f3 I = unit(ray.d);
+                        const f3 refl = sub(I, scale(Nb, 2.0f * dot(I, Nb)));
+                        ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), refl);
+                        thr = mul(thr, scale(mk(m.spec[0], m.spec[1], m.spec[2]), kr));
+                    }
+                    if (thr.x < 1e-4f && thr.y < 1e-4f && thr.z < 1e-4f) alive = false;
+                }
+            } else {
+                alive = false;
+            }
+        }
+    }
+    return clamp01(radiance);
+}
+
+// Local row -> image row for the band sharding of rt_render_opts.
+__device__ __forceinline__ int global_row(const RenderParams& P, int r) {
+    if (P.band_count <= 1) return r;
+    const int k = r / P.band_rows, within = r - k * P.band_rows;
+    return (P.band_index + k * P.band_count) * P.band_rows + within;
+}
+
+// XCD-aware block order: blocks b, b+8, b+16 ... share an XCD (round-robin dispatch), so
+// give each such group a contiguous run of tiles (shared BVH working set in that L2).
+__device__ __forceinline__ int tile_of_block(int b, int nblocks) {
+    const int q = nblocks / 8, rr = nblocks % 8;
+    const int xcd = b % 8, idx = b / 8;
+    return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+}
+
+// One sample per lane: a block covers tile_w x tile_h pixels x spp samples (spp a power
+// of two <= 256, tile_w*tile_h*spp == BLOCK); per-pixel sums run in sample order from LDS.
+template <int MODE>
+__global__ __launch_bounds__(BLOCK) void render_samples_kernel(RenderParams P) {
+    __shared__ float col[BLOCK * 3];
+    const int tile = tile_of_block((int)blockIdx.x, (int)gridDim.x);
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    const int t = (int)threadIdx.x;
+    const int s = t % P.spp;
+    const int pit = t / P.spp;
+    const int x = tx * P.tile_w + pit % P.tile_w;
+    const int r = ty * P.tile_h + pit / P.tile_w;
+    const bool valid = x < P.W && r < P.rows;
+    const int y = valid ? global_row(P, r) : 0;
+    int32_t pidx = -1;
+    float pt = -1.f;
+    const f3 c = trace_sample<MODE>(P, valid, x, y, s, &pidx, &pt);
+    if (valid && P.hit_idx) {
+        const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp + (size_t)s;
+        P.hit_idx[k] = pidx;
+        P.hit_t[k] = pt;
+    }
+    col[3 * t] = c.x;
+    col[3 * t + 1] = c.y;
+    col[3 * t + 2] = c.z;
+    __syncthreads();
+    if (valid && s == 0) {
+        // col = col + TraceRayIterative(...) in sample order, then col / float(spp)
+        f3 acc = mk(0.f, 0.f, 0.f);
+        for (int k = 0; k < P.spp; ++k) acc = add(acc, mk(col[3 * (t + k)], col[3 * (t + k) + 1], col[3 * (t + k) + 2]));
+        const float fs = (float)P.spp;
+        float* o = P.rgb + ((size_t)r * P.W + x) * 3;
+        o[0] = acc.x / fs;
+        o[1] = acc.y / fs;
+        o[2] = acc.z / fs;
+    }
+}
+
+// General spp: one pixel per lane looping over its samples in order (query.cu:146-163).
+template <int MODE>
+__global__ __launch_bounds__(BLOCK) void render_pixels_kernel(RenderParams P) {
+    const int tile = tile_of_block((int)blockIdx.x, (int)gridDim.x);
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    const int t = (int)threadIdx.x;
+    const int x = tx * P.tile_w + t % P.tile_w;
+    const int r = ty * P.tile_h + t / P.tile_w;
+    const bool valid = x < P.W && r < P.rows;
+    const int y = valid ? global_row(P, r) : 0;
+    f3 acc = mk(0.f, 0.f, 0.f);
+    for (int s = 0; s < P.spp; ++s) {
+        int32_t pidx = -1;
+        float pt = -1.f;
+        const f3 c = trace_sample<MODE>(P, valid, x, y, s, &pidx, &pt);
+        if (valid && P.hit_idx) {
+            const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp + (size_t)s;
+            P.hit_idx[k] = pidx;
+            P.hit_t[k] = pt;
+        }
+        acc = add(acc, c);
+    }
+    if (valid) {
+        const float fs = (float)P.spp;
+        float* o = P.rgb + ((size_t)r * P.W + x) * 3;
+        o[0] = acc.x / fs;
+        o[1] = acc.y / fs;
+        o[2] = acc.z / fs;
+    }
+}
+
+// ---- HW1 brute force (HW1/src/render.cpp:72-116) ----------------------------------------
+struct Hw1Params {
+    const float4* __restrict__ tri;   // 3 float4 per triangle: v0, e1, e2
+    const float4* __restrict__ nrm;   // 3 float4 per triangle: n0, n1, n2
+    int32_t num_tris;
+    f3 center, p00, du, dv;
+    int32_t W, H, spp;
+    f3 lpos, lcol;
+    const float* __restrict__ jitter;
+    float* __restrict__ rgb;
+    int32_t* __restrict__ hit_idx;
+    float* __restrict__ hit_t;
+};
+
+// HW1 shade (HW1/include/raytracer.h:21-48), material hard-coded at ray.h:111-114.
+__device__ __forceinline__ f3 shade_hw1(f3 o, f3 d, bool hit, f3 p, f3 n, f3 lpos, f3 lcol) {
+    if (!hit) {
+        const f3 ud = unit(d);
+        const float t = 0.5f * (ud.z + 1.0f);
+        return add(scale(mk(1.f, 1.f, 1.f), 1.0f - t), scale(mk(0.5f, 0.7f, 1.0f), t));
+    }
+    const f3 albedo = mk(0.8f, 0.2f, 0.2f);
+    const f3 ambient = scale(albedo, 0.1f);
+    const f3 lightDir = unit(sub(lpos, p));
+    const float diff = fmaxf(dot(n, lightDir), 0.0f);
+    const f3 diffuse = scale(mul(albedo, lcol), diff);
+    const f3 viewDir = unit(sub(o, p));
+    const f3 halfDir = unit(add(lightDir, viewDir));
+    const float spec = powf(fmaxf(dot(n, halfDir), 0.0f), 64.0f);
+    f3 c = add(add(ambient, diffuse), scale(lcol, spec));
+    if (c.x > 1.0f) c.x = 1.0f;
+    if (c.y > 1.0f) c.y = 1.0f;
+    if (c.z > 1.0f) c.z = 1.0f;
+    return c;
+}
+
+__global__ __launch_bounds__(BLOCK) void render_hw1_kernel(Hw1Params P) {
+    const int tiles_x = (P.W + 15) / 16;
+    const int tile = (int)blockIdx.x;
+    const int x = (tile % tiles_x) * 16 + (int)threadIdx.x % 16;
+    const int y = (tile / tiles_x) * 16 + (int)threadIdx.x / 16;
+    const bool valid = x < P.W && y < P.H;
+    f3 acc = mk(0.f, 0.f, 0.f);
+    for (int s = 0; s < P.spp; ++s) {
+        const float px = (float)x + P.jitter[2 * s];
+        const float py = (float)y + P.jitter[2 * s + 1];
+        const int ix = (int)px, iy = (int)py;  // get_pixel_position(int, int) truncates
+        const f3 pix = add(add(P.p00, scale(P.du, (float)ix)), scale(P.dv, (float)iy));
+        const f3 d = unit(sub(pix, P.center));  // HW1 Ray normalises (ray.h:25)
+        const f3 o = P.center;
+        float best = FLT_MAX;
+        int32_t besti = -1;
+        for (int k = 0; k < P.num_tris; ++k) {  // wave-uniform: triangle data via the scalar cache
+            const float4* T = P.tri + 3 * (size_t)k;
+            const float4 a = T[0], b = T[1], c = T[2];
+            float t, u, v;
+            if (valid && mt_hw1(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), t, u, v)) {
+                if (t < best) {  // rec.t < prev.t: the first index wins ties
+                    best = t;
+                    besti = k;
+                }
+            }
+        }
+        f3 p = mk(0.f, 0.f, 0.f), n = p;
+        const bool hit = besti >= 0;
+        if (hit) {
+            const float4* T = P.tri + 3 * (size_t)besti;
+            const float4 a = T[0], b = T[1], c = T[2];
+            float t, u, v;
+            mt_hw1(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), t, u, v);
+            p = add(o, scale(d, t));
+            const float4* N = P.nrm + 3 * (size_t)besti;
+            const float w = 1.0f - u - v;
+            n = add(add(scale(mk(N[0].x, N[0].y, N[0].z), w), scale(mk(N[1].x, N[1].y, N[1].z), u)),
+                    scale(mk(N[2].x, N[2].y, N[2].z), v));
+        }
+        acc = add(acc, shade_hw1(o, d, hit, p, n, P.lpos, P.lcol));
+        if (valid && P.hit_idx) {
+            const size_t kk = ((size_t)y * P.W + x) * (size_t)P.spp + (size_t)s;
+            P.hit_idx[kk] = besti;
+            P.hit_t[kk] = hit ? best : -1.0f;
+        }
+    }
+    if (valid) {
+        const float fs = (float)P.spp;
+        float* o = P.rgb + ((size_t)y * P.W + x) * 3;
+        o[0] = acc.x / fs;
+        o[1] = acc.y / fs;
+        o[2] = acc.z / fs;
+    }
+}
+
+}  // namespace
+
+// =========================================================================================
+// Host side
+// =========================================================================================
+using rt::set_error;
+
+namespace {
+
+std::string hip_msg(hipError_t e, const char* what) {
+    return std::string(what) + ": " + hipGetErrorString(e);
+}
+#define HIP_TRY(expr)                                                          \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) return set_error(RT_ERR_HIP, hip_msg(e_, #expr)); \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    int alloc(size_t bytes) {
+        if (p) { (void)hipFree(p); p = nullptr; }
+        n = bytes;
+        if (bytes == 0) return RT_OK;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) { p = nullptr; return set_error(RT_ERR_HIP, hip_msg(e, "hipMalloc")); }
+        return RT_OK;
+    }
+    int upload(const void* src, size_t bytes) {
+        int rc = alloc(bytes);
+        if (rc != RT_OK || bytes == 0) return rc;
+        hipError_t e = hipMemcpy(p, src, bytes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return set_error(RT_ERR_HIP, hip_msg(e, "hipMemcpy H2D"));
+        return RT_OK;
+    }
+};
+
+int check_device(int device) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return set_error(RT_ERR_NODEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) return set_error(RT_ERR_ARG, "device index out of range");
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) return set_error(RT_ERR_HIP, hip_msg(e, "hipGetDeviceProperties"));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_error(RT_ERR_NODEVICE, std::string("kernels are built for gfx950, device is ") + prop.gcnArchName);
+    return RT_OK;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(d);
+    }
+    ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+}  // namespace
+
+struct rt_scene {
+    int device = 0;
+    size_t P = 0;
+    int nmat = 0, nlights = 0;
+    uint32_t root_ref = 0;
+    float root_box[6] = {0, 0, 0, 0, 0, 0};
+    DevBuf inode, ibox, leaf, tnorm, objids, mats, lights, jitter;
+    int jitter_spp = -1;
+    std::vector<float> jitter_host;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    bool timed = false;
+    size_t bytes = 0;
+    ~rt_scene() {
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+};
+
+extern "C" int rt_device_count(int* n) {
+    if (!n) return set_error(RT_ERR_ARG, "null");
+    *n = 0;
+    hipError_t e = hipGetDeviceCount(n);
+    if (e != hipSuccess) { *n = 0; return set_error(RT_ERR_NODEVICE, hip_msg(e, "hipGetDeviceCount")); }
+    return RT_OK;
+}
+
+extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, const rt_aabb* aabbs,
+                               const rt_triangle* tris, const int32_t* objids, const rt_material* mats,
+                               int nmat, const rt_light* lights, int nlights, rt_scene** out) {
+    if (!out) return set_error(RT_ERR_ARG, "rt_scene_create: null out");
+    *out = nullptr;
+    if (P == 0 || !nodes || !aabbs || !tris) return set_error(RT_ERR_ARG, "rt_scene_create: empty scene");
+    if (P > 0x3FFFFFFFull) return set_error(RT_ERR_UNSUPPORTED, "more than 2^30 triangles");
+    if (nmat < 0 || nlights < 0 || (nmat > 0 && !mats) || (nlights > 0 && !lights))
+        return set_error(RT_ERR_ARG, "rt_scene_create: bad material/light arrays");
+    const size_t NN = 2 * P - 1;
+    // Classify nodes, give internal/leaf nodes compact ids, and check the reachable graph
+    // is a finite tree whose DFS fits the 64-entry wave stack (SearchBVH's push/pop order).
+    std::vector<uint32_t> cid(NN, NO_REF);
+    size_t n_int = 0, n_leaf = 0;
+    for (size_t n = 0; n < NN; ++n) {
+        const rt_bvh_node& nd = nodes[n];
+        if (nd.object_idx == 0xFFFFFFFFu) {
+            if ((nd.left_idx != NO_REF && nd.left_idx >= NN) || (nd.right_idx != NO_REF && nd.right_idx >= NN))
+                return set_error(RT_ERR_ARG, "BVH child index out of range");
+            cid[n] = uint32_t(n_int++);
+        } else if (nd.object_idx < P) {
+            cid[n] = LEAF_BIT | uint32_t(n_leaf++);
+        }  // leaves naming no valid triangle are skipped by SearchBVH (query.h:263): NO_REF
+    }
+    {
+        std::vector<uint8_t> state(NN, 0);  // 0 new, 1 on path, 2 done
+        std::vector<int> S(NN, 0);
+        std::vector<std::pair<uint32_t, bool>> st{{0u, false}};
+        while (!st.empty()) {
+            auto [v, post] = st.back();
+            st.pop_back();
+            const rt_bvh_node& nd = nodes[v];
+            const bool internal = nd.object_idx == 0xFFFFFFFFu;
+            if (!post) {
+                if (state[v] == 1) return set_error(RT_ERR_ARG, "BVH contains a cycle");
+                if (state[v] == 2) continue;
+                state[v] = 1;
+                st.push_back({v, true});
+                if (internal) {
+                    if (nd.left_idx != NO_REF) st.push_back({nd.left_idx, false});
+                    if (nd.right_idx != NO_REF) st.push_back({nd.right_idx, false});
+                }
+            } else {
+                state[v] = 2;
+                if (internal) {
+                    const int sl = nd.left_idx != NO_REF ? S[nd.left_idx] : 0;
+                    const int sr = nd.right_idx != NO_REF ? S[nd.right_idx] : 0;
+                    const int pushes = (nd.left_idx != NO_REF) + (nd.right_idx != NO_REF);
+                    int s = pushes;
+                    if (nd.right_idx != NO_REF) s = std::max(s, (nd.left_idx != NO_REF ? 1 : 0) + sr);
+                    if (nd.left_idx != NO_REF) s = std::max(s, sl);
+                    S[v] = s;
+                }
+            }
+        }
+        if (std::max(1, S[0]) > STACK_CAP)
+            return set_error(RT_ERR_UNSUPPORTED, "BVH needs a DFS stack deeper than 64 entries");
+    }
+    std::vector<float4> hin(4 * std::max<size_t>(n_int, 1)), hib(2 * std::max<size_t>(n_int, 1));
+    std::vector<float4> hlf(4 * std::max<size_t>(n_leaf, 1)), hnm(3 * P);
+    auto ref_of = [&](uint32_t n) -> uint32_t { return n == NO_REF ? NO_REF : cid[n]; };
+    for (size_t n = 0; n < NN; ++n) {
+        const uint32_t c = cid[n];
+        if (c == NO_REF) continue;
+        const rt_bvh_node& nd = nodes[n];
+        if (!(c & LEAF_BIT)) {
+            const rt_aabb lb = nd.left_idx != NO_REF ? aabbs[nd.left_idx] : rt_aabb{};
+            const rt_aabb rb = nd.right_idx != NO_REF ? aabbs[nd.right_idx] : rt_aabb{};
+            float4* q = &hin[4 * c];
+            q[0] = make_float4(lb.min_corner.x, lb.min_corner.y, lb.min_corner.z, lb.max_corner.x);
+            q[1] = make_float4(lb.max_corner.y, lb.max_corner.z, rb.min_corner.x, rb.min_corner.y);
+            q[2] = make_float4(rb.min_corner.z, rb.max_corner.x, rb.max_corner.y, rb.max_corner.z);
+            uint32_t refs[4] = {ref_of(nd.left_idx), ref_of(nd.right_idx), 0u, 0u};
+            std::memcpy(&q[3], refs, 16);
+            const rt_aabb& ob = aabbs[n];
+            hib[2 * c] = make_float4(ob.min_corner.x, ob.min_corner.y, ob.min_corner.z, 0.f);
+            hib[2 * c + 1] = make_float4(ob.max_corner.x, ob.max_corner.y, ob.max_corner.z, 0.f);
+        } else {
+            const uint32_t j = c & ~LEAF_BIT;
+            const rt_triangle& t = tris[nd.object_idx];
+            const rt_aabb& ob = aabbs[n];
+            float4* q = &hlf[4 * j];
+            int32_t ti = int32_t(nd.object_idx);
+            float tif;
+            std::memcpy(&tif, &ti, 4);
+            // e1 = v1 - v0, e2 = v2 - v0 exactly as intersectTriangle computes them
+            q[0] = make_float4(t.v0.x, t.v0.y, t.v0.z, tif);
+            q[1] = make_float4(t.v1.x - t.v0.x, t.v1.y - t.v0.y, t.v1.z - t.v0.z, ob.min_corner.x);
+            q[2] = make_float4(t.v2.x - t.v0.x, t.v2.y - t.v0.y, t.v2.z - t.v0.z, ob.min_corner.y);
+            q[3] = make_float4(ob.min_corner.z, ob.max_corner.x, ob.max_corner.y, ob.max_corner.z);
+        }
+    }
+    for (size_t t = 0; t < P; ++t) {
+        hnm[3 * t] = make_float4(tris[t].n0.x, tris[t].n0.y, tris[t].n0.z, 0.f);
+        hnm[3 * t + 1] = make_float4(tris[t].n1.x, tris[t].n1.y, tris[t].n1.z, 0.f);
+        hnm[3 * t + 2] = make_float4(tris[t].n2.x, tris[t].n2.y, tris[t].n2.z, 0.f);
+    }
+    int rc = check_device(device);
+    if (rc != RT_OK) return rc;
+    DeviceGuard g(device);
+    std::unique_ptr<rt_scene> s(new (std::nothrow) rt_scene());
+    if (!s) return set_error(RT_ERR_NOMEM, "out of memory");
+    s->device = device;
+    s->P = P;
+    s->nmat = nmat;
+    s->nlights = nlights;
+    s->root_ref = cid[0];
+    if (s->root_ref == NO_REF) s->root_ref = LEAF_BIT | 0u;  // degenerate: unreachable leaf
+    s->root_box[0] = aabbs[0].min_corner.x; s->root_box[1] = aabbs[0].min_corner.y; s->root_box[2] = aabbs[0].min_corner.z;
+    s->root_box[3] = aabbs[0].max_corner.x; s->root_box[4] = aabbs[0].max_corner.y; s->root_box[5] = aabbs[0].max_corner.z;
+    if (cid[0] == NO_REF) {  // root names no triangle: nothing can be hit; empty box
+        s->root_box[0] = s->root_box[1] = s->root_box[2] = INFINITY;
+        s->root_box[3] = s->root_box[4] = s->root_box[5] = -INFINITY;
+    }
+    if ((rc = s->inode.upload(hin.data(), hin.size() * sizeof(float4))) != RT_OK) return rc;
+    if ((rc = s->ibox.upload(hib.data(), hib.size() * sizeof(float4))) != RT_OK) return rc;
+    if ((rc = s->leaf.upload(hlf.data(), hlf.size() * sizeof(float4))) != RT_OK) return rc;
+    if ((rc = s->tnorm.upload(hnm.data(), hnm.size() * sizeof(float4))) != RT_OK) return rc;
+    if (objids && (rc = s->objids.upload(objids, P * sizeof(int32_t))) != RT_OK) return rc;
+    if (nmat > 0 && (rc = s->mats.upload(mats, size_t(nmat) * sizeof(rt_material))) != RT_OK) return rc;
+    if (nlights > 0 && (rc = s->lights.upload(lights, size_t(nlights) * sizeof(rt_light))) != RT_OK) return rc;
+    for (auto& e : s->ev) HIP_TRY(hipEventCreate(&e));
+    s->bytes = s->inode.n + s->ibox.n + s->leaf.n + s->tnorm.n + s->objids.n + s->mats.n + s->lights.n;
+    *out = s.release();
+    return RT_OK;
+}
+
+extern "C" void rt_scene_destroy(rt_scene* s) {
+    if (!s) return;
+    DeviceGuard g(s->device);
+    delete s;
+}
+extern "C" int rt_scene_device(const rt_scene* s) { return s ? s->device : -1; }
+extern "C" size_t rt_scene_device_bytes(const rt_scene* s) { return s ? s->bytes : 0; }
+
+extern "C" void rt_render_opts_default(rt_render_opts* o) {
+    o->max_depth = 1;
+    o->spp = 1;
+    o->diffuse_bounce = 1;
+    o->miss_color = rt_vec3{0.f, 0.f, 0.f};
+    o->jitter = nullptr;
+    o->band_rows = 8;
+    o->band_index = 0;
+    o->band_count = 1;
+    o->kernel = RT_KERNEL_AUTO;
+}
+
+extern "C" int rt_shard_rows(int H, int band_rows, int band_index, int band_count) {
+    if (H <= 0) return 0;
+    if (band_count <= 1) return H;
+    if (band_rows <= 0 || band_index < 0 || band_index >= band_count) return -1;
+    const int nbands = (H + band_rows - 1) / band_rows;
+    int rows = 0;
+    for (int b = band_index; b < nbands; b += band_count) rows += std::min(band_rows, H - b * band_rows);
+    return rows;
+}
+
+namespace {
+
+int prepare_jitter(rt_scene* s, const rt_render_opts* o) {
+    std::vector<float> tab(2 * size_t(o->spp));
+    if (o->jitter) std::memcpy(tab.data(), o->jitter, tab.size() * sizeof(float));
+    else {
+        int rc = rt_jittered_samples(o->spp, 42u, 1, tab.data());
+        if (rc != RT_OK) return rc;
+    }
+    if (s->jitter_spp == o->spp && s->jitter_host == tab) return RT_OK;
+    int rc = s->jitter.upload(tab.data(), tab.size() * sizeof(float));
+    if (rc != RT_OK) return rc;
+    s->jitter_host = tab;
+    s->jitter_spp = o->spp;
+    return RT_OK;
+}
+
+template <int MODE>
+void launch(const RenderParams& P, int blocks, bool samples, hipStream_t st) {
+    if (samples) hipLaunchKernelGGL(render_samples_kernel<MODE>, dim3(blocks), dim3(BLOCK), 0, st, P);
+    else hipLaunchKernelGGL(render_pixels_kernel<MODE>, dim3(blocks), dim3(BLOCK), 0, st, P);
+}
+
+}  // namespace
+
+extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, float* rgb,
+                                int32_t* hit_idx, float* hit_t, void* stream) {
+    if (!s || !cam || !o || !rgb) return set_error(RT_ERR_ARG, "rt_render_device: null argument");
+    if (o->spp < 1) return set_error(RT_ERR_ARG, "spp must be >= 1");
+    if ((hit_idx == nullptr) != (hit_t == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
+    const int W = cam->pixel_width, H = cam->pixel_height;
+    if (W < 1 || H < 1) return set_error(RT_ERR_ARG, "camera has no pixels");
+    const int rows = rt_shard_rows(H, o->band_rows, o->band_index, o->band_count);
+    if (rows < 0) return set_error(RT_ERR_ARG, "bad band sharding parameters");
+    DeviceGuard g(s->device);
+    int rc = prepare_jitter(s, o);
+    if (rc != RT_OK) return rc;
+    if (rows == 0) return RT_OK;
+
+    RenderParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.sc.inode = static_cast<const float4*>(s->inode.p);
+    P.sc.ibox = static_cast<const float4*>(s->ibox.p);
+    P.sc.leaf = static_cast<const float4*>(s->leaf.p);
+    P.sc.tnorm = static_cast<const float4*>(s->tnorm.p);
+    P.sc.objids = static_cast<const int32_t*>(s->objids.p);
+    P.sc.mats = static_cast<const DevMaterial*>(s->mats.p);
+    P.sc.lights = static_cast<const DevLight*>(s->lights.p);
+    P.sc.num_tris = int32_t(s->P);
+    P.sc.num_mats = s->nmat;
+    P.sc.num_lights = s->nlights;
+    P.sc.root_ref = s->root_ref;
+    std::memcpy(P.sc.root_box, s->root_box, sizeof(P.sc.root_box));
+    P.cam_center = f3{cam->center.x, cam->center.y, cam->center.z};
+    P.cam_p00 = f3{cam->pixel00_loc.x, cam->pixel00_loc.y, cam->pixel00_loc.z};
+    P.cam_du = f3{cam->pixel_delta_u.x, cam->pixel_delta_u.y, cam->pixel_delta_u.z};
+    P.cam_dv = f3{cam->pixel_delta_v.x, cam->pixel_delta_v.y, cam->pixel_delta_v.z};
+    P.W = W;
+    P.H = H;
+    P.spp = o->spp;
+    P.max_depth = o->max_depth;
+    P.diffuse_bounce = o->diffuse_bounce ? 1 : 0;
+    P.miss = f3{o->miss_color.x, o->miss_color.y, o->miss_color.z};
+    P.jitter = static_cast<const float*>(s->jitter.p);
+    P.band_rows = o->band_count <= 1 ? H : o->band_rows;
+    P.band_index = o->band_count <= 1 ? 0 : o->band_index;
+    P.band_count = o->band_count <= 1 ? 1 : o->band_count;
+    P.rows = rows;
+    P.rgb = rgb;
+    P.hit_idx = hit_idx;
+    P.hit_t = hit_t;
+    const bool samples = o->spp <= BLOCK && (o->spp & (o->spp - 1)) == 0;
+    int ppb = samples ? BLOCK / o->spp : BLOCK;  // pixels per block
+    int tw = 1;
+    while (tw * tw < ppb) tw <<= 1;                // square-ish power-of-two tile
+    int th = ppb / tw;
+    P.tile_w = tw;
+    P.tile_h = th;
+    P.tiles_x = (W + tw - 1) / tw;
+    const int tiles_y = (rows + th - 1) / th;
+    P.tiles_total = P.tiles_x * tiles_y;
+    P.lane_samples = samples ? 1 : 0;
+    const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipEventRecord(s->ev[0], st));
+    if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, P.tiles_total, samples, st);
+    else launch<RT_KERNEL_WAVE>(P, P.tiles_total, samples, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(s->ev[1], st));
+    s->timed = true;
+    return RT_OK;
+}
+
+extern "C" int rt_last_timing(const rt_scene* s, float* total_ms, float* kernel_ms) {
+    if (!s || !s->timed) return set_error(RT_ERR_ARG, "no timed render on this scene");
+    DeviceGuard g(s->device);
+    HIP_TRY(hipEventSynchronize(s->ev[1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, s->ev[0], s->ev[1]));
+    if (total_ms) *total_ms = ms;
+    if (kernel_ms) *kernel_ms = ms;
+    return RT_OK;
+}
+
+extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, float* rgb_host,
+                         int32_t* hit_idx_host, float* hit_t_host) {
+    if (!s || !cam || !o || !rgb_host) return set_error(RT_ERR_ARG, "rt_render: null argument");
+    if ((hit_idx_host == nullptr) != (hit_t_host == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
+    const int rows = rt_shard_rows(cam->pixel_height, o->band_rows, o->band_index, o->band_count);
+    if (rows < 0) return set_error(RT_ERR_ARG, "bad band sharding parameters");
+    if (o->spp < 1) return set_error(RT_ERR_ARG, "spp must be >= 1");
+    DeviceGuard g(s->device);
+    const size_t npx = size_t(rows) * size_t(std::max(cam->pixel_width, 0));
+    DevBuf rgb, hi, ht;
+    int rc;
+    if ((rc = rgb.alloc(npx * 3 * sizeof(float))) != RT_OK) return rc;
+    if (hit_idx_host) {
+        if ((rc = hi.alloc(npx * size_t(o->spp) * sizeof(int32_t))) != RT_OK) return rc;
+        if ((rc = ht.alloc(npx * size_t(o->spp) * sizeof(float))) != RT_OK) return rc;
+    }
+    rc = rt_render_device(s, cam, o, static_cast<float*>(rgb.p), static_cast<int32_t*>(hi.p),
+                          static_cast<float*>(ht.p), nullptr);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    if (npx) HIP_TRY(hipMemcpy(rgb_host, rgb.p, npx * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    if (hit_idx_host && npx) {
+        HIP_TRY(hipMemcpy(hit_idx_host, hi.p, npx * size_t(o->spp) * sizeof(int32_t), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(hit_t_host, ht.p, npx * size_t(o->spp) * sizeof(float), hipMemcpyDeviceToHost));
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_render_reference(size_t P, int W, int H, const rt_camera* cam, rt_vec3 miss, int max_depth,
+                                   int spp, const rt_bvh_node* nodes, const rt_aabb* aabbs,
+                                   const rt_triangle* tris, const int32_t* objids, const rt_material* mats,
+                                   int nmat, const rt_light* lights, int nlights, int diffuse_bounce,
+                                   rt_vec3* output) {
+    // query.cu:131-133: a null scene/output array is a silent no-op in the reference CPU
+    // branch; here it is reported.
+    if (!cam || !output) return set_error(RT_ERR_ARG, "rt_render_reference: null argument");
+    if (W != cam->pixel_width || H != cam->pixel_height)
+        return set_error(RT_ERR_ARG, "W/H must match the camera's pixel dimensions");
+    rt_scene* s = nullptr;
+    int rc = rt_scene_create(0, P, nodes, aabbs, tris, objids, mats, nmat, lights, nlights, &s);
+    if (rc != RT_OK) return rc;
+    rt_render_opts o;
+    rt_render_opts_default(&o);
+    o.max_depth = max_depth;
+    o.spp = spp;
+    o.diffuse_bounce = diffuse_bounce;
+    o.miss_color = miss;
+    rc = rt_render(s, cam, &o, reinterpret_cast<float*>(output), nullptr, nullptr);
+    rt_scene_destroy(s);
+    return rc;
+}
+
+extern "C" int rt_render_hw1(int device, const rt_vec3* pos, const rt_vec3* nrm, const uint32_t* idx, size_t P,
+                             const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp, const float* jitter,
+                             float* rgb_host, int32_t* hit_idx_host, float* hit_t_host) {
+    if (!pos || !nrm || !idx || !cam || !rgb_host || spp < 1 || P == 0)
+        return set_error(RT_ERR_ARG, "rt_render_hw1: bad argument (HW1 requires per-vertex normals)");
+    if (P > 0x7FFFFFFFull) return set_error(RT_ERR_UNSUPPORTED, "too many triangles");
+    if ((hit_idx_host == nullptr) != (hit_t_host == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
+    int rc = check_device(device);
+    if (rc != RT_OK) return rc;
+    DeviceGuard g(device);
+    const int W = cam->pixel_width, H = cam->pixel_height;
+    std::vector<float4> ht(3 * P), hn(3 * P);
+    size_t nv = 0;
+    for (size_t k = 0; k < 3 * P; ++k) nv = std::max<size_t>(nv, size_t(idx[k]) + 1);
+    for (size_t k = 0; k < P; ++k) {
+        const rt_vec3 a = pos[idx[3 * k]], b = pos[idx[3 * k + 1]], c = pos[idx[3 * k + 2]];
+        ht[3 * k] = make_float4(a.x, a.y, a.z, 0.f);
+        ht[3 * k + 1] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, 0.f);
+        ht[3 * k + 2] = make_float4(c.x - a.x, c.y - a.y, c.z - a.z, 0.f);
+        for (int j = 0; j < 3; ++j) {
+            const rt_vec3 n = nrm[idx[3 * k + j]];
+            hn[3 * k + j] = make_float4(n.x, n.y, n.z, 0.f);
+        }
+    }
+    std::vector<float> tab(2 * size_t(spp));
+    if (jitter) std::memcpy(tab.data(), jitter, tab.size() * sizeof(float));
+    else if ((rc = rt_jittered_samples(spp, 42u, 0, tab.data())) != RT_OK) return rc;
+    DevBuf dt, dn, dj, drgb, dhi, dht;
+    if ((rc = dt.upload(ht.data(), ht.size() * sizeof(float4))) != RT_OK) return rc;
+    if ((rc = dn.upload(hn.data(), hn.size() * sizeof(float4))) != RT_OK) return rc;
+    if ((rc = dj.upload(tab.data(), tab.size() * sizeof(float))) != RT_OK) return rc;
+    const size_t npx = size_t(W) * size_t(H);
+    if ((rc = drgb.alloc(npx * 3 * sizeof(float))) != RT_OK) return rc;
+    if (hit_idx_host) {
+        if ((rc = dhi.alloc(npx * size_t(spp) * sizeof(int32_t))) != RT_OK) return rc;
+        if ((rc = dht.alloc(npx * size_t(spp) * sizeof(float))) != RT_OK) return rc;
+    }
+    Hw1Params hp;
+    hp.tri = static_cast<const float4*>(dt.p);
+    hp.nrm = static_cast<const float4*>(dn.p);
+    hp.num_tris = int32_t(P);
+    hp.center = f3{cam->center.x, cam->center.y, cam->center.z};
+    hp.p00 = f3{cam->pixel00_loc.x, cam->pixel00_loc.y, cam->pixel00_loc.z};
+    hp.du = f3{cam->pixel_delta_u.x, cam->pixel_delta_u.y, cam->pixel_delta_u.z};
+    hp.dv = f3{cam->pixel_delta_v.x, cam->pixel_delta_v.y, cam->pixel_delta_v.z};
+    hp.W = W;
+    hp.H = H;
+    hp.spp = spp;
+    hp.lpos = f3{lpos.x, lpos.y, lpos.z};
+    hp.lcol = f3{lcol.x, lcol.y, lcol.z};
+    hp.jitter = static_cast<const float*>(dj.p);
+    hp.rgb = static_cast<float*>(drgb.p);
+    hp.hit_idx = static_cast<int32_t*>(dhi.p);
+    hp.hit_t = static_cast<float*>(dht.p);
+    const int blocks = ((W + 15) / 16) * ((H + 15) / 16);
+    hipLaunchKernelGGL(render_hw1_kernel, dim3(blocks), dim3(BLOCK), 0, nullptr, hp);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(rgb_host, drgb.p, npx * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    if (hit_idx_host) {
+        HIP_TRY(hipMemcpy(hit_idx_host, dhi.p, npx * size_t(spp) * sizeof(int32_t), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(hit_t_host, dht.p, npx * size_t(spp) * sizeof(float), hipMemcpyDeviceToHost));
+    }
+    (void)nv;
+    return RT_OK;
+}

@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s (camera samples/s) of the per-pixel ray path at
+1920x1080x16 spp on the frog scene (BASELINE.json configs[2]; c4 when N > 1).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c5] [--kernel wave|lane]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N ...
+
+A step = one full frame: every rank renders its image bands (rows cut into 8-row bands,
+band b -> rank b % N) with the HIP kernel into device memory, then the strips are gathered
+to rank 0 over RCCL (torch.distributed, backend "nccl").  Scene upload and BVH build are
+outside the timed region (as G/src/main.cu:362-378 times only render()).  Inputs are
+resident in HBM when timing starts.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import gzip
+import json
+import os
+import platform
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (import before librt_mi355x: one HIP runtime in the process)
+import torch.distributed as dist  # noqa: E402
+
+import raytracinginonesemester_amd as rt  # noqa: E402
+from raytracinginonesemester_amd import configs  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+BAND_ROWS = 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(configs.G_CONFIGS))
+    ap.add_argument("--kernel", default="auto", choices=["auto", "wave", "lane"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--traffic-file", default=str(REPO / "profiles" / "traffic.json"),
+                    help="per-launch HBM bytes measured by rocprofv3 --pmc (see DESIGN.md)")
+    return ap.parse_args()
+
+
+def cpu_baseline(hs, cam, cfg) -> dict:
+    """The oracle restatement (bit-exact to the reference build, tests/test_oracle.py) timed on
+    this host's cores over the full frame, plus the reference's own CPU render() built from its
+    sources (oracle/_ref/ref_g, 1 thread, as shipped) when present."""
+    from oracle import pyoracle as orc
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    b = cam.basis()
+    oc = orc.camera_from_basis(b["center"], b["pixel00_loc"], b["pixel_delta_u"], b["pixel_delta_v"],
+                               cam.pixel_width, cam.pixel_height)
+    # bounded sample: a band of rows through the frame centre (the frog), then all rows for c3
+    H, W, spp = cam.pixel_height, cam.pixel_width, cfg["spp"]
+    rows = (0, H) if cfg is configs.G_CONFIGS["c3"] else (H // 2 - 32, H // 2 + 32)
+    t0 = time.perf_counter()
+    orc.render_g(hs.num_triangles, oc, hs.nodes, hs.aabbs, hs.triangles, hs.tri_object_ids, hs.materials,
+                 hs.lights, spp=spp, max_depth=cfg["max_depth"], miss=hs.settings["miss_color"], rows=rows,
+                 threads=threads)
+    dt = time.perf_counter() - t0
+    n = (rows[1] - rows[0]) * W * spp
+    out = {"value": n / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/rt_oracle.c (bit-exact restatement) rows {rows[0]}..{rows[1]} of "
+                     f"{W}x{H}x{spp}, {n} samples, {dt:.2f} s, OpenMP {threads} threads"}
+    ref = REPO / "oracle" / "_ref" / "ref_g"
+    if ref.exists() and cfg is configs.G_CONFIGS["c3"]:
+        with tempfile.TemporaryDirectory() as td:
+            r = subprocess.run([str(ref), "scene", str(configs.SCENES / cfg["scene"]), str(REPO), td, str(W), str(H),
+                                str(spp), str(cfg["max_depth"]), "-1", "0"], capture_output=True, text=True,
+                               timeout=600)
+            if r.returncode == 0:
+                ms = json.loads((Path(td) / "meta.json").read_text())["render_ms"]
+                out["reference_as_shipped"] = {
+                    "value": W * H * spp / (ms / 1e3) / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "reference",
+                    "sample": "G/ render() CPU branch built from /root/reference sources (oracle/_ref/ref_g), "
+                              f"full frame, per-pixel jitter rebuild as shipped, {ms / 1e3:.2f} s"}
+    out["host_cpu"] = platform.processor() or platform.machine()
+    return out
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = configs.G_CONFIGS[a.config]
+    sp = configs.scene_path(cfg["scene"])
+    hs = rt.HostScene.load_json(sp, REPO if sp.parent == configs.SCENES else sp.parent)
+    cam = hs.camera(cfg["width"], cfg["height"])
+    W, H, spp = cam.pixel_width, cam.pixel_height, cfg["spp"]
+    kernel = {"auto": rt.RT_KERNEL_AUTO, "wave": rt.RT_KERNEL_WAVE, "lane": rt.RT_KERNEL_LANE}[a.kernel]
+    ds = rt.DeviceScene.from_host(hs, device=local)
+    opts, _jit = ds.make_opts(spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
+                              band_rows=BAND_ROWS, band_index=rank, band_count=world, kernel=kernel)
+    lib = rt._lib.lib()
+    rows_of = [lib.rt_shard_rows(H, BAND_ROWS, r, world) for r in range(world)]
+    max_rows = max(rows_of)
+    strip = torch.zeros((max_rows, W, 3), dtype=torch.float32, device=dev)
+    gather = [torch.empty_like(strip) for _ in range(world)] if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        ds.render_device(cam, opts, strip.data_ptr(), stream=stream)
+        if world > 1:
+            dist.gather(strip, gather_list=gather, dst=0)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    kt = ds.kernel_times(a.steps)
+    kmean = torch.tensor([float(kt.mean()) if len(kt) else float("nan")], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(kmean, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    kernel_ms = float(kmean.item())
+
+    # assemble the frame on rank 0 (band un-permute) for the parity check
+    frame = None
+    if rank == 0:
+        parts = gather if world > 1 else [strip]
+        frame = np.zeros((H, W, 3), np.float32)
+        for r in range(world):
+            ys = [y for y in range(H) if (y // BAND_ROWS) % world == r] if world > 1 else list(range(H))
+            frame[ys] = parts[r][:len(ys)].cpu().numpy()
+
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank != 0:
+        return
+
+    samples = W * H * spp
+    value = samples * a.steps / elapsed / 1e6
+    B = configs.BYTES_PER_SAMPLE[a.config]
+    per_gpu_samples = samples / world
+    achieved = B * per_gpu_samples / (kernel_ms / 1e3) / 1e9  # GB/s of the dominant kernel
+    traffic = None
+    tf = Path(a.traffic_file)
+    if tf.exists():
+        try:
+            traffic = json.loads(tf.read_text()).get(a.config, {}).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    line = {
+        "metric": "Mrays/s at 1920x1080x16spp (1/2/4/8 GPU) + PPM max-abs pixel diff",
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32+f64",
+        "data": "synthetic=false: frog.obj scene (reference asset), camera/light from frog.json"
+                if a.config == "c3" else "synthetic seeded 1,048,576-triangle heightfield",
+        "config": {"workload": f"{a.config}: {cfg['scene']} {W}x{H}x{spp}spp max_bounces={cfg['max_depth']}, "
+                               f"Lambert/Blinn-Phong + 1 hard shadow ray per light",
+                   "triangles": hs.num_triangles, "bands": f"{BAND_ROWS}-row bands round-robin over {world} GPU(s)",
+                   "gather": "RCCL gather to rank 0" if world > 1 else None,
+                   "kernel": a.kernel},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_sample": round(B, 3)},
+    }
+    if not a.no_parity and a.config == "c3":
+        ref = np.frombuffer(gzip.open(REPO / "tests" / "golden" / "scenes" / "c3_full" / "fb.f32.gz").read(),
+                            np.float32).reshape(H, W, 3)
+        ppm_ref = gzip.open(REPO / "tests" / "golden" / "scenes" / "c3_full" / "image.ppm.gz").read()
+        mine = rt.encode_p6(frame)
+        pd = np.abs(np.frombuffer(mine[17:], np.uint8).astype(int) - np.frombuffer(ppm_ref[17:], np.uint8).astype(int))
+        line["parity"] = {"vs": "reference CPU render() output (tests/golden/scenes/c3_full)",
+                          "rgb_maxabs": float(np.abs(frame - ref).max()),
+                          "rgb_bitexact_frac": float((frame.view(np.uint32) == ref.view(np.uint32)).mean()),
+                          "ppm_maxabs": int(pd.max())}
+    if world == 1 and not a.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(hs, cam, cfg)
+        line["speedup_vs_cpu_baseline"] = round(value / line["cpu_baseline"]["value"], 2)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

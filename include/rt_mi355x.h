@@ -202,9 +202,18 @@ int rt_render_hw1(int device, const rt_vec3* positions, const rt_vec3* normals,
                   rt_vec3 light_position, rt_vec3 light_color, int spp, const float* jitter,
                   float* rgb_host, int32_t* hit_idx_host, float* hit_t_host);
 
-/* Timing of the last rt_render_device launch sequence on this scene, measured with HIP
- * events on the stream the kernels ran on: total ms and the main kernel's ms. */
-int rt_last_timing(const rt_scene* s, float* total_ms, float* kernel_ms);
+/* Batched ray-triangle queries on the GPU (one triangle, n rays from `origin`), the device
+ * Möller–Trumbore used by the kernels:  hw1 != 0 -> HW1 ray_intersection
+ * (HW1/include/ray.h:67-117; the HW1 Ray constructor normalises each direction first, ray.h:25),
+ * hw1 == 0 -> G/ intersectTriangle (G/include/query.h:72-108) over [tmin, tmax] with the
+ * direction used as given.  Host arrays; hit[i] in {0,1}, t[i] = -1 on a miss. */
+int rt_intersect_rays(int device, const rt_triangle* tri, const float origin[3], const float* dirs, int n,
+                      int hw1, float tmin, float tmax, int32_t* hit, float* t);
+
+/* Durations (ms) of the render kernel of the most recent min(max, launches, 256)
+ * rt_render_device calls on this scene, oldest first, measured with HIP events recorded
+ * on the launch stream around the kernel.  Waits for those launches to finish. */
+int rt_kernel_times(const rt_scene* s, float* ms_out, int max, int* n_out);
 
 int rt_device_count(int* n);
 const char* rt_last_error(void);

@@ -6,5 +6,5 @@ include/rt_mi355x.h); this package is the host-side mirror of the reference inte
 from ._lib import RTError, RT_KERNEL_AUTO, RT_KERNEL_LANE, RT_KERNEL_WAVE  # noqa: F401
 from .api import (  # noqa: F401
     LIGHT_DTYPE, Camera, DeviceScene, HostScene, MeshHW1, build_bvh, default_material, device_count,
-    encode_p6, jittered_samples, read_p6, render, render_hw1, write_p6,
+    encode_p6, intersect_rays, jittered_samples, read_p6, render, render_hw1, write_p6,
 )

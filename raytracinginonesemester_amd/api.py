@@ -254,10 +254,12 @@ class DeviceScene:
         check(lib().rt_render_device(self._h, C.byref(camera.c), C.byref(opts), rgb_dev_ptr, hit_idx_ptr,
                                      hit_t_ptr, stream))
 
-    def last_timing(self):
-        tot, ker = C.c_float(), C.c_float()
-        check(lib().rt_last_timing(self._h, C.byref(tot), C.byref(ker)))
-        return tot.value, ker.value
+    def kernel_times(self, max_launches: int = 256) -> np.ndarray:
+        """ms of the render kernel for the most recent launches (HIP events on its stream)."""
+        out = np.zeros(max_launches, np.float32)
+        n = C.c_int()
+        check(lib().rt_kernel_times(self._h, ptr(out), max_launches, C.byref(n)))
+        return out[:n.value]
 
     def close(self) -> None:
         if self._h:
@@ -304,6 +306,20 @@ def render_hw1(positions, normals, indices, camera: Camera, light_position, ligh
                               _v3(light_position), _v3(light_color), int(spp), ptr(jit), ptr(rgb), ptr(hi),
                               ptr(ht)))
     return (rgb, hi, ht) if aov else rgb
+
+
+def intersect_rays(triangle18, dirs, origin=(0.0, 0.0, 0.0), hw1: bool = True, tmin: float = 0.0,
+                   tmax: float = 3.4028234663852886e38, device: int = 0):
+    """Device Möller–Trumbore over a batch of rays against one triangle (v0,v1,v2,n0,n1,n2 as 18
+    floats): HW1 ray_intersection semantics when hw1, else G/ intersectTriangle with [tmin, tmax]."""
+    tri = L.Triangle.from_buffer_copy(_c(triangle18, np.float32).tobytes())
+    d = _c(dirs, np.float32).reshape(-1, 3)
+    n = d.shape[0]
+    hit = np.zeros(n, np.int32)
+    t = np.zeros(n, np.float32)
+    check(lib().rt_intersect_rays(int(device), C.byref(tri), _f3(origin), ptr(d), n, 1 if hw1 else 0,
+                                  float(tmin), float(tmax), ptr(hit), ptr(t)))
+    return hit, t
 
 
 def build_bvh(positions, indices):

@@ -49,7 +49,10 @@ def build(force: bool = False) -> Path:
         _run([CXX, "-std=c++17", "-O2", "-fPIC", *FP, "-Wall", "-Wextra", *inc, "-c",
               CSRC / "rt_host.cpp", "-o", host_o])
     if force or _stale(dev_o, [CSRC / "rt_device.hip", *hdrs]):
+        # code object v5: loadable by both the image's ROCm 7.2 runtime and the ROCm 7.0 HIP
+        # runtime bundled with torch (which the process uses when torch is imported first)
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP, "-Wall",
+              "-mcode-object-version=5",
               "-Wno-unused-function", *inc, "-c", CSRC / "rt_device.hip", "-o", dev_o])
     if force or _stale(so, [host_o, dev_o]):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", host_o, dev_o, "-o", so])

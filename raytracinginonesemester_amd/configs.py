@@ -39,6 +39,15 @@ G_CONFIGS = {
     "c5": dict(scene="heightfield_c5.json", width=3840, height=2160, spp=64, max_depth=1),
 }
 
+# Algorithmic bytes per camera sample (SURVEY.md §8(d) traffic model: 24 B per AABB fetched
+# per pop-test and per pushed child test, 16 B per BVHNode entered, 72 B per Triangle tested),
+# replayed with the oracle's counters over the reference SearchBVH order (scripts/bytes_model.py):
+#   c3: whole frame, 33,177,600 samples: 300.316 B (primary 248.96 B/ray, shadow
+#       2,478.4 B/ray x 0.02072 shadow rays/sample) + 12 B/pixel framebuffer / 16 spp.
+#   c5: every 27th row (19,660,800 samples): 11,159.58 B (primary 8,316.3 B/ray, shadow
+#       13,508.3 B/ray x 0.2105/sample) + 12 B / 64 spp.
+BYTES_PER_SAMPLE = {"c3": 300.316 + 12.0 / 16, "c5": 11159.58 + 12.0 / 64}
+
 # Heightfield generator parameters for c5.
 C5_GRID = (1024, 512)          # quads in x, y -> 1,048,576 triangles
 C5_SEED = 20260315

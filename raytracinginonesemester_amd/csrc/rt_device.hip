@@ -603,6 +603,26 @@ __global__ __launch_bounds__(BLOCK) void render_hw1_kernel(Hw1Params P) {
     }
 }
 
+// Batched ray-triangle queries (KAT path): one lane per ray.
+__global__ __launch_bounds__(BLOCK) void intersect_kernel(f3 v0, f3 e1, f3 e2, f3 o, const float* __restrict__ dirs,
+                                                          int n, int hw1, float tmin, float tmax,
+                                                          int32_t* __restrict__ hit, float* __restrict__ tout) {
+    const int i = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    if (i >= n) return;
+    f3 d = mk(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+    float t = 0.f, u = 0.f, v = 0.f;
+    bool h;
+    if (hw1) {
+        d = unit(d);
+        h = mt_hw1(o, d, v0, e1, e2, t, u, v);
+    } else {
+        const RayPre r = make_ray(o, d);
+        h = mt_g(r, v0, e1, e2, tmin, tmax, t, u, v);
+    }
+    hit[i] = h ? 1 : 0;
+    tout[i] = h ? t : -1.0f;
+}
+
 }  // namespace
 
 // =========================================================================================
@@ -675,12 +695,16 @@ struct rt_scene {
     DevBuf inode, ibox, leaf, tnorm, objids, mats, lights, jitter;
     int jitter_spp = -1;
     std::vector<float> jitter_host;
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    bool timed = false;
+    // Ring of HIP event pairs around each render kernel, recorded on the launch stream.
+    static constexpr int kRing = 256;
+    hipEvent_t ev0[kRing] = {}, ev1[kRing] = {};
+    uint64_t launches = 0;
     size_t bytes = 0;
     ~rt_scene() {
-        for (auto& e : ev)
-            if (e) (void)hipEventDestroy(e);
+        for (int i = 0; i < kRing; ++i) {
+            if (ev0[i]) (void)hipEventDestroy(ev0[i]);
+            if (ev1[i]) (void)hipEventDestroy(ev1[i]);
+        }
     }
 };
 
@@ -813,7 +837,10 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     if (objids && (rc = s->objids.upload(objids, P * sizeof(int32_t))) != RT_OK) return rc;
     if (nmat > 0 && (rc = s->mats.upload(mats, size_t(nmat) * sizeof(rt_material))) != RT_OK) return rc;
     if (nlights > 0 && (rc = s->lights.upload(lights, size_t(nlights) * sizeof(rt_light))) != RT_OK) return rc;
-    for (auto& e : s->ev) HIP_TRY(hipEventCreate(&e));
+    for (int i = 0; i < rt_scene::kRing; ++i) {
+        HIP_TRY(hipEventCreate(&s->ev0[i]));
+        HIP_TRY(hipEventCreate(&s->ev1[i]));
+    }
     s->bytes = s->inode.n + s->ibox.n + s->leaf.n + s->tnorm.n + s->objids.n + s->mats.n + s->lights.n;
     *out = s.release();
     return RT_OK;
@@ -933,23 +960,27 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     P.lane_samples = samples ? 1 : 0;
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    HIP_TRY(hipEventRecord(s->ev[0], st));
+    const int slot = int(s->launches % rt_scene::kRing);
+    HIP_TRY(hipEventRecord(s->ev0[slot], st));
     if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, P.tiles_total, samples, st);
     else launch<RT_KERNEL_WAVE>(P, P.tiles_total, samples, st);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(s->ev[1], st));
-    s->timed = true;
+    HIP_TRY(hipEventRecord(s->ev1[slot], st));
+    s->launches++;
     return RT_OK;
 }
 
-extern "C" int rt_last_timing(const rt_scene* s, float* total_ms, float* kernel_ms) {
-    if (!s || !s->timed) return set_error(RT_ERR_ARG, "no timed render on this scene");
+extern "C" int rt_kernel_times(const rt_scene* s, float* ms_out, int max, int* n_out) {
+    if (!s || max < 0 || (max > 0 && !ms_out)) return set_error(RT_ERR_ARG, "rt_kernel_times: bad args");
     DeviceGuard g(s->device);
-    HIP_TRY(hipEventSynchronize(s->ev[1]));
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, s->ev[0], s->ev[1]));
-    if (total_ms) *total_ms = ms;
-    if (kernel_ms) *kernel_ms = ms;
+    const uint64_t have = std::min<uint64_t>(s->launches, uint64_t(rt_scene::kRing));
+    const int n = int(std::min<uint64_t>(have, uint64_t(max)));
+    for (int k = 0; k < n; ++k) {  // oldest first among the n most recent
+        const int slot = int((s->launches - uint64_t(n) + uint64_t(k)) % rt_scene::kRing);
+        HIP_TRY(hipEventSynchronize(s->ev1[slot]));
+        HIP_TRY(hipEventElapsedTime(&ms_out[k], s->ev0[slot], s->ev1[slot]));
+    }
+    if (n_out) *n_out = n;
     return RT_OK;
 }
 
@@ -1069,5 +1100,29 @@ extern "C" int rt_render_hw1(int device, const rt_vec3* pos, const rt_vec3* nrm,
         HIP_TRY(hipMemcpy(hit_t_host, dht.p, npx * size_t(spp) * sizeof(float), hipMemcpyDeviceToHost));
     }
     (void)nv;
+    return RT_OK;
+}
+
+extern "C" int rt_intersect_rays(int device, const rt_triangle* tri, const float origin[3], const float* dirs, int n,
+                                 int hw1, float tmin, float tmax, int32_t* hit, float* t) {
+    if (!tri || !origin || n < 0 || (n > 0 && (!dirs || !hit || !t))) return set_error(RT_ERR_ARG, "rt_intersect_rays: bad args");
+    int rc = check_device(device);
+    if (rc != RT_OK) return rc;
+    if (n == 0) return RT_OK;
+    DeviceGuard g(device);
+    DevBuf dd, dh, dt;
+    if ((rc = dd.upload(dirs, size_t(n) * 3 * sizeof(float))) != RT_OK) return rc;
+    if ((rc = dh.alloc(size_t(n) * sizeof(int32_t))) != RT_OK) return rc;
+    if ((rc = dt.alloc(size_t(n) * sizeof(float))) != RT_OK) return rc;
+    const f3 v0{tri->v0.x, tri->v0.y, tri->v0.z};
+    const f3 e1{tri->v1.x - tri->v0.x, tri->v1.y - tri->v0.y, tri->v1.z - tri->v0.z};
+    const f3 e2{tri->v2.x - tri->v0.x, tri->v2.y - tri->v0.y, tri->v2.z - tri->v0.z};
+    hipLaunchKernelGGL(intersect_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, nullptr, v0, e1, e2,
+                       f3{origin[0], origin[1], origin[2]}, static_cast<const float*>(dd.p), n, hw1 ? 1 : 0, tmin,
+                       tmax, static_cast<int32_t*>(dh.p), static_cast<float*>(dt.p));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(hit, dh.p, size_t(n) * sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(t, dt.p, size_t(n) * sizeof(float), hipMemcpyDeviceToHost));
     return RT_OK;
 }

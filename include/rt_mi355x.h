@@ -210,6 +210,12 @@ int rt_render_hw1(int device, const rt_vec3* positions, const rt_vec3* normals,
 int rt_intersect_rays(int device, const rt_triangle* tri, const float origin[3], const float* dirs, int n,
                       int hw1, float tmin, float tmax, int32_t* hit, float* t);
 
+/* The Blinn-Phong powf of the kernels (restatement of the reference libm's powf, see
+ * csrc/rt_math.hpp): rt_powf_host evaluates the host build, rt_powf_batch the device build
+ * over n (x, y) pairs.  Exposed so both can be pinned against the C library's powf. */
+float rt_powf_host(float x, float y);
+int rt_powf_batch(int device, const float* x, const float* y, int n, float* out);
+
 /* Durations (ms) of the render kernel of the most recent min(max, launches, 256)
  * rt_render_device calls on this scene, oldest first, measured with HIP events recorded
  * on the launch stream around the kernel.  Waits for those launches to finish. */

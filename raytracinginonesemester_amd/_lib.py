@@ -126,6 +126,8 @@ SIGNATURES = {
     "rt_render_reference": (I, [SZ, I, I, P, Vec3, I, I, P, P, P, P, P, I, P, I, I, P]),
     "rt_render_hw1": (I, [I, P, P, P, SZ, P, Vec3, Vec3, I, P, P, P, P]),
     "rt_intersect_rays": (I, [I, P, P, P, I, I, C.c_float, C.c_float, P, P]),
+    "rt_powf_host": (C.c_float, [C.c_float, C.c_float]),
+    "rt_powf_batch": (I, [I, P, P, I, P]),
     "rt_kernel_times": (I, [P, P, I, P]),
     "rt_device_count": (I, [P]),
     "rt_last_error": (C.c_char_p, []),

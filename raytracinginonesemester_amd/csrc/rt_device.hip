@@ -318,7 +318,7 @@ __device__ __forceinline__ f3 eval_brdf(const DevMaterial& m, f3 N, f3 V, f3 L) 
     const float NdotH = fmaxf(dot(N, Hh), 0.0f);
     const float inv2Pi = 0.15915494309f;
     const float specNorm = (m.shininess + 2.0f) * inv2Pi;
-    const float specLobe = specNorm * powf(NdotH, m.shininess);
+    const float specLobe = specNorm * ref_powf(NdotH, m.shininess);
     const f3 fs = scale(scale(mk(m.spec[0], m.spec[1], m.spec[2]), m.ks), specLobe);
     return add(fd, fs);
 }
@@ -539,7 +539,7 @@ __device__ __forceinline__ f3 shade_hw1(f3 o, f3 d, bool hit, f3 p, f3 n, f3 lpo
     const f3 diffuse = scale(mul(albedo, lcol), diff);
     const f3 viewDir = unit(sub(o, p));
     const f3 halfDir = unit(add(lightDir, viewDir));
-    const float spec = powf(fmaxf(dot(n, halfDir), 0.0f), 64.0f);
+    const float spec = ref_powf(fmaxf(dot(n, halfDir), 0.0f), 64.0f);
     f3 c = add(add(ambient, diffuse), scale(lcol, spec));
     if (c.x > 1.0f) c.x = 1.0f;
     if (c.y > 1.0f) c.y = 1.0f;
@@ -601,6 +601,12 @@ __global__ __launch_bounds__(BLOCK) void render_hw1_kernel(Hw1Params P) {
         o[1] = acc.y / fs;
         o[2] = acc.z / fs;
     }
+}
+
+__global__ __launch_bounds__(BLOCK) void powf_kernel(const float* __restrict__ x, const float* __restrict__ y, int n,
+                                                     float* __restrict__ out) {
+    const int i = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    if (i < n) out[i] = ref_powf(x[i], y[i]);
 }
 
 // Batched ray-triangle queries (KAT path): one lane per ray.
@@ -1124,5 +1130,25 @@ extern "C" int rt_intersect_rays(int device, const rt_triangle* tri, const float
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(hit, dh.p, size_t(n) * sizeof(int32_t), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(t, dt.p, size_t(n) * sizeof(float), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+extern "C" float rt_powf_host(float x, float y) { return ref_powf(x, y); }
+
+extern "C" int rt_powf_batch(int device, const float* x, const float* y, int n, float* out) {
+    if (n < 0 || (n > 0 && (!x || !y || !out))) return set_error(RT_ERR_ARG, "rt_powf_batch: bad args");
+    int rc = check_device(device);
+    if (rc != RT_OK) return rc;
+    if (n == 0) return RT_OK;
+    DeviceGuard g(device);
+    DevBuf dx, dy, dout;
+    if ((rc = dx.upload(x, size_t(n) * sizeof(float))) != RT_OK) return rc;
+    if ((rc = dy.upload(y, size_t(n) * sizeof(float))) != RT_OK) return rc;
+    if ((rc = dout.alloc(size_t(n) * sizeof(float))) != RT_OK) return rc;
+    hipLaunchKernelGGL(powf_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, nullptr,
+                       static_cast<const float*>(dx.p), static_cast<const float*>(dy.p), n, static_cast<float*>(dout.p));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, dout.p, size_t(n) * sizeof(float), hipMemcpyDeviceToHost));
     return RT_OK;
 }

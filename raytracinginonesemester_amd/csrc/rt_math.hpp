@@ -187,6 +187,153 @@ __device__ __forceinline__ f3 random_unit_vector(uint32_t& st) {
     }
 }
 
+// ---- powf: the reference's libm, restated ---------------------------------------------
+// The reference calls powf from glibc (Ubuntu GLIBC 2.35-0ubuntu3.11 in this image), whose
+// single-precision pow is the ARM optimized-routines algorithm (glibc
+// sysdeps/ieee754/flt-32/e_powf.c, e_powf_log2_data.c, e_exp2f_data.c): log2 through a
+// 16-entry (invc, log2 c) table + degree-5 polynomial in double, times y, then exp2 through
+// a 32-entry 2^(i/32) table + degree-3 polynomial, rounded once to float.  On x86-64 with
+// FMA, glibc dispatches to the -mfma build of that file, where every a*b+c of the
+// polynomial steps is one fused multiply-add; the fma() calls below are exactly those.
+// Constants are the values of __powf_log2_data / __exp2f_data.  The restatement is pinned
+// bit for bit against glibc powf by tests/test_powf.py (host build of this code and the
+// device kernel); with it the whole shading chain is reproduced bit for bit.
+namespace pw {
+struct LogEntry {
+    double invc, logc;
+};
+__host__ __device__ __forceinline__ LogEntry log_tab(int i) {
+    switch (i) {
+        case 0: return {0x1.661ec79f8f3bep+0, -0x1.efec65b963019p-2};
+        case 1: return {0x1.571ed4aaf883dp+0, -0x1.b0b6832d4fca4p-2};
+        case 2: return {0x1.49539f0f010b0p+0, -0x1.7418b0a1fb77bp-2};
+        case 3: return {0x1.3c995b0b80385p+0, -0x1.39de91a6dcf7bp-2};
+        case 4: return {0x1.30d190c8864a5p+0, -0x1.01d9bf3f2b631p-2};
+        case 5: return {0x1.25e227b0b8ea0p+0, -0x1.97c1d1b3b7af0p-3};
+        case 6: return {0x1.1bb4a4a1a343fp+0, -0x1.2f9e393af3c9fp-3};
+        case 7: return {0x1.12358f08ae5bap+0, -0x1.960cbbf788d5cp-4};
+        case 8: return {0x1.0953f419900a7p+0, -0x1.a6f9db6475fcep-5};
+        case 9: return {0x1.0000000000000p+0, 0x0.0p+0};
+        case 10: return {0x1.e608cfd9a47acp-1, 0x1.338ca9f24f53dp-4};
+        case 11: return {0x1.ca4b31f026aa0p-1, 0x1.476a9543891bap-3};
+        case 12: return {0x1.b2036576afce6p-1, 0x1.e840b4ac4e4d2p-3};
+        case 13: return {0x1.9c2d163a1aa2dp-1, 0x1.40645f0c6651cp-2};
+        case 14: return {0x1.886e6037841edp-1, 0x1.88e9c2c1b9ff8p-2};
+        default: return {0x1.767dcf5534862p-1, 0x1.ce0a44eb17bccp-2};
+    }
+}
+__host__ __device__ __forceinline__ uint64_t exp2_tab(int i) {
+    constexpr uint64_t T[32] = {
+        0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+        0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+        0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+        0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+        0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+        0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+        0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+        0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+    return T[i];
+}
+__host__ __device__ __forceinline__ uint32_t asu(float f) { uint32_t u; __builtin_memcpy(&u, &f, 4); return u; }
+__host__ __device__ __forceinline__ float asf(uint32_t u) { float f; __builtin_memcpy(&f, &u, 4); return f; }
+__host__ __device__ __forceinline__ uint64_t asu64(double f) { uint64_t u; __builtin_memcpy(&u, &f, 8); return u; }
+__host__ __device__ __forceinline__ double asd(uint64_t u) { double f; __builtin_memcpy(&f, &u, 8); return f; }
+
+__host__ __device__ __forceinline__ double log2_inline(uint32_t ix) {
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = int((tmp >> 19) % 16u);
+    const uint32_t top = tmp & 0xff800000u;
+    const uint32_t iz = ix - top;
+    const int k = int32_t(top) >> 23;
+    const LogEntry e = log_tab(i);
+    const double z = double(asf(iz));
+    const double A0 = 0x1.27616c9496e0bp-2, A1 = -0x1.71969a075c67ap-2, A2 = 0x1.ec70a6ca7baddp-2,
+                 A3 = -0x1.7154748bef6c8p-1, A4 = 0x1.71547652ab82bp+0;
+    const double r = fma(z, e.invc, -1.0);
+    const double y0 = e.logc + double(k);
+    const double r2 = r * r;
+    double y = fma(A0, r, A1);
+    const double p = fma(A2, r, A3);
+    const double r4 = r2 * r2;
+    double q = fma(A4, r, y0);
+    q = fma(p, r2, q);
+    y = fma(y, r4, q);
+    return y;
+}
+
+__host__ __device__ __forceinline__ float exp2_inline(double xd, uint32_t sign_bias) {
+    const double SHIFT = 0x1.8p+47;  // 0x1.8p52 / 32
+    const double C0 = 0x1.c6af84b912394p-5, C1 = 0x1.ebfce50fac4f3p-3, C2 = 0x1.62e42ff0c52d6p-1;
+    double kd = xd + SHIFT;
+    const uint64_t ki = asu64(kd);
+    kd -= SHIFT;
+    const double r = xd - kd;
+    uint64_t t = exp2_tab(int(ki % 32u));
+    const uint64_t ski = ki + sign_bias;
+    t += ski << (52 - 5);
+    const double s = asd(t);
+    const double z = fma(C0, r, C1);
+    const double r2 = r * r;
+    double y = fma(C2, r, 1.0);
+    y = fma(z, r2, y);
+    y = y * s;
+    return float(y);
+}
+
+__host__ __device__ __forceinline__ int checkint(uint32_t iy) {
+    const int e = int(iy >> 23 & 0xff);
+    if (e < 0x7f) return 0;
+    if (e > 0x7f + 23) return 2;
+    if (iy & ((1u << (0x7f + 23 - e)) - 1)) return 0;
+    if (iy & (1u << (0x7f + 23 - e))) return 1;
+    return 2;
+}
+__host__ __device__ __forceinline__ bool zeroinfnan(uint32_t ix) { return 2 * ix - 1 >= 2u * 0x7f800000u - 1; }
+__host__ __device__ __forceinline__ bool issignaling(uint32_t ix) {
+    return 2 * (ix ^ 0x00400000u) > 2u * 0x7fc00000u;
+}
+}  // namespace pw
+
+__host__ __device__ inline float ref_powf(float x, float y) {
+    using namespace pw;
+    uint32_t sign_bias = 0;
+    uint32_t ix = asu(x);
+    const uint32_t iy = asu(y);
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u || zeroinfnan(iy)) {
+        if (zeroinfnan(iy)) {
+            if (2 * iy == 0) return issignaling(ix) ? x + y : 1.0f;
+            if (ix == 0x3f800000u) return issignaling(iy) ? x + y : 1.0f;
+            if (2 * ix > 2u * 0x7f800000u || 2 * iy > 2u * 0x7f800000u) return x + y;
+            if (2 * ix == 2 * 0x3f800000u) return 1.0f;
+            if ((2 * ix < 2 * 0x3f800000u) == !(iy & 0x80000000u)) return 0.0f;
+            return y * y;
+        }
+        if (zeroinfnan(ix)) {
+            float x2 = x * x;
+            if ((ix & 0x80000000u) && checkint(iy) == 1) x2 = -x2;
+            return (iy & 0x80000000u) ? 1.0f / x2 : x2;
+        }
+        if (ix & 0x80000000u) {
+            const int yint = checkint(iy);
+            if (yint == 0) return (x - x) / (x - x);
+            if (yint == 1) sign_bias = 1u << (5 + 11);
+            ix &= 0x7fffffffu;
+        }
+        if (ix < 0x00800000u) {
+            ix = asu(x * 0x1p23f);
+            ix &= 0x7fffffffu;
+            ix -= 23u << 23;
+        }
+    }
+    const double logx = log2_inline(ix);
+    const double ylogx = double(y) * logx;
+    if ((asu64(ylogx) >> 47 & 0xffff) >= asu64(126.0) >> 47) {
+        if (ylogx > 0x1.fffffffd1d571p+6) return sign_bias ? -INFINITY : INFINITY;
+        if (ylogx <= -150.0) return sign_bias ? -0.0f : 0.0f;
+    }
+    return exp2_inline(ylogx, sign_bias);
+}
+
 __device__ __forceinline__ f3 clamp01(f3 c) {  // shader.h:24-32
     if (c.x > 1.0f) c.x = 1.0f;
     if (c.y > 1.0f) c.y = 1.0f;

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Run GPU steps in order; each under its own time limit; stop at the first fatal exit
+# (time limit 124/137, abort 134, segfault 139) so nothing else touches a sick GPU.
+# usage: scripts/gpu_session.sh "name:seconds:command" ...
+mkdir -p gpurun_out
+for spec in "$@"; do
+  name="${spec%%:*}"; rest="${spec#*:}"; secs="${rest%%:*}"; cmd="${rest#*:}"
+  echo "== $name ($secs s): $cmd"
+  timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
+  rc=$?
+  echo "== $name rc=$rc"; tail -4 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ]; then echo "fatal exit $rc: stopping"; exit $rc; fi
+done

@@ -1,0 +1,77 @@
+"""Multi-rank path on CPU (gloo, world_size 2 and 4): band sharding + one gather reassemble
+exactly the single-rank frame.  Strips are rendered by the oracle (the GPU path's checker),
+so this covers the sharding/gather logic bench.py runs over RCCL."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import host_scene, oracle_camera
+
+from raytracinginonesemester_amd import dist as rdist
+
+W, H, SPP, BAND = 64, 45, 4, 8
+
+
+def _render_rows(y0, y1):
+    from oracle import pyoracle as orc
+
+    hs = host_scene("frog.json")
+    cam = hs.camera(W, H)
+    rgb = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles, hs.tri_object_ids,
+                       hs.materials, hs.lights, spp=SPP, rows=(y0, y1), threads=1)
+    return rgb[y0:y1]
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rows = rdist.rows_of(H, BAND, rank, world)
+        parts = [_render_rows(y0, y1) for (y0, y1) in rdist.bands_of(H, BAND, rank, world)]
+        mine = np.concatenate(parts, axis=0) if parts else np.zeros((0, W, 3), np.float32)
+        assert mine.shape[0] == len(rows)
+        strip = torch.zeros((rdist.max_strip_rows(H, BAND, world), W, 3), dtype=torch.float32)
+        strip[:len(rows)] = torch.from_numpy(mine)
+        frame = rdist.gather_frame(strip, H, BAND, world, rank)
+        if rank == 0:
+            q.put(frame)
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_band_gather_reassembles_single_rank_frame(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frame = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full = _render_rows(0, H)
+    assert np.array_equal(frame.view(np.uint32), full.view(np.uint32))
+
+
+def test_band_assignment_partitions_rows():
+    for world in (1, 2, 3, 8):
+        seen = sorted(y for r in range(world) for y in rdist.rows_of(1080, 8, r, world))
+        assert seen == list(range(1080))
+        idx = rdist.strip_index(1080, 8, world)
+        assert idx[:, 0].max() == world - 1

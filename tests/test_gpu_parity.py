@@ -2,10 +2,11 @@
 
 Bar:
 * primary-hit triangle indices and their t: bit-exact (index work);
-* float framebuffer: max-abs <= RGB_TOL = 2e-6 against the reference / oracle — the only
-  inexact operation is powf in the Blinn-Phong lobe (device libm vs glibc, <= 1 ulp);
-  every other operation is reproduced bit for bit, so nearly every pixel is bit-exact
-  (checked: >= 99.9 % of framebuffer floats identical);
+* float framebuffer: bit-exact.  Every float/double operation of the path is reproduced in
+  the reference's order without contraction, HIP's f32 division/sqrt are correctly
+  rounded like x86's, and powf is a restatement of the reference libm's powf
+  (tests/test_powf.py).  RGB_TOL = 2e-6 is the stated tolerance the checks also report
+  against (the bound a device-libm powf would need, SURVEY.md Appendix B item 6);
 * P6 output (ppm_p6 defaults): max-abs <= 1 per 8-bit sample.
 """
 from __future__ import annotations
@@ -37,7 +38,7 @@ def _device_scene(scene):
     return cache[key]
 
 
-def _check_fb(rgb, ref, exact_frac=0.999):
+def _check_fb(rgb, ref, exact_frac=1.0):
     rgb = np.asarray(rgb, np.float32).reshape(-1)
     ref = np.asarray(ref, np.float32).reshape(-1)
     assert np.isfinite(rgb).all()
@@ -71,7 +72,7 @@ def test_c3_full_frame_matches_reference():
     rgb, hi, ht = _device_scene("frog.json").render(cam, spp=16, max_depth=1, aov=True)
     assert hashlib.sha256(hi.tobytes()).hexdigest() == meta["sha256"]["hits.i32"]
     assert hashlib.sha256(ht.tobytes()).hexdigest() == meta["sha256"]["hitt.f32"]
-    _check_fb(rgb, golden_array("c3_full", "fb.f32.gz", np.float32), exact_frac=0.9999)
+    _check_fb(rgb, golden_array("c3_full", "fb.f32.gz", np.float32))
     ppm = gzip.open(GOLDEN / "scenes" / "c3_full" / "image.ppm.gz").read()
     mine = rt.encode_p6(rgb)
     assert len(mine) == len(ppm) and mine[:17] == ppm[:17]
@@ -89,7 +90,7 @@ def test_odd_shapes_against_oracle(spp, W, H, kernel):
                                  hs.tri_object_ids, hs.materials, hs.lights, spp=spp, max_depth=1, aov=True)
     assert np.array_equal(hi, rhi)
     assert np.array_equal(ht.view(np.uint32), rht.view(np.uint32))
-    _check_fb(rgb, ref, exact_frac=0.99)
+    _check_fb(rgb, ref)
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -102,7 +103,7 @@ def test_multibounce_mirror_path_against_oracle(kernel):
     ref = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,
                        hs.tri_object_ids, hs.materials, hs.lights, spp=2, max_depth=4, diffuse_bounce=False,
                        miss=(0.1, 0.2, 0.3))
-    _check_fb(rgb, ref, exact_frac=0.99)
+    _check_fb(rgb, ref)
 
 
 @pytest.mark.parametrize("band_count", [2, 3, 8])
@@ -238,4 +239,4 @@ def test_full_size_properties_c5():
         ref = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,
                            hs.tri_object_ids, hs.materials, hs.lights, spp=64, max_depth=1, miss=miss,
                            rows=(y0, y0 + 2))
-        _check_fb(rgb[y0:y0 + 2], ref[y0:y0 + 2], exact_frac=0.99)
+        _check_fb(rgb[y0:y0 + 2], ref[y0:y0 + 2])

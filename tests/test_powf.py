@@ -1,0 +1,65 @@
+"""The kernels' powf (csrc/rt_math.hpp: ref_powf) is a restatement of the reference's libm powf
+(glibc 2.35, ARM optimized-routines algorithm, FMA build).  Pinned bit for bit against the
+C library's own powf — the function the reference and the oracle call — on the host build
+(CPU) and the device build (GPU), over the Blinn-Phong domain (x in [0,1], the JSON
+shininess values) and over random/special inputs."""
+from __future__ import annotations
+
+import ctypes as C
+import ctypes.util
+
+import numpy as np
+import pytest
+
+import raytracinginonesemester_amd as rt  # noqa: F401
+from raytracinginonesemester_amd import _lib
+
+libm = C.CDLL(ctypes.util.find_library("m") or "libm.so.6")
+libm.powf.restype = C.c_float
+libm.powf.argtypes = [C.c_float, C.c_float]
+
+
+def _inputs(n_grid=1 << 16, n_rand=1 << 15, seed=3):
+    rng = np.random.default_rng(seed)
+    xs, ys = [], []
+    grid = np.linspace(0, 0x3F800000, n_grid, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    for y in (1.0, 2.0, 16.0, 32.0, 64.0, 128.0, 7.3, 0.5):
+        xs.append(grid)
+        ys.append(np.full_like(grid, y))
+    r = rng.integers(0, 2 ** 32, size=(2, n_rand), dtype=np.uint64).astype(np.uint32).view(np.float32)
+    xs.append(r[0])
+    ys.append(r[1])
+    xs.append(np.abs(rng.normal(size=n_rand)).astype(np.float32))
+    ys.append(rng.uniform(-200, 200, size=n_rand).astype(np.float32))
+    sp = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 1e-45, 1e-40, 2.0, -2.0, 0.5, 1e38],
+                  np.float32)
+    xx, yy = np.meshgrid(sp, sp)
+    xs.append(xx.ravel())
+    ys.append(yy.ravel())
+    return np.concatenate(xs), np.concatenate(ys)
+
+
+def _same(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    both_nan = np.isnan(a) & np.isnan(b)
+    return (a.view(np.uint32) == b.view(np.uint32)) | both_nan
+
+
+def test_host_build_matches_libm_powf():
+    x, y = _inputs(n_grid=1 << 13, n_rand=1 << 13)
+    f = _lib.lib().rt_powf_host
+    mine = np.array([f(float(a), float(b)) for a, b in zip(x, y)], np.float32)
+    ref = np.array([libm.powf(float(a), float(b)) for a, b in zip(x, y)], np.float32)
+    ok = _same(mine, ref)
+    assert ok.all(), (x[~ok][:5], y[~ok][:5], mine[~ok][:5], ref[~ok][:5])
+
+
+@pytest.mark.gpu
+def test_device_build_matches_libm_powf():
+    x, y = _inputs()
+    out = np.zeros_like(x)
+    _lib.check(_lib.lib().rt_powf_batch(0, x.ctypes.data, y.ctypes.data, x.size, out.ctypes.data))
+    ref = np.array([libm.powf(float(a), float(b)) for a, b in zip(x, y)], np.float32)
+    ok = _same(out, ref)
+    assert ok.all(), (x[~ok][:5], y[~ok][:5], out[~ok][:5], ref[~ok][:5])

@@ -171,7 +171,15 @@ typedef struct {
      * ("strip" layout).  band_count <= 1 renders the whole frame in row-major order. */
     int32_t band_rows, band_index, band_count;
     int32_t kernel;           /* RT_KERNEL_* */
+    int32_t tile_order;       /* RT_TILES_*: block -> pixel-tile order (speed only) */
 } rt_render_opts;
+
+enum {
+    RT_TILES_AUTO = 0,        /* RT_TILES_ROWS */
+    RT_TILES_LINEAR = 1,      /* block b renders tile b (dispatch deals blocks round-robin to XCDs) */
+    RT_TILES_XCD_CHUNK = 2,   /* each XCD's blocks take one contiguous 1/8 of the tiles */
+    RT_TILES_ROWS = 3         /* each XCD's blocks take every 8th row of tiles */
+};
 void rt_render_opts_default(rt_render_opts* o);
 
 /* Rows covered by (band_rows, band_index, band_count) for an H-row image. */

@@ -3,7 +3,8 @@
 The compute lives in librt_mi355x.so (HIP kernels for gfx950 + the C ABI of
 include/rt_mi355x.h); this package is the host-side mirror of the reference interface.
 """
-from ._lib import RTError, RT_KERNEL_AUTO, RT_KERNEL_LANE, RT_KERNEL_WAVE  # noqa: F401
+from ._lib import (RTError, RT_KERNEL_AUTO, RT_KERNEL_LANE, RT_KERNEL_WAVE, RT_TILES_AUTO,  # noqa: F401
+                   RT_TILES_LINEAR, RT_TILES_ROWS, RT_TILES_XCD_CHUNK)
 from .api import (  # noqa: F401
     LIGHT_DTYPE, Camera, DeviceScene, HostScene, MeshHW1, build_bvh, default_material, device_count,
     encode_p6, intersect_rays, jittered_samples, read_p6, render, render_hw1, write_p6,

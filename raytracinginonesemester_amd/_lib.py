@@ -18,6 +18,7 @@ RT_ERR = {
     -5: "RT_ERR_NOMEM", -6: "RT_ERR_NODEVICE", -7: "RT_ERR_UNSUPPORTED",
 }
 RT_KERNEL_AUTO, RT_KERNEL_WAVE, RT_KERNEL_LANE = 0, 1, 2
+RT_TILES_AUTO, RT_TILES_LINEAR, RT_TILES_XCD_CHUNK, RT_TILES_ROWS = 0, 1, 2, 3
 
 
 class RTError(RuntimeError):
@@ -90,7 +91,8 @@ class PPMOptions(C.Structure):
 class RenderOpts(C.Structure):
     _fields_ = [("max_depth", C.c_int32), ("spp", C.c_int32), ("diffuse_bounce", C.c_int32),
                 ("miss_color", Vec3), ("jitter", C.c_void_p), ("band_rows", C.c_int32),
-                ("band_index", C.c_int32), ("band_count", C.c_int32), ("kernel", C.c_int32)]
+                ("band_index", C.c_int32), ("band_count", C.c_int32), ("kernel", C.c_int32),
+                ("tile_order", C.c_int32)]
 
 
 P = C.c_void_p

@@ -81,6 +81,7 @@ struct RenderParams {
     int32_t band_rows, band_index, band_count, rows;  // rows = local rows rendered
     int32_t tile_w, tile_h, tiles_x, tiles_total;     // pixel tile per block
     int32_t lane_samples;                             // 1: one sample per lane; else pixel loop
+    int32_t tile_order;                               // RT_TILES_*
     float* __restrict__ rgb;
     int32_t* __restrict__ hit_idx;
     float* __restrict__ hit_t;
@@ -434,12 +435,25 @@ __device__ __forceinline__ int global_row(const RenderParams& P, int r) {
     return (P.band_index + k * P.band_count) * P.band_rows + within;
 }
 
-// XCD-aware block order: blocks b, b+8, b+16 ... share an XCD (round-robin dispatch), so
-// give each such group a contiguous run of tiles (shared BVH working set in that L2).
-__device__ __forceinline__ int tile_of_block(int b, int nblocks) {
-    const int q = nblocks / 8, rr = nblocks % 8;
+// Block -> tile order.  Dispatch deals blocks round-robin over the 8 XCDs, so blocks b,
+// b+8, b+16 ... share one L2 (a speed property only).  XCD_CHUNK gives each XCD a
+// contiguous 1/8 of the tiles (best L2 sharing, worst balance when the geometry covers a
+// band of the frame); ROWS gives each XCD every 8th row of tiles (neighbouring tiles on one
+// XCD, work spread evenly); LINEAR leaves the dispatcher's order.
+__device__ __forceinline__ int tile_of_block(int b, int nblocks, int order, int tiles_x) {
+    if (order == RT_TILES_LINEAR) return b;
     const int xcd = b % 8, idx = b / 8;
-    return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+    if (order == RT_TILES_XCD_CHUNK) {
+        const int q = nblocks / 8, rr = nblocks % 8;  // bijective for any nblocks
+        return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+    }
+    // RT_TILES_ROWS: XCD k walks tile rows k, k+8, k+16 ...; the tail (rows that do not fill
+    // a group of 8) falls back to the linear order so the mapping stays a bijection.
+    const int tiles_y = nblocks / tiles_x;
+    const int full = (tiles_y / 8) * 8 * tiles_x;  // blocks covered by whole groups of 8 rows
+    if (b >= full) return b;
+    const int row_in = idx / tiles_x, col = idx % tiles_x;
+    return (row_in * 8 + xcd) * tiles_x + col;
 }
 
 // One sample per lane: a block covers tile_w x tile_h pixels x spp samples (spp a power
@@ -447,7 +461,7 @@ __device__ __forceinline__ int tile_of_block(int b, int nblocks) {
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void render_samples_kernel(RenderParams P) {
     __shared__ float col[BLOCK * 3];
-    const int tile = tile_of_block((int)blockIdx.x, (int)gridDim.x);
+    const int tile = tile_of_block((int)blockIdx.x, (int)gridDim.x, P.tile_order, P.tiles_x);
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int t = (int)threadIdx.x;
     const int s = t % P.spp;
@@ -483,7 +497,7 @@ __global__ __launch_bounds__(BLOCK) void render_samples_kernel(RenderParams P) {
 // General spp: one pixel per lane looping over its samples in order (query.cu:146-163).
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void render_pixels_kernel(RenderParams P) {
-    const int tile = tile_of_block((int)blockIdx.x, (int)gridDim.x);
+    const int tile = tile_of_block((int)blockIdx.x, (int)gridDim.x, P.tile_order, P.tiles_x);
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int t = (int)threadIdx.x;
     const int x = tx * P.tile_w + t % P.tile_w;
@@ -870,6 +884,7 @@ extern "C" void rt_render_opts_default(rt_render_opts* o) {
     o->band_index = 0;
     o->band_count = 1;
     o->kernel = RT_KERNEL_AUTO;
+    o->tile_order = RT_TILES_AUTO;
 }
 
 extern "C" int rt_shard_rows(int H, int band_rows, int band_index, int band_count) {
@@ -964,6 +979,7 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     const int tiles_y = (rows + th - 1) / th;
     P.tiles_total = P.tiles_x * tiles_y;
     P.lane_samples = samples ? 1 : 0;
+    P.tile_order = o->tile_order == RT_TILES_AUTO ? RT_TILES_ROWS : o->tile_order;
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int slot = int(s->launches % rt_scene::kRing);

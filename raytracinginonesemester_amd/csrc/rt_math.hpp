@@ -2,8 +2,8 @@
 // evaluation order (G/include/vec3.h, bvh.h, query.h, shader.h, brdf.h, camera.h).
 // The translation unit is compiled with -ffp-contract=off (no v_fma for a*b+c) and with
 // HIP's default correctly-rounded f32 division and sqrt, so every helper below returns the
-// bits the reference's x86-64 build returns; powf is the one libm call whose device
-// implementation may differ in the last place ("Parity").
+// bits the reference's x86-64 build returns; the one libm call on the path, powf, is a
+// restatement of the reference libm's own algorithm (ref_powf below, DESIGN.md "Parity").
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -199,40 +199,48 @@ __device__ __forceinline__ f3 random_unit_vector(uint32_t& st) {
 // bit for bit against glibc powf by tests/test_powf.py (host build of this code and the
 // device kernel); with it the whole shading chain is reproduced bit for bit.
 namespace pw {
+// (invc, log2 c) pairs of __powf_log2_data.tab and the 2^(i/32) bit patterns of
+// __exp2f_data.tab.  Device copies live in constant memory (indexed per lane: an L1-cached
+// vector load, no registers held across the kernel); the host copies serve rt_powf_host.
+#define RT_POW_LOG_TAB                                                                        \
+    {0x1.661ec79f8f3bep+0, -0x1.efec65b963019p-2, 0x1.571ed4aaf883dp+0, -0x1.b0b6832d4fca4p-2, \
+     0x1.49539f0f010b0p+0, -0x1.7418b0a1fb77bp-2, 0x1.3c995b0b80385p+0, -0x1.39de91a6dcf7bp-2, \
+     0x1.30d190c8864a5p+0, -0x1.01d9bf3f2b631p-2, 0x1.25e227b0b8ea0p+0, -0x1.97c1d1b3b7af0p-3, \
+     0x1.1bb4a4a1a343fp+0, -0x1.2f9e393af3c9fp-3, 0x1.12358f08ae5bap+0, -0x1.960cbbf788d5cp-4, \
+     0x1.0953f419900a7p+0, -0x1.a6f9db6475fcep-5, 0x1.0000000000000p+0, 0x0.0p+0,              \
+     0x1.e608cfd9a47acp-1, 0x1.338ca9f24f53dp-4, 0x1.ca4b31f026aa0p-1, 0x1.476a9543891bap-3,   \
+     0x1.b2036576afce6p-1, 0x1.e840b4ac4e4d2p-3, 0x1.9c2d163a1aa2dp-1, 0x1.40645f0c6651cp-2,   \
+     0x1.886e6037841edp-1, 0x1.88e9c2c1b9ff8p-2, 0x1.767dcf5534862p-1, 0x1.ce0a44eb17bccp-2}
+#define RT_EXP2_TAB                                                                           \
+    {0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull, \
+     0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull, \
+     0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull, \
+     0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull, \
+     0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull, \
+     0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull, \
+     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull, \
+     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull}
+__constant__ const double kLogTabDev[32] = RT_POW_LOG_TAB;
+__constant__ const uint64_t kExp2TabDev[32] = RT_EXP2_TAB;
+static const double kLogTabHost[32] = RT_POW_LOG_TAB;
+static const uint64_t kExp2TabHost[32] = RT_EXP2_TAB;
+
 struct LogEntry {
     double invc, logc;
 };
 __host__ __device__ __forceinline__ LogEntry log_tab(int i) {
-    switch (i) {
-        case 0: return {0x1.661ec79f8f3bep+0, -0x1.efec65b963019p-2};
-        case 1: return {0x1.571ed4aaf883dp+0, -0x1.b0b6832d4fca4p-2};
-        case 2: return {0x1.49539f0f010b0p+0, -0x1.7418b0a1fb77bp-2};
-        case 3: return {0x1.3c995b0b80385p+0, -0x1.39de91a6dcf7bp-2};
-        case 4: return {0x1.30d190c8864a5p+0, -0x1.01d9bf3f2b631p-2};
-        case 5: return {0x1.25e227b0b8ea0p+0, -0x1.97c1d1b3b7af0p-3};
-        case 6: return {0x1.1bb4a4a1a343fp+0, -0x1.2f9e393af3c9fp-3};
-        case 7: return {0x1.12358f08ae5bap+0, -0x1.960cbbf788d5cp-4};
-        case 8: return {0x1.0953f419900a7p+0, -0x1.a6f9db6475fcep-5};
-        case 9: return {0x1.0000000000000p+0, 0x0.0p+0};
-        case 10: return {0x1.e608cfd9a47acp-1, 0x1.338ca9f24f53dp-4};
-        case 11: return {0x1.ca4b31f026aa0p-1, 0x1.476a9543891bap-3};
-        case 12: return {0x1.b2036576afce6p-1, 0x1.e840b4ac4e4d2p-3};
-        case 13: return {0x1.9c2d163a1aa2dp-1, 0x1.40645f0c6651cp-2};
-        case 14: return {0x1.886e6037841edp-1, 0x1.88e9c2c1b9ff8p-2};
-        default: return {0x1.767dcf5534862p-1, 0x1.ce0a44eb17bccp-2};
-    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    return {kLogTabDev[2 * i], kLogTabDev[2 * i + 1]};
+#else
+    return {kLogTabHost[2 * i], kLogTabHost[2 * i + 1]};
+#endif
 }
 __host__ __device__ __forceinline__ uint64_t exp2_tab(int i) {
-    constexpr uint64_t T[32] = {
-        0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
-        0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
-        0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
-        0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
-        0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
-        0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
-        0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
-        0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
-    return T[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+    return kExp2TabDev[i];
+#else
+    return kExp2TabHost[i];
+#endif
 }
 __host__ __device__ __forceinline__ uint32_t asu(float f) { uint32_t u; __builtin_memcpy(&u, &f, 4); return u; }
 __host__ __device__ __forceinline__ float asf(uint32_t u) { float f; __builtin_memcpy(&f, &u, 4); return f; }

@@ -224,6 +224,13 @@ int rt_intersect_rays(int device, const rt_triangle* tri, const float origin[3],
 float rt_powf_host(float x, float y);
 int rt_powf_batch(int device, const float* x, const float* y, int n, float* out);
 
+/* Host build of the kernels' AABB test for n (ray, box, [tmin,tmax]) triples: out_exact =
+ * the reference's double slab test (bvh.h:81-129), out_fast = the float-pre-classified test
+ * the kernels run (must equal out_exact), out_class = 0 miss / 1 hit / 2 ambiguous (decided
+ * in double).  rays: n*6 floats (orig, dir), boxes: n*6 (min, max), tminmax: n*2. */
+int rt_box_test_host(const float* rays, const float* boxes, const float* tminmax, int n,
+                     int32_t* out_fast, int32_t* out_exact, int32_t* out_class);
+
 /* Durations (ms) of the render kernel of the most recent min(max, launches, 256)
  * rt_render_device calls on this scene, oldest first, measured with HIP events recorded
  * on the launch stream around the kernel.  Waits for those launches to finish. */

@@ -130,6 +130,7 @@ SIGNATURES = {
     "rt_intersect_rays": (I, [I, P, P, P, I, I, C.c_float, C.c_float, P, P]),
     "rt_powf_host": (C.c_float, [C.c_float, C.c_float]),
     "rt_powf_batch": (I, [I, P, P, I, P]),
+    "rt_box_test_host": (I, [P, P, P, I, P, P, P]),
     "rt_kernel_times": (I, [P, P, I, P]),
     "rt_device_count": (I, [P]),
     "rt_last_error": (C.c_char_p, []),

@@ -82,6 +82,7 @@ struct RenderParams {
     int32_t tile_w, tile_h, tiles_x, tiles_total;     // pixel tile per block
     int32_t lane_samples;                             // 1: one sample per lane; else pixel loop
     int32_t tile_order;                               // RT_TILES_*
+    int32_t spp_log2, tile_w_log2;                    // samples kernel: both powers of two
     float* __restrict__ rgb;
     int32_t* __restrict__ hit_idx;
     float* __restrict__ hit_t;
@@ -126,7 +127,7 @@ __device__ __forceinline__ Box own_box(const SceneView& sc, uint32_t ref, bool i
 }
 
 __device__ __forceinline__ bool box_test(const RayPre& r, const Box& b, float bestT) {
-    return box_hit(r, b.mn[0], b.mn[1], b.mn[2], b.mx[0], b.mx[1], b.mx[2], (double)kRayTMin, (double)bestT);
+    return box_hit(r, b.mn[0], b.mn[1], b.mn[2], b.mx[0], b.mx[1], b.mx[2], kRayTMin, bestT);
 }
 
 // Result of one closest-hit query.
@@ -194,7 +195,7 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
         const uint4 q3 = *reinterpret_cast<const uint4*>(N + 3);
         const uint32_t lref = q3.x, rref = q3.y;
         if (lref != NO_REF) {
-            const bool pl = act && box_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, (double)kRayTMin, (double)hs.bestT);
+            const bool pl = act && box_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, kRayTMin, hs.bestT);
             const uint64_t ml = ballot(pl);
             if (ml != 0) {
                 st_ref = wrlane(lref, sp, st_ref);
@@ -205,7 +206,7 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
             }
         }
         if (rref != NO_REF) {
-            const bool pr = act && box_hit(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, (double)kRayTMin, (double)hs.bestT);
+            const bool pr = act && box_hit(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, kRayTMin, hs.bestT);
             const uint64_t mr = ballot(pr);
             if (mr != 0) {
                 st_ref = wrlane(rref, sp, st_ref);
@@ -256,13 +257,13 @@ __device__ __forceinline__ void traverse_lane(const SceneView& sc, const RayPre&
         const float4 q0 = N[0], q1 = N[1], q2 = N[2];
         const uint4 q3 = *reinterpret_cast<const uint4*>(N + 3);
         if (q3.x != NO_REF &&
-            box_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, (double)kRayTMin, (double)hs.bestT)) {
+            box_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, kRayTMin, hs.bestT)) {
             st_ref[sp] = q3.x;
             st_ver[sp] = ver;
             ++sp;
         }
         if (q3.y != NO_REF &&
-            box_hit(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, (double)kRayTMin, (double)hs.bestT)) {
+            box_hit(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, kRayTMin, hs.bestT)) {
             st_ref[sp] = q3.y;
             st_ver[sp] = ver;
             ++sp;
@@ -464,10 +465,10 @@ __global__ __launch_bounds__(BLOCK) void render_samples_kernel(RenderParams P) {
     const int tile = tile_of_block((int)blockIdx.x, (int)gridDim.x, P.tile_order, P.tiles_x);
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int t = (int)threadIdx.x;
-    const int s = t % P.spp;
-    const int pit = t / P.spp;
-    const int x = tx * P.tile_w + pit % P.tile_w;
-    const int r = ty * P.tile_h + pit / P.tile_w;
+    const int s = t & (P.spp - 1);            // spp and tile_w are powers of two here
+    const int pit = t >> P.spp_log2;
+    const int x = tx * P.tile_w + (pit & (P.tile_w - 1));
+    const int r = ty * P.tile_h + (pit >> P.tile_w_log2);
     const bool valid = x < P.W && r < P.rows;
     const int y = valid ? global_row(P, r) : 0;
     int32_t pidx = -1;
@@ -486,11 +487,13 @@ __global__ __launch_bounds__(BLOCK) void render_samples_kernel(RenderParams P) {
         // col = col + TraceRayIterative(...) in sample order, then col / float(spp)
         f3 acc = mk(0.f, 0.f, 0.f);
         for (int k = 0; k < P.spp; ++k) acc = add(acc, mk(col[3 * (t + k)], col[3 * (t + k) + 1], col[3 * (t + k) + 2]));
-        const float fs = (float)P.spp;
+        // x / 2^k and x * 2^-k are the same correctly rounded value (the exact quotients are
+        // equal), so the power-of-two divide is a multiply here.
+        const float rs = 1.0f / (float)P.spp;
         float* o = P.rgb + ((size_t)r * P.W + x) * 3;
-        o[0] = acc.x / fs;
-        o[1] = acc.y / fs;
-        o[2] = acc.z / fs;
+        o[0] = acc.x * rs;
+        o[1] = acc.y * rs;
+        o[2] = acc.z * rs;
     }
 }
 
@@ -975,6 +978,8 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     int th = ppb / tw;
     P.tile_w = tw;
     P.tile_h = th;
+    P.tile_w_log2 = __builtin_ctz(unsigned(tw));
+    P.spp_log2 = samples ? __builtin_ctz(unsigned(o->spp)) : 0;
     P.tiles_x = (W + tw - 1) / tw;
     const int tiles_y = (rows + th - 1) / th;
     P.tiles_total = P.tiles_x * tiles_y;
@@ -1166,5 +1171,20 @@ extern "C" int rt_powf_batch(int device, const float* x, const float* y, int n, 
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out, dout.p, size_t(n) * sizeof(float), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+extern "C" int rt_box_test_host(const float* rays, const float* boxes, const float* tminmax, int n,
+                                int32_t* out_fast, int32_t* out_exact, int32_t* out_class) {
+    if (n < 0 || (n > 0 && (!rays || !boxes || !tminmax || !out_fast || !out_exact || !out_class)))
+        return set_error(RT_ERR_ARG, "rt_box_test_host: bad args");
+    for (int i = 0; i < n; ++i) {
+        const float* R = rays + 6 * i;
+        const float* B = boxes + 6 * i;
+        const RayPre r = make_ray(mk(R[0], R[1], R[2]), mk(R[3], R[4], R[5]));
+        out_class[i] = box_classify(r, B, B + 3, tminmax[2 * i], tminmax[2 * i + 1]);
+        out_fast[i] = box_hit(r, B[0], B[1], B[2], B[3], B[4], B[5], tminmax[2 * i], tminmax[2 * i + 1]) ? 1 : 0;
+        out_exact[i] = box_hit_exact(r, B, B + 3, (double)tminmax[2 * i], (double)tminmax[2 * i + 1]) ? 1 : 0;
+    }
     return RT_OK;
 }

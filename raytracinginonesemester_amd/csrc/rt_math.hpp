@@ -16,76 +16,75 @@ struct f3 {
     float x, y, z;
 };
 
-__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
-__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ f3 mul(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ f3 scale(f3 v, float t) { return mk(v.x * t, v.y * t, v.z * t); }
-__device__ __forceinline__ float dot(f3 u, f3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
-__device__ __forceinline__ f3 cross(f3 u, f3 v) {
+__host__ __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__host__ __device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__host__ __device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__host__ __device__ __forceinline__ f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
+__host__ __device__ __forceinline__ f3 mul(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__host__ __device__ __forceinline__ f3 scale(f3 v, float t) { return mk(v.x * t, v.y * t, v.z * t); }
+__host__ __device__ __forceinline__ float dot(f3 u, f3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
+__host__ __device__ __forceinline__ f3 cross(f3 u, f3 v) {
     return mk(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
 }
 // Vec3 / double(len) == correctly rounded f32 division (vec3.h:334).
-__device__ __forceinline__ f3 divf(f3 v, float t) { return mk(v.x / t, v.y / t, v.z / t); }
+__host__ __device__ __forceinline__ f3 divf(f3 v, float t) { return mk(v.x / t, v.y / t, v.z / t); }
 // unit_vector (vec3.h:345-348) and normalize (vec3.h:343) round identically.
-__device__ __forceinline__ f3 unit(f3 v) {
+__host__ __device__ __forceinline__ f3 unit(f3 v) {
     const float len = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
     return divf(v, len);
 }
 // Camera::unit_vector with the 1e-12 fallback (camera.h:218-223).
-__device__ __forceinline__ f3 cam_unit(f3 v) {
+__host__ __device__ __forceinline__ f3 cam_unit(f3 v) {
     const float len = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
     if ((double)len < 1e-12) return mk(0.0f, 0.0f, 1.0f);
     return divf(v, len);
 }
 
-// Per-ray constants of intersectAABB (bvh.h:81-129): the reference recomputes
-// 1.0/double(dir) at every test; it depends on the ray only, so it is hoisted here
-// (same double value, bit for bit).
+// A ray as the slab test needs it.  `par` bit a: |dir[a]| < 1e-8f, where intersectAABB
+// degenerates to an exact inside test on that axis (bvh.h:90-91).  `invf` is a float
+// reciprocal of the direction (any <= 2 ulp approximation), used only by the conservative
+// pre-classification below, never to decide an ambiguous case.
 struct RayPre {
     f3 o, d;
-    double od[3];
-    double inv[3];
-    uint32_t par;  // bit a set: |dir[a]| < 1e-8f (slab degenerates to an inside test)
+    f3 invf;
+    uint32_t par;
 };
 
-__device__ __forceinline__ RayPre make_ray(f3 o, f3 d) {
+__host__ __device__ __forceinline__ float rcp_approx(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);  // v_rcp_f32, 1 ulp
+#else
+    return 1.0f / x;
+#endif
+}
+
+__host__ __device__ __forceinline__ RayPre make_ray(f3 o, f3 d) {
     RayPre r;
     r.o = o;
     r.d = d;
-    r.od[0] = (double)o.x;
-    r.od[1] = (double)o.y;
-    r.od[2] = (double)o.z;
     const float eps = 1e-8f;
-    r.par = 0;
-    const float dd[3] = {d.x, d.y, d.z};
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        if (fabsf(dd[a]) < eps) {
-            r.par |= 1u << a;
-            r.inv[a] = 0.0;
-        } else {
-            r.inv[a] = 1.0 / (double)dd[a];
-        }
-    }
+    r.par = (fabsf(d.x) < eps ? 1u : 0u) | (fabsf(d.y) < eps ? 2u : 0u) | (fabsf(d.z) < eps ? 4u : 0u);
+    r.invf = mk(rcp_approx(d.x), rcp_approx(d.y), rcp_approx(d.z));
     return r;
 }
 
-// intersectAABB(ray, box, tmin, tmax) — double slabs, reference compare/swap order.
-__device__ __forceinline__ bool box_hit(const RayPre& r, float mnx, float mny, float mnz, float mxx,
-                                        float mxy, float mxz, double tmin, double tmax) {
+// intersectAABB(ray, box, tmin, tmax) exactly as the reference evaluates it (bvh.h:81-129):
+// per axis inv = 1.0/double(dir), tNear/tFar = (double(bound) - double(orig)) * inv,
+// reference compare/swap order.  The boolean equals the reference's early-return form
+// because t0 only grows and t1 only shrinks.
+__host__ __device__ inline bool box_hit_exact(const RayPre& r, const float mn[3], const float mx[3], double tmin,
+                                              double tmax) {
     double t0 = tmin, t1 = tmax;
-    const float mn[3] = {mnx, mny, mnz}, mx[3] = {mxx, mxy, mxz};
-    const float o[3] = {r.o.x, r.o.y, r.o.z};
+    const float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
     bool ok = true;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         if (r.par & (1u << a)) {
             ok = ok && !(o[a] < mn[a] || o[a] > mx[a]);
         } else {
-            double tn = ((double)mn[a] - r.od[a]) * r.inv[a];
-            double tf = ((double)mx[a] - r.od[a]) * r.inv[a];
+            const double inv = 1.0 / (double)d[a];
+            double tn = ((double)mn[a] - (double)o[a]) * inv;
+            double tf = ((double)mx[a] - (double)o[a]) * inv;
             if (tn > tf) {
                 const double tmp = tn;
                 tn = tf;
@@ -93,15 +92,64 @@ __device__ __forceinline__ bool box_hit(const RayPre& r, float mnx, float mny, f
             }
             if (tn > t0) t0 = tn;
             if (tf < t1) t1 = tf;
-            ok = ok && !(t0 > t1);  // monotone: an early return gives the same boolean
+            ok = ok && !(t0 > t1);
         }
     }
     return ok;
 }
 
+// Conservative float pre-classification of the same test: MISS / HIT are returned only when
+// the reference's double computation is guaranteed to give that answer; AMBIG otherwise.
+// Error budget (finite inputs): the reference's tNear/tFar carry <= 3 double roundings
+// (<= 3.4e-16 relative to the exact (bound-orig)/dir), the float estimates here <= 3 float
+// roundings + a 1-ulp reciprocal (<= 3.6e-7), and the +-E adjustments below one more float
+// rounding; E = 4e-6 * max(|tn'|,|tf'|) + 1e-30 bounds their distance with > 10x slack (the
+// 1e-30 term covers subnormal absolute error).  With Lmax = max over axes of the exact
+// reference lows, Hmin = min of the highs (tmin/tmax are exact in both precisions):
+//   MISS  if max(tmin, lo'-E) > min(tmax, hi'+E)      (then Lmax > Hmin: reference rejects)
+//   HIT   if max(tmin, lo'+E) <= min(tmax, hi'-E)     (then Lmax <= Hmin: reference accepts)
+// A non-finite estimate (coordinates near FLT_MAX) never yields HIT; NaN compares false and
+// falls to AMBIG.  Parallel axes use the reference's exact float inside test.
+enum : int { BOX_MISS = 0, BOX_HIT = 1, BOX_AMBIG = 2 };
+__host__ __device__ __forceinline__ int box_classify(const RayPre& r, const float mn[3], const float mx[3],
+                                                     float tmin, float tmax) {
+    const float o[3] = {r.o.x, r.o.y, r.o.z}, iv[3] = {r.invf.x, r.invf.y, r.invf.z};
+    float lowLo = tmin, lowHi = tmin, highLo = tmax, highHi = tmax;
+    bool inside = true, finite = true;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (r.par & (1u << a)) {
+            inside = inside && !(o[a] < mn[a] || o[a] > mx[a]);
+        } else {
+            const float tn = (mn[a] - o[a]) * iv[a];
+            const float tf = (mx[a] - o[a]) * iv[a];
+            const float lo = fminf(tn, tf), hi = fmaxf(tn, tf);
+            const float E = 4e-6f * fmaxf(fabsf(tn), fabsf(tf)) + 1e-30f;
+            finite = finite && (E < 3.0e38f);
+            lowLo = fmaxf(lowLo, lo - E);
+            lowHi = fmaxf(lowHi, lo + E);
+            highLo = fminf(highLo, hi - E);
+            highHi = fminf(highHi, hi + E);
+        }
+    }
+    if (!inside) return BOX_MISS;
+    if (lowLo > highHi) return BOX_MISS;
+    if (finite && lowHi <= highLo) return BOX_HIT;
+    return BOX_AMBIG;
+}
+
+// intersectAABB with the float fast path; bit-identical answer to box_hit_exact.
+__host__ __device__ __forceinline__ bool box_hit(const RayPre& r, float mnx, float mny, float mnz, float mxx,
+                                                 float mxy, float mxz, float tmin, float tmax) {
+    const float mn[3] = {mnx, mny, mnz}, mx[3] = {mxx, mxy, mxz};
+    const int c = box_classify(r, mn, mx, tmin, tmax);
+    if (c != BOX_AMBIG) return c == BOX_HIT;
+    return box_hit_exact(r, mn, mx, (double)tmin, (double)tmax);
+}
+
 // Möller–Trumbore of intersectTriangle (query.h:72-108) with e1 = v1-v0, e2 = v2-v0
 // precomputed on the host (same float subtraction).  Returns hit and t/u/v.
-__device__ __forceinline__ bool mt_g(const RayPre& r, f3 v0, f3 e1, f3 e2, float tmin, float tmax,
+__host__ __device__ __forceinline__ bool mt_g(const RayPre& r, f3 v0, f3 e1, f3 e2, float tmin, float tmax,
                                      float& t_out, float& u_out, float& v_out) {
     const f3 pvec = cross(r.d, e2);
     const float det = dot(e1, pvec);
@@ -122,7 +170,7 @@ __device__ __forceinline__ bool mt_g(const RayPre& r, f3 v0, f3 e1, f3 e2, float
 }
 
 // HW1 ray_intersection (HW1/include/ray.h:67-104): eps = FLT_EPSILON, t >= 0, no tmax.
-__device__ __forceinline__ bool mt_hw1(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& t_out, float& u_out,
+__host__ __device__ __forceinline__ bool mt_hw1(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& t_out, float& u_out,
                                        float& v_out) {
     const f3 pvec = cross(d, e2);
     const float det = dot(pvec, e1);
@@ -143,7 +191,7 @@ __device__ __forceinline__ bool mt_hw1(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& t
 }
 
 // Hit-record completion of intersectTriangle (query.h:110-127) for the winning triangle.
-__device__ __forceinline__ void hit_frame(const RayPre& r, f3 e1, f3 e2, f3 n0, f3 n1, f3 n2, float t,
+__host__ __device__ __forceinline__ void hit_frame(const RayPre& r, f3 e1, f3 e2, f3 n0, f3 n1, f3 n2, float t,
                                           float u, float v, f3& p, f3& shadingN) {
     p = add(r.o, scale(r.d, t));
     f3 geomN = unit(cross(e1, e2));
@@ -161,7 +209,7 @@ __device__ __forceinline__ void hit_frame(const RayPre& r, f3 e1, f3 e2, f3 n0, 
 }
 
 // G/include/query.h:32-48
-__device__ __forceinline__ float rng_next(uint32_t& state) {
+__host__ __device__ __forceinline__ float rng_next(uint32_t& state) {
     state = state * 1664525u + 1013904223u;
     uint32_t h = state;
     h = (h ^ 61u) ^ (h >> 16u);
@@ -171,10 +219,10 @@ __device__ __forceinline__ float rng_next(uint32_t& state) {
     h ^= h >> 15u;
     return (float)h / (float)0xFFFFFFFFu;
 }
-__device__ __forceinline__ uint32_t make_rng_seed(int x, int y, int s) {
+__host__ __device__ __forceinline__ uint32_t make_rng_seed(int x, int y, int s) {
     return (uint32_t)x * 73856093u ^ (uint32_t)y * 19349663u ^ (uint32_t)s * 83492791u;
 }
-__device__ __forceinline__ f3 random_unit_vector(uint32_t& st) {
+__host__ __device__ __forceinline__ f3 random_unit_vector(uint32_t& st) {
     for (;;) {
         const float x = 2.0f * rng_next(st) - 1.0f;
         const float y = 2.0f * rng_next(st) - 1.0f;
@@ -342,7 +390,7 @@ __host__ __device__ inline float ref_powf(float x, float y) {
     return exp2_inline(ylogx, sign_bias);
 }
 
-__device__ __forceinline__ f3 clamp01(f3 c) {  // shader.h:24-32
+__host__ __device__ __forceinline__ f3 clamp01(f3 c) {  // shader.h:24-32
     if (c.x > 1.0f) c.x = 1.0f;
     if (c.y > 1.0f) c.y = 1.0f;
     if (c.z > 1.0f) c.z = 1.0f;

@@ -157,7 +157,8 @@ size_t rt_scene_device_bytes(const rt_scene* s);
 enum {
     RT_KERNEL_AUTO = 0,      /* the fastest parity-equivalent kernel */
     RT_KERNEL_WAVE = 1,      /* wave-coherent masked DFS (shared per-wave stack) */
-    RT_KERNEL_LANE = 2       /* one private DFS stack per lane (baseline variant) */
+    RT_KERNEL_LANE = 2,      /* one private DFS stack per lane (baseline variant) */
+    RT_KERNEL_WAVE_PIXELS = 3 /* WAVE traversal, one pixel per lane looping over its samples */
 };
 
 typedef struct {

@@ -17,7 +17,7 @@ RT_ERR = {
     -1: "RT_ERR_ARG", -2: "RT_ERR_IO", -3: "RT_ERR_PARSE", -4: "RT_ERR_HIP",
     -5: "RT_ERR_NOMEM", -6: "RT_ERR_NODEVICE", -7: "RT_ERR_UNSUPPORTED",
 }
-RT_KERNEL_AUTO, RT_KERNEL_WAVE, RT_KERNEL_LANE = 0, 1, 2
+RT_KERNEL_AUTO, RT_KERNEL_WAVE, RT_KERNEL_LANE, RT_KERNEL_WAVE_PIXELS = 0, 1, 2, 3
 RT_TILES_AUTO, RT_TILES_LINEAR, RT_TILES_XCD_CHUNK, RT_TILES_ROWS = 0, 1, 2, 3
 
 

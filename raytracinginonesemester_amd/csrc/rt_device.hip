@@ -460,7 +460,7 @@ __device__ __forceinline__ int tile_of_block(int b, int nblocks, int order, int 
 // One sample per lane: a block covers tile_w x tile_h pixels x spp samples (spp a power
 // of two <= 256, tile_w*tile_h*spp == BLOCK); per-pixel sums run in sample order from LDS.
 template <int MODE>
-__global__ __launch_bounds__(BLOCK) void render_samples_kernel(RenderParams P) {
+__global__ __launch_bounds__(BLOCK, 4) void render_samples_kernel(RenderParams P) {
     __shared__ float col[BLOCK * 3];
     const int tile = tile_of_block((int)blockIdx.x, (int)gridDim.x, P.tile_order, P.tiles_x);
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
@@ -499,7 +499,7 @@ __global__ __launch_bounds__(BLOCK) void render_samples_kernel(RenderParams P) {
 
 // General spp: one pixel per lane looping over its samples in order (query.cu:146-163).
 template <int MODE>
-__global__ __launch_bounds__(BLOCK) void render_pixels_kernel(RenderParams P) {
+__global__ __launch_bounds__(BLOCK, 4) void render_pixels_kernel(RenderParams P) {
     const int tile = tile_of_block((int)blockIdx.x, (int)gridDim.x, P.tile_order, P.tiles_x);
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int t = (int)threadIdx.x;
@@ -971,7 +971,7 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     P.rgb = rgb;
     P.hit_idx = hit_idx;
     P.hit_t = hit_t;
-    const bool samples = o->spp <= BLOCK && (o->spp & (o->spp - 1)) == 0;
+    const bool samples = o->kernel != RT_KERNEL_WAVE_PIXELS && o->spp <= BLOCK && (o->spp & (o->spp - 1)) == 0;
     int ppb = samples ? BLOCK / o->spp : BLOCK;  // pixels per block
     int tw = 1;
     while (tw * tw < ppb) tw <<= 1;                // square-ish power-of-two tile

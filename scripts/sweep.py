@@ -33,7 +33,7 @@ sp = configs.scene_path(cfg["scene"])
 hs = rt.HostScene.load_json(sp, REPO if sp.parent == configs.SCENES else sp.parent)
 cam = hs.camera(cfg["width"], cfg["height"])
 ds = rt.DeviceScene.from_host(hs)
-K = {"wave": rt.RT_KERNEL_WAVE, "lane": rt.RT_KERNEL_LANE}
+K = {"wave": rt.RT_KERNEL_WAVE, "lane": rt.RT_KERNEL_LANE, "wavepix": rt._lib.RT_KERNEL_WAVE_PIXELS}
 T = {"linear": rt.RT_TILES_LINEAR, "xcd_chunk": rt.RT_TILES_XCD_CHUNK, "rows": rt.RT_TILES_ROWS}
 variants = list(itertools.product(a.kernels.split(","), a.tiles.split(",")))
 times = {v: [] for v in variants}

@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--kernel", default="auto", choices=["auto", "wave", "lane"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: CPU-staged gather (lets N ranks share one GPU to exercise the N>1 path)")
     ap.add_argument("--traffic-file", default=str(REPO / "profiles" / "traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (see DESIGN.md)")
     return ap.parse_args()
@@ -98,10 +100,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)  # gloo rehearsal: several ranks may share one GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     cfg = configs.G_CONFIGS[a.config]
     sp = configs.scene_path(cfg["scene"])
@@ -116,13 +123,16 @@ def main():
     rows_of = [lib.rt_shard_rows(H, BAND_ROWS, r, world) for r in range(world)]
     max_rows = max(rows_of)
     strip = torch.zeros((max_rows, W, 3), dtype=torch.float32, device=dev)
-    gather = [torch.empty_like(strip) for _ in range(world)] if (world > 1 and rank == 0) else None
+    gdev = dev if a.backend == "nccl" else torch.device("cpu")
+    gather = [torch.empty(strip.shape, dtype=strip.dtype, device=gdev) for _ in range(world)] \
+        if (world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def step():
         ds.render_device(cam, opts, strip.data_ptr(), stream=stream)
         if world > 1:
-            dist.gather(strip, gather_list=gather, dst=0)
+            src = strip if a.backend == "nccl" else strip.cpu()
+            dist.gather(src, gather_list=gather, dst=0)
 
     for _ in range(a.warmup):
         step()
@@ -137,9 +147,9 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=gdev)
     kt = ds.kernel_times(a.steps)
-    kmean = torch.tensor([float(kt.mean()) if len(kt) else float("nan")], dtype=torch.float64, device=dev)
+    kmean = torch.tensor([float(kt.mean()) if len(kt) else float("nan")], dtype=torch.float64, device=gdev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
         dist.all_reduce(kmean, op=dist.ReduceOp.MAX)
@@ -187,10 +197,12 @@ def main():
         "dtype": "f32+f64",
         "data": "synthetic=false: frog.obj scene (reference asset), camera/light from frog.json"
                 if a.config == "c3" else "synthetic seeded 1,048,576-triangle heightfield",
-        "config": {"workload": f"{a.config}: {cfg['scene']} {W}x{H}x{spp}spp max_bounces={cfg['max_depth']}, "
+        "config": {"workload": f"{a.config if world == 1 else 'c4'}: {cfg['scene']} {W}x{H}x{spp}spp "
+                               f"max_bounces={cfg['max_depth']}, "
                                f"Lambert/Blinn-Phong + 1 hard shadow ray per light",
                    "triangles": hs.num_triangles, "bands": f"{BAND_ROWS}-row bands round-robin over {world} GPU(s)",
-                   "gather": "RCCL gather to rank 0" if world > 1 else None,
+                   "gather": (f"{'RCCL' if a.backend == 'nccl' else 'gloo (CPU-staged)'} gather to rank 0"
+                              if world > 1 else None),
                    "kernel": a.kernel},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,

@@ -173,7 +173,12 @@ typedef struct {
     int32_t band_rows, band_index, band_count;
     int32_t kernel;           /* RT_KERNEL_* */
     int32_t tile_order;       /* RT_TILES_*: block -> pixel-tile order (speed only) */
+    int32_t flags;            /* RT_FLAG_* */
 } rt_render_opts;
+
+enum {
+    RT_FLAG_NO_CULL = 1       /* disable tile culling against the root box (A/B; same output) */
+};
 
 enum {
     RT_TILES_AUTO = 0,        /* RT_TILES_ROWS */

@@ -19,6 +19,7 @@ RT_ERR = {
 }
 RT_KERNEL_AUTO, RT_KERNEL_WAVE, RT_KERNEL_LANE, RT_KERNEL_WAVE_PIXELS = 0, 1, 2, 3
 RT_TILES_AUTO, RT_TILES_LINEAR, RT_TILES_XCD_CHUNK, RT_TILES_ROWS = 0, 1, 2, 3
+RT_FLAG_NO_CULL = 1
 
 
 class RTError(RuntimeError):
@@ -92,7 +93,7 @@ class RenderOpts(C.Structure):
     _fields_ = [("max_depth", C.c_int32), ("spp", C.c_int32), ("diffuse_bounce", C.c_int32),
                 ("miss_color", Vec3), ("jitter", C.c_void_p), ("band_rows", C.c_int32),
                 ("band_index", C.c_int32), ("band_count", C.c_int32), ("kernel", C.c_int32),
-                ("tile_order", C.c_int32)]
+                ("tile_order", C.c_int32), ("flags", C.c_int32)]
 
 
 P = C.c_void_p

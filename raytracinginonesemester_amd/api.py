@@ -219,7 +219,7 @@ class DeviceScene:
     @staticmethod
     def make_opts(spp: int = 1, max_depth: int = 1, diffuse_bounce: bool = True, miss_color=(0, 0, 0),
                   jitter=None, band_rows: int = 8, band_index: int = 0, band_count: int = 1,
-                  kernel: int = L.RT_KERNEL_AUTO, tile_order: int = L.RT_TILES_AUTO):
+                  kernel: int = L.RT_KERNEL_AUTO, tile_order: int = L.RT_TILES_AUTO, flags: int = 0):
         o = L.RenderOpts()
         lib().rt_render_opts_default(C.byref(o))
         o.spp, o.max_depth, o.diffuse_bounce = int(spp), int(max_depth), 1 if diffuse_bounce else 0
@@ -230,15 +230,16 @@ class DeviceScene:
             o.jitter = jit.ctypes.data
         o.band_rows, o.band_index, o.band_count, o.kernel = int(band_rows), int(band_index), int(band_count), int(kernel)
         o.tile_order = int(tile_order)
+        o.flags = int(flags)
         return o, jit
 
     def render(self, camera: Camera, spp: int = 1, max_depth: int = 1, diffuse_bounce: bool = True,
                miss_color=(0, 0, 0), jitter=None, aov: bool = False, band_rows: int = 8,
                band_index: int = 0, band_count: int = 1, kernel: int = L.RT_KERNEL_AUTO,
-               tile_order: int = L.RT_TILES_AUTO):
+               tile_order: int = L.RT_TILES_AUTO, flags: int = 0):
         """Synchronous render to host: (rows, W, 3) float32 [+ (rows, W, spp) hit idx / t]."""
         o, _jit = self.make_opts(spp, max_depth, diffuse_bounce, miss_color, jitter, band_rows, band_index,
-                                 band_count, kernel, tile_order)
+                                 band_count, kernel, tile_order, flags)
         W = camera.pixel_width
         rows = lib().rt_shard_rows(camera.pixel_height, o.band_rows, o.band_index, o.band_count)
         if rows < 0:

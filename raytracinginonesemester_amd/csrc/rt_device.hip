@@ -83,6 +83,7 @@ struct RenderParams {
     int32_t lane_samples;                             // 1: one sample per lane; else pixel loop
     int32_t tile_order;                               // RT_TILES_*
     int32_t spp_log2, tile_w_log2;                    // samples kernel: both powers of two
+    int32_t cull;                                     // tile culling against the root box
     float* __restrict__ rgb;
     int32_t* __restrict__ hit_idx;
     float* __restrict__ hit_t;
@@ -429,6 +430,72 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
     return clamp01(radiance);
 }
 
+// ---- tile culling ---------------------------------------------------------------------
+// True only if every camera ray of pixels [x0,x1] x rows [y0,y1] provably fails the root
+// test of SearchBVH (intersectAABB(ray, root box, 1e-4, FLT_MAX), bvh.h:81-129), so the whole
+// tile's samples are misses.  Ray directions are positive multiples of
+// D(px,py) = pixel00 + px*du + py*dv - center with px in [x0-0.5, x1+0.5) (jitter), an affine
+// map: its per-component range over the (1-pixel-padded) tile comes from the corners, widened
+// by 1e-5*|D| plus 8 float ulps of every term to cover the float rounding of the per-sample
+// computation (pixel position, difference, cam_unit).  Scaling d by k > 0 scales every slab
+// parameter by 1/k, so "some axis's entry > another axis's exit" is scale-free.  An axis whose
+// component can come near 0 (|d_a| < 1e-6 |d|, far above the 1e-8 parallel threshold) is
+// ignored (no constraint): conservative.  Culled iff, with 1e-9 relative slack (the
+// reference's doubles carry ~1e-15), some axis's smallest entry exceeds some axis's largest
+// exit, or some axis's largest exit is < 0 (< tmin).  The camera inside the padded box never
+// culls.
+__device__ __forceinline__ bool tile_misses_root(const RenderParams& P, int x0, int x1, int y0, int y1) {
+    const double c[3] = {P.cam_center.x, P.cam_center.y, P.cam_center.z};
+    const double p0[3] = {P.cam_p00.x, P.cam_p00.y, P.cam_p00.z};
+    const double du[3] = {P.cam_du.x, P.cam_du.y, P.cam_du.z};
+    const double dv[3] = {P.cam_dv.x, P.cam_dv.y, P.cam_dv.z};
+    const double pxl = x0 - 1.0, pxh = x1 + 1.0, pyl = y0 - 1.0, pyh = y1 + 1.0;
+    const double pxm = fmax(fabs(pxl), fabs(pxh)), pym = fmax(fabs(pyl), fabs(pyh));
+    double Dl[3], Dh[3], scale = 0.0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double base = p0[a] - c[a];
+        const double u0 = pxl * du[a], u1 = pxh * du[a], v0 = pyl * dv[a], v1 = pyh * dv[a];
+        const double ulp = 8.0 * 1.1920928955078125e-7 * (fabs(c[a]) + fabs(p0[a]) + pxm * fabs(du[a]) + pym * fabs(dv[a]));
+        Dl[a] = base + fmin(u0, u1) + fmin(v0, v1) - ulp;
+        Dh[a] = base + fmax(u0, u1) + fmax(v0, v1) + ulp;
+        scale = fmax(scale, fmax(fabs(Dl[a]), fabs(Dh[a])));
+    }
+    const float* rb = P.sc.root_box;
+    const double mn[3] = {rb[0], rb[1], rb[2]}, mx[3] = {rb[3], rb[4], rb[5]};
+    bool inside = true;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        Dl[a] -= 1e-5 * scale;
+        Dh[a] += 1e-5 * scale;
+        const double tol = 1e-6 * (fabs(mn[a]) + fabs(mx[a]) + fabs(c[a])) + 1e-30;
+        inside = inside && c[a] >= mn[a] - tol && c[a] <= mx[a] + tol;
+    }
+    if (inside || !(scale > 0.0) || !(mn[0] <= mx[0] && mn[1] <= mx[1] && mn[2] <= mx[2])) return false;
+    double entry_min = -INFINITY, exit_max = INFINITY;  // max over axes of min entry; min of max exit
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (!(Dl[a] > 1e-6 * scale || Dh[a] < -1e-6 * scale)) continue;  // may be ~parallel
+        const double nA = mn[a] - c[a], xA = mx[a] - c[a];
+        // d > 0: entry (mn-c)/d, exit (mx-c)/d; d < 0: swapped.  Over d in [Dl, Dh] each
+        // quotient is monotone in d, so its range sits at the endpoints.
+        const double e0 = (Dl[a] > 0 ? nA : xA) / Dl[a], e1 = (Dl[a] > 0 ? nA : xA) / Dh[a];
+        const double f0 = (Dl[a] > 0 ? xA : nA) / Dl[a], f1 = (Dl[a] > 0 ? xA : nA) / Dh[a];
+        entry_min = fmax(entry_min, fmin(e0, e1));
+        exit_max = fmin(exit_max, fmax(f0, f1));
+    }
+    if (!(exit_max == exit_max) || !(entry_min == entry_min)) return false;
+    if (exit_max < -1e-9 * fabs(exit_max) - 1e-30) return true;
+    return entry_min - exit_max > 1e-9 * (fabs(entry_min) + fabs(exit_max)) + 1e-30;
+}
+
+// What a sample that misses the root returns: clamp(0 + (1,1,1) * missColor) (query.h:181-183),
+// or 0 when max_depth <= 0 (query.h:172).
+__device__ __forceinline__ f3 miss_sample_color(const RenderParams& P) {
+    if (P.max_depth <= 0) return mk(0.f, 0.f, 0.f);
+    return clamp01(add(mk(0.f, 0.f, 0.f), mul(mk(1.f, 1.f, 1.f), P.miss)));
+}
+
 // Local row -> image row for the band sharding of rt_render_opts.
 __device__ __forceinline__ int global_row(const RenderParams& P, int r) {
     if (P.band_count <= 1) return r;
@@ -473,7 +540,12 @@ __global__ __launch_bounds__(BLOCK, 4) void render_samples_kernel(RenderParams P
     const int y = valid ? global_row(P, r) : 0;
     int32_t pidx = -1;
     float pt = -1.f;
-    const f3 c = trace_sample<MODE>(P, valid, x, y, s, &pidx, &pt);
+    // block-uniform: the whole tile provably misses the scene's root box
+    const int xa = tx * P.tile_w, ra = ty * P.tile_h;
+    const bool culled = P.cull && xa < P.W && ra < P.rows &&
+                        tile_misses_root(P, xa, min(xa + P.tile_w, P.W) - 1, global_row(P, ra),
+                                         global_row(P, min(ra + P.tile_h, P.rows) - 1));
+    const f3 c = culled ? miss_sample_color(P) : trace_sample<MODE>(P, valid, x, y, s, &pidx, &pt);
     if (valid && P.hit_idx) {
         const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp + (size_t)s;
         P.hit_idx[k] = pidx;
@@ -507,11 +579,15 @@ __global__ __launch_bounds__(BLOCK, 4) void render_pixels_kernel(RenderParams P)
     const int r = ty * P.tile_h + t / P.tile_w;
     const bool valid = x < P.W && r < P.rows;
     const int y = valid ? global_row(P, r) : 0;
+    const int xa = tx * P.tile_w, ra = ty * P.tile_h;
+    const bool culled = P.cull && xa < P.W && ra < P.rows &&
+                        tile_misses_root(P, xa, min(xa + P.tile_w, P.W) - 1, global_row(P, ra),
+                                         global_row(P, min(ra + P.tile_h, P.rows) - 1));
     f3 acc = mk(0.f, 0.f, 0.f);
     for (int s = 0; s < P.spp; ++s) {
         int32_t pidx = -1;
         float pt = -1.f;
-        const f3 c = trace_sample<MODE>(P, valid, x, y, s, &pidx, &pt);
+        const f3 c = culled ? miss_sample_color(P) : trace_sample<MODE>(P, valid, x, y, s, &pidx, &pt);
         if (valid && P.hit_idx) {
             const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp + (size_t)s;
             P.hit_idx[k] = pidx;
@@ -888,6 +964,7 @@ extern "C" void rt_render_opts_default(rt_render_opts* o) {
     o->band_count = 1;
     o->kernel = RT_KERNEL_AUTO;
     o->tile_order = RT_TILES_AUTO;
+    o->flags = 0;
 }
 
 extern "C" int rt_shard_rows(int H, int band_rows, int band_index, int band_count) {
@@ -985,6 +1062,7 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     P.tiles_total = P.tiles_x * tiles_y;
     P.lane_samples = samples ? 1 : 0;
     P.tile_order = o->tile_order == RT_TILES_AUTO ? RT_TILES_ROWS : o->tile_order;
+    P.cull = (o->flags & RT_FLAG_NO_CULL) ? 0 : 1;
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int slot = int(s->launches % rt_scene::kRing);

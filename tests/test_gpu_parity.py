@@ -240,3 +240,27 @@ def test_full_size_properties_c5():
                            hs.tri_object_ids, hs.materials, hs.lights, spp=64, max_depth=1, miss=miss,
                            rows=(y0, y0 + 2))
         _check_fb(rgb[y0:y0 + 2], ref[y0:y0 + 2])
+
+
+@pytest.mark.parametrize("scene", ["frog.json", "cornell.json", "sphere_single.json"])
+def test_tile_culling_changes_nothing(scene):
+    """Tile culling against the root box is exact: random cameras (near, far, inside the box,
+    grazing, far from the origin) give bit-identical frames and hit AOVs with it on and off."""
+    hs = host_scene(scene)
+    ds = _device_scene(scene)
+    box = np.concatenate([hs.aabbs[0, :3], hs.aabbs[0, 3:]])
+    ctr = (box[:3] + box[3:]) / 2
+    ext = np.linalg.norm(box[3:] - box[:3])
+    rng = np.random.default_rng(11)
+    for k in range(12):
+        dist_ = ext * rng.choice([0.3, 0.8, 2.0, 10.0, 200.0])
+        pos = ctr + rng.normal(size=3) * dist_
+        look = ctr + rng.normal(size=3) * ext * rng.choice([0.0, 0.5, 3.0])
+        if k == 0:
+            pos = ctr  # inside the box
+        up = (0.0, 0.0, 1.0) if k % 2 else (0.0, 1.0, 0.0)
+        cam = rt.Camera(pos, look, up, float(rng.choice([18.0, 50.0, 300.0])), 24.0, 96, 64)
+        a = ds.render(cam, spp=4, max_depth=1, aov=True)
+        b = ds.render(cam, spp=4, max_depth=1, aov=True, flags=rt._lib.RT_FLAG_NO_CULL)
+        for x, y in zip(a, b):
+            assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), k

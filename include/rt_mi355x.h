@@ -177,7 +177,8 @@ typedef struct {
 } rt_render_opts;
 
 enum {
-    RT_FLAG_NO_CULL = 1       /* disable tile culling against the root box (A/B; same output) */
+    RT_FLAG_NO_CULL = 1,      /* disable tile culling against the root box (A/B; same output) */
+    RT_FLAG_PERSISTENT = 2    /* persistent blocks dequeue live tiles (A/B; same output) */
 };
 
 enum {

@@ -84,6 +84,11 @@ struct RenderParams {
     int32_t tile_order;                               // RT_TILES_*
     int32_t spp_log2, tile_w_log2;                    // samples kernel: both powers of two
     int32_t cull;                                     // tile culling against the root box
+    f3 miss_pixel;                                    // pixel value when all spp samples miss
+    uint32_t* live_count;                             // [k * COUNTER_STRIDE], tile_cull_kernel
+    int32_t* live_tiles;                              // nqueues lists of queue_cap entries
+    int32_t nqueues;
+    int32_t queue_cap;
     float* __restrict__ rgb;
     int32_t* __restrict__ hit_idx;
     float* __restrict__ hit_t;
@@ -503,49 +508,133 @@ __device__ __forceinline__ int global_row(const RenderParams& P, int r) {
     return (P.band_index + k * P.band_count) * P.band_rows + within;
 }
 
-// Block -> tile order.  Dispatch deals blocks round-robin over the 8 XCDs, so blocks b,
-// b+8, b+16 ... share one L2 (a speed property only).  XCD_CHUNK gives each XCD a
-// contiguous 1/8 of the tiles (best L2 sharing, worst balance when the geometry covers a
-// band of the frame); ROWS gives each XCD every 8th row of tiles (neighbouring tiles on one
-// XCD, work spread evenly); LINEAR leaves the dispatcher's order.
-__device__ __forceinline__ int tile_of_block(int b, int nblocks, int order, int tiles_x) {
-    if (order == RT_TILES_LINEAR) return b;
-    const int xcd = b % 8, idx = b / 8;
-    if (order == RT_TILES_XCD_CHUNK) {
-        const int q = nblocks / 8, rr = nblocks % 8;  // bijective for any nblocks
-        return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
-    }
-    // RT_TILES_ROWS: XCD k walks tile rows k, k+8, k+16 ...; the tail (rows that do not fill
-    // a group of 8) falls back to the linear order so the mapping stays a bijection.
-    const int tiles_y = nblocks / tiles_x;
-    const int full = (tiles_y / 8) * 8 * tiles_x;  // blocks covered by whole groups of 8 rows
-    if (b >= full) return b;
-    const int row_in = idx / tiles_x, col = idx % tiles_x;
-    return (row_in * 8 + xcd) * tiles_x + col;
+// ---- tile work lists ---------------------------------------------------------------------
+// Pre-pass, one lane per pixel tile: a tile whose every ray provably misses the root box gets
+// its pixels written here (P.miss_pixel = the reference's sum of spp miss samples / spp; hit
+// AOV -1), every other tile is appended to a live list the render kernels dequeue.
+// There are P.nqueues lists.  Workgroups are dealt round-robin over the 8 XCDs, so with 8
+// lists a block's home list is blockIdx % 8: RT_TILES_ROWS gives XCD k the tile rows k, k+8,
+// ... (neighbouring tiles share an L2, the work spreads evenly); RT_TILES_XCD_CHUNK gives it
+// a contiguous 1/8 of the frame (planned_tile balances uneven lists).
+// RT_TILES_LINEAR is one list in raster order.  The order is a speed property only.
+// Each list has a length counter (appends) and a cursor (persistent dequeue) 128 B apart; the
+// lists' counters sit 256 B apart (separate L2 channels) so the atomics do not serialise.
+constexpr int COUNTER_STRIDE = 64;
+__device__ __forceinline__ int queue_of_tile(const RenderParams& P, int tile) {
+    if (P.nqueues == 1) return 0;
+    if (P.tile_order == RT_TILES_XCD_CHUNK) return (int)((int64_t)tile * 8 / P.tiles_total);
+    return (tile / P.tiles_x) & 7;
 }
 
-// One sample per lane: a block covers tile_w x tile_h pixels x spp samples (spp a power
+__global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
+    const int tile = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    bool live = false;
+    if (tile < P.tiles_total) {
+        const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        const int xa = tx * P.tile_w, ra = ty * P.tile_h;
+        const int xb = min(xa + P.tile_w, P.W) - 1, rb = min(ra + P.tile_h, P.rows) - 1;
+        const bool culled = P.cull && tile_misses_root(P, xa, xb, global_row(P, ra), global_row(P, rb));
+        if (culled) {
+            for (int r = ra; r <= rb; ++r)
+                for (int x = xa; x <= xb; ++x) {
+                    float* o = P.rgb + ((size_t)r * P.W + x) * 3;
+                    o[0] = P.miss_pixel.x;
+                    o[1] = P.miss_pixel.y;
+                    o[2] = P.miss_pixel.z;
+                    if (P.hit_idx) {
+                        const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp;
+                        for (int s = 0; s < P.spp; ++s) {
+                            P.hit_idx[k + s] = -1;
+                            P.hit_t[k + s] = -1.0f;
+                        }
+                    }
+                }
+        } else {
+            live = true;
+        }
+    }
+    // Wave-aggregated append: one atomic per (wave, list).
+    const int q = live ? queue_of_tile(P, tile) : 0;
+    const uint32_t lane = lane_id();
+    uint64_t pending = ballot(live);
+    while (pending != 0) {
+        const uint32_t leader = (uint32_t)__builtin_ctzll(pending);
+        const int lq = rdlane(q, leader);
+        const uint64_t m = pending & ballot(q == lq);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&P.live_count[lq * COUNTER_STRIDE], (uint32_t)__popcll(m));
+        base = rdlane(base, leader);
+        if ((m >> lane) & 1ull)
+            P.live_tiles[(size_t)lq * P.queue_cap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = tile;
+        pending &= ~m;
+    }
+}
+
+// Block -> live tile, without atomics.  The grid has tiles_total blocks, dealt round-robin
+// over the 8 XCDs: block b = 8*i + k runs on XCD k and takes slot i of list k.  Lists longer
+// than their XCD's share of blocks hand their leftover slots, in list order, to the blocks
+// left idle by shorter lists (ranked by XCD, then i); blocks past the live count exit.  The
+// working blocks come first in dispatch order, the idle ones drain behind them.
+__device__ __forceinline__ int planned_tile(const RenderParams& P) {
+    const int b = (int)blockIdx.x;
+    if (P.nqueues == 1) return b < (int)P.live_count[0] ? P.live_tiles[b] : -1;
+    const int G = (int)gridDim.x;
+    const int q = b & 7, i = b >> 3;
+    int c[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = (int)P.live_count[k * COUNTER_STRIDE];
+    if (i < c[q]) return P.live_tiles[(size_t)q * P.queue_cap + i];
+    int r = i - c[q];  // rank among the idle blocks
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (k < q) r += max(0, (G - k + 7) / 8 - c[k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int nk = (G - k + 7) / 8, lk = max(0, c[k] - nk);
+        if (r >= 0 && r < lk) return P.live_tiles[(size_t)k * P.queue_cap + nk + r];
+        r -= lk;
+    }
+    return -1;
+}
+
+// Take the next live tile for a persistent block (thread 0, then broadcast): home list first
+// (blockIdx % 8 is the block's XCD when the whole grid is resident), then the others.  -1
+// once every list is drained; every block gets there, since the lists only shrink while the
+// render kernel runs.
+__device__ __forceinline__ int take_tile(const RenderParams& P, int* tile_sh) {
+    if (threadIdx.x == 0) {
+        int tile = -1;
+        const int home = (int)(blockIdx.x % (uint32_t)P.nqueues);
+        for (int k = 0; k < P.nqueues && tile < 0; ++k) {
+            const int q = home + k < P.nqueues ? home + k : home + k - P.nqueues;
+            uint32_t* cursor = &P.live_count[q * COUNTER_STRIDE + COUNTER_STRIDE / 2];
+            const uint32_t n = __hip_atomic_load(&P.live_count[q * COUNTER_STRIDE], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n) continue;
+            const uint32_t slot = atomicAdd(cursor, 1u);
+            if (slot < n) tile = P.live_tiles[(size_t)q * P.queue_cap + slot];
+        }
+        *tile_sh = tile;
+    }
+    __syncthreads();
+    return *tile_sh;
+}
+
+// One sample per lane: a block covers a tile_w x tile_h pixel tile x spp samples (spp a power
 // of two <= 256, tile_w*tile_h*spp == BLOCK); per-pixel sums run in sample order from LDS.
 template <int MODE>
-__global__ __launch_bounds__(BLOCK, 4) void render_samples_kernel(RenderParams P) {
-    __shared__ float col[BLOCK * 3];
-    const int tile = tile_of_block((int)blockIdx.x, (int)gridDim.x, P.tile_order, P.tiles_x);
-    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+__device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, float* col) {
     const int t = (int)threadIdx.x;
     const int s = t & (P.spp - 1);            // spp and tile_w are powers of two here
     const int pit = t >> P.spp_log2;
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int x = tx * P.tile_w + (pit & (P.tile_w - 1));
     const int r = ty * P.tile_h + (pit >> P.tile_w_log2);
     const bool valid = x < P.W && r < P.rows;
     const int y = valid ? global_row(P, r) : 0;
     int32_t pidx = -1;
     float pt = -1.f;
-    // block-uniform: the whole tile provably misses the scene's root box
-    const int xa = tx * P.tile_w, ra = ty * P.tile_h;
-    const bool culled = P.cull && xa < P.W && ra < P.rows &&
-                        tile_misses_root(P, xa, min(xa + P.tile_w, P.W) - 1, global_row(P, ra),
-                                         global_row(P, min(ra + P.tile_h, P.rows) - 1));
-    const f3 c = culled ? miss_sample_color(P) : trace_sample<MODE>(P, valid, x, y, s, &pidx, &pt);
+    const f3 c = trace_sample<MODE>(P, valid, x, y, s, &pidx, &pt);
     if (valid && P.hit_idx) {
         const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp + (size_t)s;
         P.hit_idx[k] = pidx;
@@ -558,7 +647,8 @@ __global__ __launch_bounds__(BLOCK, 4) void render_samples_kernel(RenderParams P
     if (valid && s == 0) {
         // col = col + TraceRayIterative(...) in sample order, then col / float(spp)
         f3 acc = mk(0.f, 0.f, 0.f);
-        for (int k = 0; k < P.spp; ++k) acc = add(acc, mk(col[3 * (t + k)], col[3 * (t + k) + 1], col[3 * (t + k) + 2]));
+        for (int k = 0; k < P.spp; ++k)
+            acc = add(acc, mk(col[3 * (t + k)], col[3 * (t + k) + 1], col[3 * (t + k) + 2]));
         // x / 2^k and x * 2^-k are the same correctly rounded value (the exact quotients are
         // equal), so the power-of-two divide is a multiply here.
         const float rs = 1.0f / (float)P.spp;
@@ -571,23 +661,18 @@ __global__ __launch_bounds__(BLOCK, 4) void render_samples_kernel(RenderParams P
 
 // General spp: one pixel per lane looping over its samples in order (query.cu:146-163).
 template <int MODE>
-__global__ __launch_bounds__(BLOCK, 4) void render_pixels_kernel(RenderParams P) {
-    const int tile = tile_of_block((int)blockIdx.x, (int)gridDim.x, P.tile_order, P.tiles_x);
-    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+__device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
     const int t = (int)threadIdx.x;
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int x = tx * P.tile_w + t % P.tile_w;
     const int r = ty * P.tile_h + t / P.tile_w;
     const bool valid = x < P.W && r < P.rows;
     const int y = valid ? global_row(P, r) : 0;
-    const int xa = tx * P.tile_w, ra = ty * P.tile_h;
-    const bool culled = P.cull && xa < P.W && ra < P.rows &&
-                        tile_misses_root(P, xa, min(xa + P.tile_w, P.W) - 1, global_row(P, ra),
-                                         global_row(P, min(ra + P.tile_h, P.rows) - 1));
     f3 acc = mk(0.f, 0.f, 0.f);
     for (int s = 0; s < P.spp; ++s) {
         int32_t pidx = -1;
         float pt = -1.f;
-        const f3 c = culled ? miss_sample_color(P) : trace_sample<MODE>(P, valid, x, y, s, &pidx, &pt);
+        const f3 c = trace_sample<MODE>(P, valid, x, y, s, &pidx, &pt);
         if (valid && P.hit_idx) {
             const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp + (size_t)s;
             P.hit_idx[k] = pidx;
@@ -601,6 +686,30 @@ __global__ __launch_bounds__(BLOCK, 4) void render_pixels_kernel(RenderParams P)
         o[0] = acc.x / fs;
         o[1] = acc.y / fs;
         o[2] = acc.z / fs;
+    }
+}
+
+// One block per tile of the frame; blocks past the live count exit at once (planned_tile).
+template <int MODE, bool SAMPLES>
+__global__ __launch_bounds__(BLOCK, 4) void render_tiles_kernel(RenderParams P) {
+    __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
+    const int tile = planned_tile(P);
+    if (tile < 0) return;
+    if constexpr (SAMPLES) samples_tile<MODE>(P, tile, col);
+    else pixels_tile<MODE>(P, tile);
+}
+
+// Persistent blocks (as many as are resident at once) looping over the live lists.
+template <int MODE, bool SAMPLES>
+__global__ __launch_bounds__(BLOCK, 4) void render_persistent_kernel(RenderParams P) {
+    __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
+    __shared__ int tile_sh;
+    for (;;) {
+        const int tile = take_tile(P, &tile_sh);
+        if (tile < 0) break;
+        if constexpr (SAMPLES) samples_tile<MODE>(P, tile, col);
+        else pixels_tile<MODE>(P, tile);
+        __syncthreads();  // tile_sh and col are rewritten by the next tile
     }
 }
 
@@ -792,6 +901,8 @@ struct rt_scene {
     uint32_t root_ref = 0;
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     DevBuf inode, ibox, leaf, tnorm, objids, mats, lights, jitter;
+    DevBuf work;  // live tile list counters + the lists
+    int cus = 256;
     int jitter_spp = -1;
     std::vector<float> jitter_host;
     // Ring of HIP event pairs around each render kernel, recorded on the launch stream.
@@ -918,6 +1029,11 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     std::unique_ptr<rt_scene> s(new (std::nothrow) rt_scene());
     if (!s) return set_error(RT_ERR_NOMEM, "out of memory");
     s->device = device;
+    {
+        hipDeviceProp_t prop;
+        HIP_TRY(hipGetDeviceProperties(&prop, device));
+        s->cus = std::max(1, prop.multiProcessorCount);
+    }
     s->P = P;
     s->nmat = nmat;
     s->nlights = nlights;
@@ -994,10 +1110,39 @@ int prepare_jitter(rt_scene* s, const rt_render_opts* o) {
     return RT_OK;
 }
 
+// RT_FLAG_PERSISTENT: as many blocks as are resident at once (occupancy x CUs), each looping
+// over the live lists; otherwise one block per tile, the blocks past the live count exiting
+// at once (planned_tile).
+template <int MODE, bool SAMPLES>
+int launch_mode(const rt_scene* s, const RenderParams& P, bool persistent, hipStream_t st) {
+    if (!persistent) {
+        hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES>), dim3(P.tiles_total), dim3(BLOCK), 0, st, P);
+        return RT_OK;
+    }
+    int per_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&render_persistent_kernel<MODE, SAMPLES>), BLOCK, 0));
+    const int blocks = std::max(1, std::min(P.tiles_total, std::max(1, per_cu) * s->cus));
+    hipLaunchKernelGGL((render_persistent_kernel<MODE, SAMPLES>), dim3(blocks), dim3(BLOCK), 0, st, P);
+    return RT_OK;
+}
+
 template <int MODE>
-void launch(const RenderParams& P, int blocks, bool samples, hipStream_t st) {
-    if (samples) hipLaunchKernelGGL(render_samples_kernel<MODE>, dim3(blocks), dim3(BLOCK), 0, st, P);
-    else hipLaunchKernelGGL(render_pixels_kernel<MODE>, dim3(blocks), dim3(BLOCK), 0, st, P);
+int launch(const rt_scene* s, const RenderParams& P, bool samples, bool persistent, hipStream_t st) {
+    return samples ? launch_mode<MODE, true>(s, P, persistent, st) : launch_mode<MODE, false>(s, P, persistent, st);
+}
+
+// Host restatement of a pixel whose spp samples all miss the root: each sample is
+// clamp(0 + (1,1,1) * missColor) (query.h:181-183), or 0 when max_depth <= 0 (query.h:172);
+// col accumulates them in order and is divided by float(spp) (query.cu:146-163).
+f3 miss_pixel_value(const rt_render_opts* o) {
+    f3 c = mk(0.f, 0.f, 0.f);
+    if (o->max_depth > 0)
+        c = clamp01(add(mk(0.f, 0.f, 0.f), mul(mk(1.f, 1.f, 1.f), f3{o->miss_color.x, o->miss_color.y, o->miss_color.z})));
+    f3 acc = mk(0.f, 0.f, 0.f);
+    for (int k = 0; k < o->spp; ++k) acc = add(acc, c);
+    const float fs = (float)o->spp;
+    return f3{acc.x / fs, acc.y / fs, acc.z / fs};
 }
 
 }  // namespace
@@ -1063,12 +1208,25 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     P.lane_samples = samples ? 1 : 0;
     P.tile_order = o->tile_order == RT_TILES_AUTO ? RT_TILES_ROWS : o->tile_order;
     P.cull = (o->flags & RT_FLAG_NO_CULL) ? 0 : 1;
+    P.miss_pixel = miss_pixel_value(o);
+    P.nqueues = P.tile_order == RT_TILES_LINEAR ? 1 : 8;
+    P.queue_cap = P.tiles_total;
+    constexpr size_t kCounterBytes = 8 * COUNTER_STRIDE * sizeof(uint32_t);
+    const size_t work_bytes = kCounterBytes + size_t(P.nqueues) * size_t(P.queue_cap) * sizeof(int32_t);
+    if (s->work.n < work_bytes && (rc = s->work.alloc(work_bytes)) != RT_OK) return rc;
+    P.live_count = static_cast<uint32_t*>(s->work.p);
+    P.live_tiles = reinterpret_cast<int32_t*>(static_cast<char*>(s->work.p) + kCounterBytes);
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
+    const bool persistent = (o->flags & RT_FLAG_PERSISTENT) != 0;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int slot = int(s->launches % rt_scene::kRing);
     HIP_TRY(hipEventRecord(s->ev0[slot], st));
-    if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, P.tiles_total, samples, st);
-    else launch<RT_KERNEL_WAVE>(P, P.tiles_total, samples, st);
+    HIP_TRY(hipMemsetAsync(s->work.p, 0, kCounterBytes, st));
+    hipLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, P);
+    HIP_TRY(hipGetLastError());
+    if ((rc = mode == RT_KERNEL_LANE ? launch<RT_KERNEL_LANE>(s, P, samples, persistent, st)
+                                     : launch<RT_KERNEL_WAVE>(s, P, samples, persistent, st)) != RT_OK)
+        return rc;
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(s->ev1[slot], st));
     s->launches++;

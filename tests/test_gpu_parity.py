@@ -28,6 +28,10 @@ pytestmark = pytest.mark.gpu
 
 RGB_TOL = 2e-6
 KERNELS = [rt.RT_KERNEL_WAVE, rt.RT_KERNEL_LANE]
+# (flags, tile order): the launch shapes, all of which must give the same frame
+LAUNCHES = [(0, rt.RT_TILES_AUTO), (rt._lib.RT_FLAG_PERSISTENT, rt.RT_TILES_ROWS),
+            (rt._lib.RT_FLAG_PERSISTENT, rt.RT_TILES_LINEAR), (0, rt.RT_TILES_XCD_CHUNK),
+            (rt._lib.RT_FLAG_PERSISTENT | rt._lib.RT_FLAG_NO_CULL, rt.RT_TILES_XCD_CHUNK)]
 
 
 def _device_scene(scene):
@@ -64,12 +68,15 @@ def test_golden_scene_parity(name, kernel):
     _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
 
 
-def test_c3_full_frame_matches_reference():
-    """1920x1080x16 frog (config c3) against the reference's own full-size outputs."""
+@pytest.mark.parametrize("flags,tiles", LAUNCHES)
+def test_c3_full_frame_matches_reference(flags, tiles):
+    """1920x1080x16 frog (config c3) against the reference's own full-size outputs, for every
+    launch shape (one block per tile / persistent blocks; tile orders; culling on/off)."""
     meta = golden_meta("c3_full")
     hs = host_scene("frog.json")
     cam = hs.camera(1920, 1080)
-    rgb, hi, ht = _device_scene("frog.json").render(cam, spp=16, max_depth=1, aov=True)
+    rgb, hi, ht = _device_scene("frog.json").render(cam, spp=16, max_depth=1, aov=True, flags=flags,
+                                                    tile_order=tiles)
     assert hashlib.sha256(hi.tobytes()).hexdigest() == meta["sha256"]["hits.i32"]
     assert hashlib.sha256(ht.tobytes()).hexdigest() == meta["sha256"]["hitt.f32"]
     _check_fb(rgb, golden_array("c3_full", "fb.f32.gz", np.float32))
@@ -80,12 +87,14 @@ def test_c3_full_frame_matches_reference():
     assert diff.max() <= 1
 
 
+@pytest.mark.parametrize("flags", [0, rt._lib.RT_FLAG_PERSISTENT])
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("spp,W,H", [(1, 37, 23), (3, 40, 21), (64, 9, 7), (2, 1, 1), (16, 65, 3)])
-def test_odd_shapes_against_oracle(spp, W, H, kernel):
+def test_odd_shapes_against_oracle(spp, W, H, kernel, flags):
     hs = host_scene("frog.json")
     cam = hs.camera(W, H)
-    rgb, hi, ht = _device_scene("frog.json").render(cam, spp=spp, max_depth=1, aov=True, kernel=kernel)
+    rgb, hi, ht = _device_scene("frog.json").render(cam, spp=spp, max_depth=1, aov=True, kernel=kernel,
+                                                    flags=flags)
     ref, rhi, rht = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,
                                  hs.tri_object_ids, hs.materials, hs.lights, spp=spp, max_depth=1, aov=True)
     assert np.array_equal(hi, rhi)
@@ -264,3 +273,20 @@ def test_tile_culling_changes_nothing(scene):
         b = ds.render(cam, spp=4, max_depth=1, aov=True, flags=rt._lib.RT_FLAG_NO_CULL)
         for x, y in zip(a, b):
             assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), k
+
+
+@pytest.mark.parametrize("spp", [3, 16])
+def test_persistent_blocks_over_many_tiles(spp):
+    """More live tiles than resident blocks (the persistent loop turns over many times), for
+    the sample-per-lane and pixel-per-lane kernels: identical to one block per tile, and rows
+    of it against the oracle."""
+    hs = host_scene("frog.json")
+    cam = hs.camera(1280, 720)
+    ds = _device_scene("frog.json")
+    a = ds.render(cam, spp=spp, max_depth=1, aov=True)
+    b = ds.render(cam, spp=spp, max_depth=1, aov=True, flags=rt._lib.RT_FLAG_PERSISTENT)
+    for x, y in zip(a, b):
+        assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32))
+    ref = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,
+                       hs.tri_object_ids, hs.materials, hs.lights, spp=spp, max_depth=1, rows=(352, 368))
+    _check_fb(b[0][352:368], ref[352:368])

@@ -148,13 +148,14 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=gdev)
-    kt = ds.kernel_times(a.steps)
-    kmean = torch.tensor([float(kt.mean()) if len(kt) else float("nan")], dtype=torch.float64, device=gdev)
+    kt, ft = ds.kernel_times(a.steps), ds.frame_times(a.steps)
+    kmean = torch.tensor([float(kt.mean()) if len(kt) else float("nan"),
+                          float(ft.mean()) if len(ft) else float("nan")], dtype=torch.float64, device=gdev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
         dist.all_reduce(kmean, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
-    kernel_ms = float(kmean.item())
+    kernel_ms, frame_ms = float(kmean[0].item()), float(kmean[1].item())
 
     # assemble the frame on rank 0 (band un-permute) for the parity check
     frame = None
@@ -206,7 +207,8 @@ def main():
                    "kernel": a.kernel},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_sample": round(B, 3)},
+                     "kernel": "render_tiles_kernel", "kernel_ms": round(kernel_ms, 4),
+                     "frame_ms": round(frame_ms, 4), "algorithmic_bytes_per_sample": round(B, 3)},
     }
     if not a.no_parity and a.config == "c3":
         ref = np.frombuffer(gzip.open(REPO / "tests" / "golden" / "scenes" / "c3_full" / "fb.f32.gz").read(),

@@ -242,6 +242,8 @@ int rt_box_test_host(const float* rays, const float* boxes, const float* tminmax
  * rt_render_device calls on this scene, oldest first, measured with HIP events recorded
  * on the launch stream around the kernel.  Waits for those launches to finish. */
 int rt_kernel_times(const rt_scene* s, float* ms_out, int max, int* n_out);
+/* The same for the whole device frame: list reset, tile cull pre-pass and render kernel. */
+int rt_frame_times(const rt_scene* s, float* ms_out, int max, int* n_out);
 
 int rt_device_count(int* n);
 const char* rt_last_error(void);

@@ -134,6 +134,7 @@ SIGNATURES = {
     "rt_powf_batch": (I, [I, P, P, I, P]),
     "rt_box_test_host": (I, [P, P, P, I, P, P, P]),
     "rt_kernel_times": (I, [P, P, I, P]),
+    "rt_frame_times": (I, [P, P, I, P]),
     "rt_device_count": (I, [P]),
     "rt_last_error": (C.c_char_p, []),
     "rt_abi_version": (I, []),

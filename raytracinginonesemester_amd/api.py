@@ -264,6 +264,13 @@ class DeviceScene:
         check(lib().rt_kernel_times(self._h, ptr(out), max_launches, C.byref(n)))
         return out[:n.value]
 
+    def frame_times(self, max_launches: int = 256) -> np.ndarray:
+        """ms of the whole device frame (list reset, cull pre-pass, render kernel)."""
+        out = np.zeros(max_launches, np.float32)
+        n = C.c_int()
+        check(lib().rt_frame_times(self._h, ptr(out), max_launches, C.byref(n)))
+        return out[:n.value]
+
     def close(self) -> None:
         if self._h:
             lib().rt_scene_destroy(self._h)

@@ -907,12 +907,14 @@ struct rt_scene {
     std::vector<float> jitter_host;
     // Ring of HIP event pairs around each render kernel, recorded on the launch stream.
     static constexpr int kRing = 256;
-    hipEvent_t ev0[kRing] = {}, ev1[kRing] = {};
+    // ev0 | counter reset + tile_cull_kernel | evm | render kernel | ev1
+    hipEvent_t ev0[kRing] = {}, evm[kRing] = {}, ev1[kRing] = {};
     uint64_t launches = 0;
     size_t bytes = 0;
     ~rt_scene() {
         for (int i = 0; i < kRing; ++i) {
             if (ev0[i]) (void)hipEventDestroy(ev0[i]);
+            if (evm[i]) (void)hipEventDestroy(evm[i]);
             if (ev1[i]) (void)hipEventDestroy(ev1[i]);
         }
     }
@@ -1054,6 +1056,7 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     if (nlights > 0 && (rc = s->lights.upload(lights, size_t(nlights) * sizeof(rt_light))) != RT_OK) return rc;
     for (int i = 0; i < rt_scene::kRing; ++i) {
         HIP_TRY(hipEventCreate(&s->ev0[i]));
+        HIP_TRY(hipEventCreate(&s->evm[i]));
         HIP_TRY(hipEventCreate(&s->ev1[i]));
     }
     s->bytes = s->inode.n + s->ibox.n + s->leaf.n + s->tnorm.n + s->objids.n + s->mats.n + s->lights.n;
@@ -1224,6 +1227,7 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     HIP_TRY(hipMemsetAsync(s->work.p, 0, kCounterBytes, st));
     hipLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, P);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(s->evm[slot], st));
     if ((rc = mode == RT_KERNEL_LANE ? launch<RT_KERNEL_LANE>(s, P, samples, persistent, st)
                                      : launch<RT_KERNEL_WAVE>(s, P, samples, persistent, st)) != RT_OK)
         return rc;
@@ -1233,18 +1237,28 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     return RT_OK;
 }
 
-extern "C" int rt_kernel_times(const rt_scene* s, float* ms_out, int max, int* n_out) {
-    if (!s || max < 0 || (max > 0 && !ms_out)) return set_error(RT_ERR_ARG, "rt_kernel_times: bad args");
+namespace {
+int event_times(const rt_scene* s, const hipEvent_t* from, float* ms_out, int max, int* n_out) {
+    if (!s || max < 0 || (max > 0 && !ms_out)) return set_error(RT_ERR_ARG, "kernel times: bad args");
     DeviceGuard g(s->device);
     const uint64_t have = std::min<uint64_t>(s->launches, uint64_t(rt_scene::kRing));
     const int n = int(std::min<uint64_t>(have, uint64_t(max)));
     for (int k = 0; k < n; ++k) {  // oldest first among the n most recent
         const int slot = int((s->launches - uint64_t(n) + uint64_t(k)) % rt_scene::kRing);
         HIP_TRY(hipEventSynchronize(s->ev1[slot]));
-        HIP_TRY(hipEventElapsedTime(&ms_out[k], s->ev0[slot], s->ev1[slot]));
+        HIP_TRY(hipEventElapsedTime(&ms_out[k], from[slot], s->ev1[slot]));
     }
     if (n_out) *n_out = n;
     return RT_OK;
+}
+}  // namespace
+
+extern "C" int rt_kernel_times(const rt_scene* s, float* ms_out, int max, int* n_out) {
+    return event_times(s, s ? s->evm : nullptr, ms_out, max, n_out);
+}
+
+extern "C" int rt_frame_times(const rt_scene* s, float* ms_out, int max, int* n_out) {
+    return event_times(s, s ? s->ev0 : nullptr, ms_out, max, n_out);
 }
 
 extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, float* rgb_host,

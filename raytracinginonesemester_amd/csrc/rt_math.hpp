@@ -42,8 +42,8 @@ __host__ __device__ __forceinline__ f3 cam_unit(f3 v) {
 
 // A ray as the slab test needs it.  `par` bit a: |dir[a]| < 1e-8f, where intersectAABB
 // degenerates to an exact inside test on that axis (bvh.h:90-91).  `invf` is a float
-// reciprocal of the direction (any <= 2 ulp approximation), used only by the conservative
-// pre-classification below, never to decide an ambiguous case.
+// reciprocal of the direction (any <= 2 ulp approximation), +inf on parallel axes, used only
+// by the conservative pre-classification below, never to decide an ambiguous case.
 struct RayPre {
     f3 o, d;
     f3 invf;
@@ -63,8 +63,9 @@ __host__ __device__ __forceinline__ RayPre make_ray(f3 o, f3 d) {
     r.o = o;
     r.d = d;
     const float eps = 1e-8f;
-    r.par = (fabsf(d.x) < eps ? 1u : 0u) | (fabsf(d.y) < eps ? 2u : 0u) | (fabsf(d.z) < eps ? 4u : 0u);
-    r.invf = mk(rcp_approx(d.x), rcp_approx(d.y), rcp_approx(d.z));
+    const bool px = fabsf(d.x) < eps, py = fabsf(d.y) < eps, pz = fabsf(d.z) < eps;
+    r.par = (px ? 1u : 0u) | (py ? 2u : 0u) | (pz ? 4u : 0u);
+    r.invf = mk(px ? INFINITY : rcp_approx(d.x), py ? INFINITY : rcp_approx(d.y), pz ? INFINITY : rcp_approx(d.z));
     return r;
 }
 
@@ -108,33 +109,31 @@ __host__ __device__ inline bool box_hit_exact(const RayPre& r, const float mn[3]
 // reference lows, Hmin = min of the highs (tmin/tmax are exact in both precisions):
 //   MISS  if max(tmin, lo'-E) > min(tmax, hi'+E)      (then Lmax > Hmin: reference rejects)
 //   HIT   if max(tmin, lo'+E) <= min(tmax, hi'-E)     (then Lmax <= Hmin: reference accepts)
-// A non-finite estimate (coordinates near FLT_MAX) never yields HIT; NaN compares false and
-// falls to AMBIG.  Parallel axes use the reference's exact float inside test.
+// Branch-free over the axes: a parallel axis has invf = +inf, so its tn'/tf' are +-inf or
+// NaN and its E is +inf or NaN; fmaxf/fminf drop the NaN terms and +-inf - inf terms, so the
+// axis constrains nothing, and the sum of the E's (non-finite) rules HIT out.  MISS then
+// rests on the other axes alone, which is sound since the reference's t-interval is the
+// intersection over its non-parallel axes (its inside test can only reject more).  The same
+// sum rules HIT out for estimates near FLT_MAX; NaN compares false and falls to AMBIG.
 enum : int { BOX_MISS = 0, BOX_HIT = 1, BOX_AMBIG = 2 };
 __host__ __device__ __forceinline__ int box_classify(const RayPre& r, const float mn[3], const float mx[3],
                                                      float tmin, float tmax) {
     const float o[3] = {r.o.x, r.o.y, r.o.z}, iv[3] = {r.invf.x, r.invf.y, r.invf.z};
-    float lowLo = tmin, lowHi = tmin, highLo = tmax, highHi = tmax;
-    bool inside = true, finite = true;
+    float lowLo = tmin, lowHi = tmin, highLo = tmax, highHi = tmax, esum = 0.f;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        if (r.par & (1u << a)) {
-            inside = inside && !(o[a] < mn[a] || o[a] > mx[a]);
-        } else {
-            const float tn = (mn[a] - o[a]) * iv[a];
-            const float tf = (mx[a] - o[a]) * iv[a];
-            const float lo = fminf(tn, tf), hi = fmaxf(tn, tf);
-            const float E = 4e-6f * fmaxf(fabsf(tn), fabsf(tf)) + 1e-30f;
-            finite = finite && (E < 3.0e38f);
-            lowLo = fmaxf(lowLo, lo - E);
-            lowHi = fmaxf(lowHi, lo + E);
-            highLo = fminf(highLo, hi - E);
-            highHi = fminf(highHi, hi + E);
-        }
+        const float tn = (mn[a] - o[a]) * iv[a];
+        const float tf = (mx[a] - o[a]) * iv[a];
+        const float lo = fminf(tn, tf), hi = fmaxf(tn, tf);
+        const float E = 4e-6f * fmaxf(fabsf(tn), fabsf(tf)) + 1e-30f;
+        esum = esum + E;
+        lowLo = fmaxf(lowLo, lo - E);
+        lowHi = fmaxf(lowHi, lo + E);
+        highLo = fminf(highLo, hi - E);
+        highHi = fminf(highHi, hi + E);
     }
-    if (!inside) return BOX_MISS;
     if (lowLo > highHi) return BOX_MISS;
-    if (finite && lowHi <= highLo) return BOX_HIT;
+    if (esum < 3.0e38f && lowHi <= highLo) return BOX_HIT;
     return BOX_AMBIG;
 }
 

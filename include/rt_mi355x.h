@@ -177,8 +177,7 @@ typedef struct {
 } rt_render_opts;
 
 enum {
-    RT_FLAG_NO_CULL = 1,      /* disable tile culling against the root box (A/B; same output) */
-    RT_FLAG_PERSISTENT = 2    /* persistent blocks dequeue live tiles (A/B; same output) */
+    RT_FLAG_NO_CULL = 1       /* disable tile culling against the root box (A/B; same output) */
 };
 
 enum {
@@ -244,6 +243,9 @@ int rt_box_test_host(const float* rays, const float* boxes, const float* tminmax
 int rt_kernel_times(const rt_scene* s, float* ms_out, int max, int* n_out);
 /* The same for the whole device frame: list reset, tile cull pre-pass and render kernel. */
 int rt_frame_times(const rt_scene* s, float* ms_out, int max, int* n_out);
+/* Pixel tiles of the most recent rt_render_device call that survived the root-box cull
+ * (traced), and all tiles.  Waits for that call to finish. */
+int rt_live_tiles(const rt_scene* s, int64_t* live, int64_t* total);
 
 int rt_device_count(int* n);
 const char* rt_last_error(void);

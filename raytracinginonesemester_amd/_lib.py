@@ -20,7 +20,6 @@ RT_ERR = {
 RT_KERNEL_AUTO, RT_KERNEL_WAVE, RT_KERNEL_LANE, RT_KERNEL_WAVE_PIXELS = 0, 1, 2, 3
 RT_TILES_AUTO, RT_TILES_LINEAR, RT_TILES_XCD_CHUNK, RT_TILES_ROWS = 0, 1, 2, 3
 RT_FLAG_NO_CULL = 1
-RT_FLAG_PERSISTENT = 2
 
 
 class RTError(RuntimeError):
@@ -135,6 +134,7 @@ SIGNATURES = {
     "rt_box_test_host": (I, [P, P, P, I, P, P, P]),
     "rt_kernel_times": (I, [P, P, I, P]),
     "rt_frame_times": (I, [P, P, I, P]),
+    "rt_live_tiles": (I, [P, P, P]),
     "rt_device_count": (I, [P]),
     "rt_last_error": (C.c_char_p, []),
     "rt_abi_version": (I, []),

@@ -264,6 +264,12 @@ class DeviceScene:
         check(lib().rt_kernel_times(self._h, ptr(out), max_launches, C.byref(n)))
         return out[:n.value]
 
+    def live_tiles(self) -> tuple:
+        """(traced tiles, all tiles) of the most recent render."""
+        live, total = C.c_int64(), C.c_int64()
+        check(lib().rt_live_tiles(self._h, C.byref(live), C.byref(total)))
+        return live.value, total.value
+
     def frame_times(self, max_launches: int = 256) -> np.ndarray:
         """ms of the whole device frame (list reset, cull pre-pass, render kernel)."""
         out = np.zeros(max_launches, np.float32)

@@ -29,6 +29,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <algorithm>
 #include <memory>
@@ -89,6 +90,8 @@ struct RenderParams {
     int32_t* live_tiles;                              // nqueues lists of queue_cap entries
     int32_t nqueues;
     int32_t queue_cap;
+    int32_t tiles_per_block;                          // virtual blocks per render block
+    int32_t tiles_virtual;                            // virtual blocks (planned_tile)
     float* __restrict__ rgb;
     int32_t* __restrict__ hit_idx;
     float* __restrict__ hit_t;
@@ -109,6 +112,28 @@ __device__ __forceinline__ uint32_t wrlane(uint32_t v, uint32_t l, uint32_t old)
 }
 
 // ---- node accessors ---------------------------------------------------------------------
+// Scene arrays are immutable while a frame renders: read them through the constant address
+// space, so wave-uniform node addresses become scalar loads even inside loops that also
+// store (the compiler cannot otherwise prove the stores do not clobber them).
+typedef float __attribute__((ext_vector_type(4))) vf4;
+typedef uint32_t __attribute__((ext_vector_type(4))) vu4;
+__device__ __forceinline__ float4 ldc(const float4* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const vf4 v = *(const __attribute__((address_space(4))) vf4*)p;
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ uint4 ldc_u(const float4* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const vu4 v = *(const __attribute__((address_space(4))) vu4*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+
 struct Box {
     float mn[3], mx[3];
 };
@@ -120,12 +145,12 @@ __device__ __forceinline__ Box own_box(const SceneView& sc, uint32_t ref, bool i
         b.mx[0] = sc.root_box[3]; b.mx[1] = sc.root_box[4]; b.mx[2] = sc.root_box[5];
     } else if (ref & LEAF_BIT) {
         const float4* L = sc.leaf + 4 * (size_t)(ref & ~LEAF_BIT);
-        const float4 a = L[1], c = L[2], d = L[3];
+        const float4 a = ldc(L + 1), c = ldc(L + 2), d = ldc(L + 3);
         b.mn[0] = a.w; b.mn[1] = c.w; b.mn[2] = d.x;
         b.mx[0] = d.y; b.mx[1] = d.z; b.mx[2] = d.w;
     } else {
         const float4* B = sc.ibox + 2 * (size_t)ref;
-        const float4 lo = B[0], hi = B[1];
+        const float4 lo = ldc(B), hi = ldc(B + 1);
         b.mn[0] = lo.x; b.mn[1] = lo.y; b.mn[2] = lo.z;
         b.mx[0] = hi.x; b.mx[1] = hi.y; b.mx[2] = hi.z;
     }
@@ -134,6 +159,21 @@ __device__ __forceinline__ Box own_box(const SceneView& sc, uint32_t ref, bool i
 
 __device__ __forceinline__ bool box_test(const RayPre& r, const Box& b, float bestT) {
     return box_hit(r, b.mn[0], b.mn[1], b.mn[2], b.mx[0], b.mx[1], b.mx[2], kRayTMin, bestT);
+}
+
+// box_hit for the lanes in `act` of a wave (all lanes call it): the float pre-classification
+// for everyone, the exact double test only behind a wave-uniform branch taken when some lane
+// is ambiguous.
+__device__ __forceinline__ bool box_hit_wave(const RayPre& r, float mnx, float mny, float mnz, float mxx,
+                                             float mxy, float mxz, float tmax, bool act) {
+    const float mn[3] = {mnx, mny, mnz}, mx[3] = {mxx, mxy, mxz};
+    const int c = box_classify(r, mn, mx, kRayTMin, tmax);
+    bool res = act && c == BOX_HIT;
+    const bool amb = act && c == BOX_AMBIG;
+    if (ballot(amb) != 0) {
+        if (amb) res = box_hit_exact(r, mn, mx, (double)kRayTMin, (double)tmax);
+    }
+    return res;
 }
 
 // Result of one closest-hit query.
@@ -173,7 +213,7 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
         bool act = (mask & lane_bit) != 0;
         if (ver != wave_ver) {  // some lane's bestT changed since the push: pop-time re-test
             const Box b = own_box(sc, ref, ver == VER_FORCE);
-            const bool pass = act && box_test(r, b, hs.bestT);
+            const bool pass = box_hit_wave(r, b.mn[0], b.mn[1], b.mn[2], b.mx[0], b.mx[1], b.mx[2], hs.bestT, act);
             mask = ballot(pass);
             act = pass;
             if (mask == 0) continue;
@@ -181,7 +221,7 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
         if (ref & LEAF_BIT) {
             const uint32_t slot = ref & ~LEAF_BIT;
             const float4* L = sc.leaf + 4 * (size_t)slot;
-            const float4 a = L[0], b = L[1], c = L[2];
+            const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
             float t, u, v;
             const bool h = act && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), kRayTMin,
                                        hs.bestT, t, u, v);
@@ -197,11 +237,11 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
             continue;
         }
         const float4* N = sc.inode + 4 * (size_t)ref;
-        const float4 q0 = N[0], q1 = N[1], q2 = N[2];
-        const uint4 q3 = *reinterpret_cast<const uint4*>(N + 3);
+        const float4 q0 = ldc(N), q1 = ldc(N + 1), q2 = ldc(N + 2);
+        const uint4 q3 = ldc_u(N + 3);
         const uint32_t lref = q3.x, rref = q3.y;
         if (lref != NO_REF) {
-            const bool pl = act && box_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, kRayTMin, hs.bestT);
+            const bool pl = box_hit_wave(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hs.bestT, act);
             const uint64_t ml = ballot(pl);
             if (ml != 0) {
                 st_ref = wrlane(lref, sp, st_ref);
@@ -212,7 +252,7 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
             }
         }
         if (rref != NO_REF) {
-            const bool pr = act && box_hit(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, kRayTMin, hs.bestT);
+            const bool pr = box_hit_wave(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hs.bestT, act);
             const uint64_t mr = ballot(pr);
             if (mr != 0) {
                 st_ref = wrlane(rref, sp, st_ref);
@@ -249,7 +289,7 @@ __device__ __forceinline__ void traverse_lane(const SceneView& sc, const RayPre&
         if (ref & LEAF_BIT) {
             const uint32_t slot = ref & ~LEAF_BIT;
             const float4* L = sc.leaf + 4 * (size_t)slot;
-            const float4 a = L[0], b = L[1], c = L[2];
+            const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
             float t, u, v;
             if (mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), kRayTMin, hs.bestT, t, u, v)) {
                 hs.bestT = t;
@@ -260,8 +300,8 @@ __device__ __forceinline__ void traverse_lane(const SceneView& sc, const RayPre&
             continue;
         }
         const float4* N = sc.inode + 4 * (size_t)ref;
-        const float4 q0 = N[0], q1 = N[1], q2 = N[2];
-        const uint4 q3 = *reinterpret_cast<const uint4*>(N + 3);
+        const float4 q0 = ldc(N), q1 = ldc(N + 1), q2 = ldc(N + 2);
+        const uint4 q3 = ldc_u(N + 3);
         if (q3.x != NO_REF &&
             box_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, kRayTMin, hs.bestT)) {
             st_ref[sp] = q3.x;
@@ -515,10 +555,10 @@ __device__ __forceinline__ int global_row(const RenderParams& P, int r) {
 // There are P.nqueues lists.  Workgroups are dealt round-robin over the 8 XCDs, so with 8
 // lists a block's home list is blockIdx % 8: RT_TILES_ROWS gives XCD k the tile rows k, k+8,
 // ... (neighbouring tiles share an L2, the work spreads evenly); RT_TILES_XCD_CHUNK gives it
-// a contiguous 1/8 of the frame (planned_tile balances uneven lists).
+// a contiguous 1/8 of the frame.
 // RT_TILES_LINEAR is one list in raster order.  The order is a speed property only.
-// Each list has a length counter (appends) and a cursor (persistent dequeue) 128 B apart; the
-// lists' counters sit 256 B apart (separate L2 channels) so the atomics do not serialise.
+// The lists' length counters sit 256 B apart (separate channels) so the appends do not
+// serialise.
 constexpr int COUNTER_STRIDE = 64;
 __device__ __forceinline__ int queue_of_tile(const RenderParams& P, int tile) {
     if (P.nqueues == 1) return 0;
@@ -570,54 +610,29 @@ __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
     }
 }
 
-// Block -> live tile, without atomics.  The grid has tiles_total blocks, dealt round-robin
-// over the 8 XCDs: block b = 8*i + k runs on XCD k and takes slot i of list k.  Lists longer
-// than their XCD's share of blocks hand their leftover slots, in list order, to the blocks
-// left idle by shorter lists (ranked by XCD, then i); blocks past the live count exit.  The
-// working blocks come first in dispatch order, the idle ones drain behind them.
-__device__ __forceinline__ int planned_tile(const RenderParams& P) {
-    const int b = (int)blockIdx.x;
-    if (P.nqueues == 1) return b < (int)P.live_count[0] ? P.live_tiles[b] : -1;
-    const int G = (int)gridDim.x;
-    const int q = b & 7, i = b >> 3;
-    int c[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) c[k] = (int)P.live_count[k * COUNTER_STRIDE];
-    if (i < c[q]) return P.live_tiles[(size_t)q * P.queue_cap + i];
-    int r = i - c[q];  // rank among the idle blocks
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if (k < q) r += max(0, (G - k + 7) / 8 - c[k]);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int nk = (G - k + 7) / 8, lk = max(0, c[k] - nk);
-        if (r >= 0 && r < lk) return P.live_tiles[(size_t)k * P.queue_cap + nk + r];
-        r -= lk;
-    }
-    return -1;
+// Virtual block -> live tile, without atomics.  With 8 lists there are tiles_virtual =
+// 8 * tiles_x * ceil(tiles_y / 8) virtual blocks, at least 8 times the longest list (RT_TILES_ROWS
+// puts at most tiles_x * ceil(tiles_y / 8) tiles in a list, RT_TILES_XCD_CHUNK at most
+// ceil(tiles / 8)); virtual block j = 8*i + k takes slot i of list k, or nothing.  Dispatch
+// deals blocks round-robin over the XCDs and a real block runs the virtual blocks
+// blockIdx.x + m*gridDim.x with gridDim.x a multiple of 8, so list k is rendered on XCD k.
+// With one list (RT_TILES_LINEAR) virtual block j takes slot j.  The list lengths are read once
+// per block: the lists are immutable while the render kernel runs, so they and their entries
+// are read through the constant address space (scalar loads).
+__device__ __forceinline__ uint32_t ldc_u32(const uint32_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *(const __attribute__((address_space(4))) uint32_t*)p;
+#else
+    return *p;
+#endif
 }
 
-// Take the next live tile for a persistent block (thread 0, then broadcast): home list first
-// (blockIdx % 8 is the block's XCD when the whole grid is resident), then the others.  -1
-// once every list is drained; every block gets there, since the lists only shrink while the
-// render kernel runs.
-__device__ __forceinline__ int take_tile(const RenderParams& P, int* tile_sh) {
-    if (threadIdx.x == 0) {
-        int tile = -1;
-        const int home = (int)(blockIdx.x % (uint32_t)P.nqueues);
-        for (int k = 0; k < P.nqueues && tile < 0; ++k) {
-            const int q = home + k < P.nqueues ? home + k : home + k - P.nqueues;
-            uint32_t* cursor = &P.live_count[q * COUNTER_STRIDE + COUNTER_STRIDE / 2];
-            const uint32_t n = __hip_atomic_load(&P.live_count[q * COUNTER_STRIDE], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-            if (__hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n) continue;
-            const uint32_t slot = atomicAdd(cursor, 1u);
-            if (slot < n) tile = P.live_tiles[(size_t)q * P.queue_cap + slot];
-        }
-        *tile_sh = tile;
-    }
-    __syncthreads();
-    return *tile_sh;
+__device__ __forceinline__ int list_length(const RenderParams& P, int q) {
+    return (int)ldc_u32(&P.live_count[q * COUNTER_STRIDE]);
+}
+
+__device__ __forceinline__ int planned_tile(const RenderParams& P, int len, int q, int i) {
+    return i < len ? (int)ldc_u32(reinterpret_cast<const uint32_t*>(P.live_tiles) + (size_t)q * P.queue_cap + i) : -1;
 }
 
 // One sample per lane: a block covers a tile_w x tile_h pixel tile x spp samples (spp a power
@@ -689,27 +704,22 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
     }
 }
 
-// One block per tile of the frame; blocks past the live count exit at once (planned_tile).
+// Each block runs tiles_per_block virtual blocks (planned_tile): fewer, longer blocks, so
+// the dispatcher does not spend the frame launching blocks that find no live tile.
 template <int MODE, bool SAMPLES>
 __global__ __launch_bounds__(BLOCK, 4) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
-    const int tile = planned_tile(P);
-    if (tile < 0) return;
-    if constexpr (SAMPLES) samples_tile<MODE>(P, tile, col);
-    else pixels_tile<MODE>(P, tile);
-}
-
-// Persistent blocks (as many as are resident at once) looping over the live lists.
-template <int MODE, bool SAMPLES>
-__global__ __launch_bounds__(BLOCK, 4) void render_persistent_kernel(RenderParams P) {
-    __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
-    __shared__ int tile_sh;
-    for (;;) {
-        const int tile = take_tile(P, &tile_sh);
-        if (tile < 0) break;
+    const int b = (int)blockIdx.x, g = (int)gridDim.x;
+    const int q = P.nqueues == 1 ? 0 : (b & 7);
+    const int len = list_length(P, q);
+    for (int m = 0; m < P.tiles_per_block; ++m) {
+        const int j = b + m * g;
+        if (j >= P.tiles_virtual) break;
+        const int tile = planned_tile(P, len, q, P.nqueues == 1 ? j : (j >> 3));
+        if (tile < 0) continue;
         if constexpr (SAMPLES) samples_tile<MODE>(P, tile, col);
         else pixels_tile<MODE>(P, tile);
-        __syncthreads();  // tile_sh and col are rewritten by the next tile
+        if constexpr (SAMPLES) __syncthreads();  // col is rewritten by the next tile
     }
 }
 
@@ -902,6 +912,7 @@ struct rt_scene {
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     DevBuf inode, ibox, leaf, tnorm, objids, mats, lights, jitter;
     DevBuf work;  // live tile list counters + the lists
+    int64_t last_tiles_total = 0;
     int cus = 256;
     int jitter_spp = -1;
     std::vector<float> jitter_host;
@@ -1031,11 +1042,6 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     std::unique_ptr<rt_scene> s(new (std::nothrow) rt_scene());
     if (!s) return set_error(RT_ERR_NOMEM, "out of memory");
     s->device = device;
-    {
-        hipDeviceProp_t prop;
-        HIP_TRY(hipGetDeviceProperties(&prop, device));
-        s->cus = std::max(1, prop.multiProcessorCount);
-    }
     s->P = P;
     s->nmat = nmat;
     s->nlights = nlights;
@@ -1113,26 +1119,18 @@ int prepare_jitter(rt_scene* s, const rt_render_opts* o) {
     return RT_OK;
 }
 
-// RT_FLAG_PERSISTENT: as many blocks as are resident at once (occupancy x CUs), each looping
-// over the live lists; otherwise one block per tile, the blocks past the live count exiting
-// at once (planned_tile).
+// tiles_virtual / tiles_per_block blocks (rounded up to a multiple of 8) over the planned
+// virtual blocks (planned_tile).
 template <int MODE, bool SAMPLES>
-int launch_mode(const rt_scene* s, const RenderParams& P, bool persistent, hipStream_t st) {
-    if (!persistent) {
-        hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES>), dim3(P.tiles_total), dim3(BLOCK), 0, st, P);
-        return RT_OK;
-    }
-    int per_cu = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(&render_persistent_kernel<MODE, SAMPLES>), BLOCK, 0));
-    const int blocks = std::max(1, std::min(P.tiles_total, std::max(1, per_cu) * s->cus));
-    hipLaunchKernelGGL((render_persistent_kernel<MODE, SAMPLES>), dim3(blocks), dim3(BLOCK), 0, st, P);
-    return RT_OK;
+void launch_mode(const RenderParams& P, hipStream_t st) {
+    const int g = (P.tiles_virtual + P.tiles_per_block - 1) / P.tiles_per_block;
+    hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES>), dim3((g + 7) / 8 * 8), dim3(BLOCK), 0, st, P);
 }
 
 template <int MODE>
-int launch(const rt_scene* s, const RenderParams& P, bool samples, bool persistent, hipStream_t st) {
-    return samples ? launch_mode<MODE, true>(s, P, persistent, st) : launch_mode<MODE, false>(s, P, persistent, st);
+void launch(const RenderParams& P, bool samples, hipStream_t st) {
+    if (samples) launch_mode<MODE, true>(P, st);
+    else launch_mode<MODE, false>(P, st);
 }
 
 // Host restatement of a pixel whose spp samples all miss the root: each sample is
@@ -1214,13 +1212,16 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     P.miss_pixel = miss_pixel_value(o);
     P.nqueues = P.tile_order == RT_TILES_LINEAR ? 1 : 8;
     P.queue_cap = P.tiles_total;
+    P.tiles_virtual = P.nqueues == 1 ? P.tiles_total : 8 * P.tiles_x * ((tiles_y + 7) / 8);
+    P.tiles_per_block = 2;
+    if (const char* e = std::getenv("RT_TILES_PER_BLOCK")) P.tiles_per_block = std::max(1, std::atoi(e));
     constexpr size_t kCounterBytes = 8 * COUNTER_STRIDE * sizeof(uint32_t);
     const size_t work_bytes = kCounterBytes + size_t(P.nqueues) * size_t(P.queue_cap) * sizeof(int32_t);
     if (s->work.n < work_bytes && (rc = s->work.alloc(work_bytes)) != RT_OK) return rc;
     P.live_count = static_cast<uint32_t*>(s->work.p);
+    s->last_tiles_total = P.tiles_total;
     P.live_tiles = reinterpret_cast<int32_t*>(static_cast<char*>(s->work.p) + kCounterBytes);
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
-    const bool persistent = (o->flags & RT_FLAG_PERSISTENT) != 0;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int slot = int(s->launches % rt_scene::kRing);
     HIP_TRY(hipEventRecord(s->ev0[slot], st));
@@ -1228,9 +1229,8 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     hipLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, P);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(s->evm[slot], st));
-    if ((rc = mode == RT_KERNEL_LANE ? launch<RT_KERNEL_LANE>(s, P, samples, persistent, st)
-                                     : launch<RT_KERNEL_WAVE>(s, P, samples, persistent, st)) != RT_OK)
-        return rc;
+    if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, st);
+    else launch<RT_KERNEL_WAVE>(P, samples, st);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(s->ev1[slot], st));
     s->launches++;
@@ -1252,6 +1252,20 @@ int event_times(const rt_scene* s, const hipEvent_t* from, float* ms_out, int ma
     return RT_OK;
 }
 }  // namespace
+
+extern "C" int rt_live_tiles(const rt_scene* s, int64_t* live, int64_t* total) {
+    if (!s || !live || !total) return set_error(RT_ERR_ARG, "rt_live_tiles: null argument");
+    *live = 0;
+    *total = s->last_tiles_total;
+    if (!s->work.p || s->launches == 0) return RT_OK;
+    DeviceGuard g(s->device);
+    const int slot = int((s->launches - 1) % rt_scene::kRing);
+    HIP_TRY(hipEventSynchronize(s->ev1[slot]));
+    uint32_t c[8 * COUNTER_STRIDE];
+    HIP_TRY(hipMemcpy(c, s->work.p, sizeof(c), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 8; ++k) *live += c[k * COUNTER_STRIDE];
+    return RT_OK;
+}
 
 extern "C" int rt_kernel_times(const rt_scene* s, float* ms_out, int max, int* n_out) {
     return event_times(s, s ? s->evm : nullptr, ms_out, max, n_out);

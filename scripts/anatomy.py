@@ -24,10 +24,15 @@ nolt = rt.DeviceScene(hs.num_triangles, hs.nodes, hs.aabbs, hs.triangles, hs.tri
                       np.zeros(0, rt.LIGHT_DTYPE))
 cases = {"full": (full, cam), "no_light": (nolt, cam), "all_miss": (full, away)}
 times = {k: [] for k in cases}
+frames = {k: [] for k in cases}
+live = {}
 for r in range(int(sys.argv[1]) if len(sys.argv) > 1 else 5):
     for k, (ds, c) in cases.items():
         for _ in range(3):
             ds.render(c, spp=16, max_depth=1)
         times[k] += list(ds.kernel_times(3))
+        frames[k] += list(ds.frame_times(3))
+        live[k] = ds.live_tiles()
 for k, t in times.items():
-    print(json.dumps({"case": k, "median_ms": round(float(np.median(t)), 4), "min_ms": round(float(np.min(t)), 4)}))
+    print(json.dumps({"case": k, "kernel_median_ms": round(float(np.median(t)), 4), "min_ms": round(float(np.min(t)), 4),
+                      "frame_median_ms": round(float(np.median(frames[k])), 4), "live_tiles": live[k]}))

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build an experimental variant of the device library with extra compile flags:
+#   scripts/build_variant.sh <name> [-DFLAG ...]  ->  build/variants/<name>/librt_mi355x.so
+# Run against it with RT_MI355X_LIB=build/variants/<name>/librt_mi355x.so.
+set -eu
+NAME=$1; shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$ROOT/build/variants/$NAME
+mkdir -p "$OUT"
+python3 -c "import sys; sys.path.insert(0, '$ROOT'); from raytracinginonesemester_amd import build; build.build()" > /dev/null
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall \
+    -mcode-object-version=5 -Wno-unused-function "$@" -I"$ROOT/include" -I"$ROOT/raytracinginonesemester_amd/csrc" \
+    -c "$ROOT/raytracinginonesemester_amd/csrc/rt_device.hip" -o "$OUT/rt_device.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$ROOT/build/obj/rt_host.o" "$OUT/rt_device.o" \
+    -o "$OUT/librt_mi355x.so"
+echo "$OUT/librt_mi355x.so"

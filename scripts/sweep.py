@@ -8,6 +8,7 @@ every variant's frame is bit-identical to the first variant's.
 import argparse
 import itertools
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -27,7 +28,7 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--kernels", default="wave,lane")
 ap.add_argument("--tiles", default="linear,xcd_chunk,rows")
 ap.add_argument("--cull", default="on", help="on,off")
-ap.add_argument("--persist", default="off", help="on,off")
+ap.add_argument("--tpb", default="2", help="tiles per render block (RT_TILES_PER_BLOCK), e.g. 1,2,4,8")
 a = ap.parse_args()
 
 cfg = configs.G_CONFIGS[a.config]
@@ -38,16 +39,16 @@ ds = rt.DeviceScene.from_host(hs)
 K = {"wave": rt.RT_KERNEL_WAVE, "lane": rt.RT_KERNEL_LANE, "wavepix": rt._lib.RT_KERNEL_WAVE_PIXELS}
 T = {"linear": rt.RT_TILES_LINEAR, "xcd_chunk": rt.RT_TILES_XCD_CHUNK, "rows": rt.RT_TILES_ROWS}
 variants = list(itertools.product(a.kernels.split(","), a.tiles.split(","), a.cull.split(","),
-                                  a.persist.split(",")))
+                                  a.tpb.split(",")))
 times = {v: [] for v in variants}
 ref = None
 for r in range(a.rounds):
     for v in variants:
+        os.environ["RT_TILES_PER_BLOCK"] = v[3]
         for _ in range(a.reps):
             img = ds.render(cam, spp=cfg["spp"], max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
                             kernel=K[v[0]], tile_order=T[v[1]],
-                            flags=(0 if v[2] == "on" else rt._lib.RT_FLAG_NO_CULL)
-                            | (rt._lib.RT_FLAG_PERSISTENT if v[3] == "on" else 0))
+                            flags=0 if v[2] == "on" else rt._lib.RT_FLAG_NO_CULL)
         times[v] += list(ds.kernel_times(a.reps))
         if ref is None:
             ref = img
@@ -55,7 +56,7 @@ for r in range(a.rounds):
 samples = cfg["width"] * cfg["height"] * cfg["spp"]
 for v in variants:
     t = np.array(times[v])
-    print(json.dumps({"config": a.config, "kernel": v[0], "tiles": v[1], "cull": v[2], "persist": v[3],
+    print(json.dumps({"config": a.config, "kernel": v[0], "tiles": v[1], "cull": v[2], "tpb": v[3],
                       "median_ms": round(float(np.median(t)), 4),
                       "min_ms": round(float(t.min()), 4), "Gsamples_s": round(float(samples / np.median(t) / 1e6), 3)}),
           flush=True)

@@ -25,7 +25,7 @@ a = ap.parse_args()
 
 
 def short(name):
-    for k in ("render_tiles_kernel", "render_persistent_kernel", "render_samples_kernel", "tile_cull_kernel",
+    for k in ("render_tiles_kernel", "render_samples_kernel", "tile_cull_kernel",
               "render_hw1_kernel", "copyBuffer", "fillBuffer", "elementwise"):
         if k in name:
             return k

@@ -28,10 +28,9 @@ pytestmark = pytest.mark.gpu
 
 RGB_TOL = 2e-6
 KERNELS = [rt.RT_KERNEL_WAVE, rt.RT_KERNEL_LANE]
-# (flags, tile order): the launch shapes, all of which must give the same frame
-LAUNCHES = [(0, rt.RT_TILES_AUTO), (rt._lib.RT_FLAG_PERSISTENT, rt.RT_TILES_ROWS),
-            (rt._lib.RT_FLAG_PERSISTENT, rt.RT_TILES_LINEAR), (0, rt.RT_TILES_XCD_CHUNK),
-            (rt._lib.RT_FLAG_PERSISTENT | rt._lib.RT_FLAG_NO_CULL, rt.RT_TILES_XCD_CHUNK)]
+# (flags, tile order, tiles per render block): launch shapes, all of which must give the same frame
+LAUNCHES = [(0, rt.RT_TILES_AUTO, None), (0, rt.RT_TILES_LINEAR, "1"), (0, rt.RT_TILES_ROWS, "5"),
+            (0, rt.RT_TILES_XCD_CHUNK, "3"), (rt._lib.RT_FLAG_NO_CULL, rt.RT_TILES_XCD_CHUNK, "2")]
 
 
 def _device_scene(scene):
@@ -68,10 +67,12 @@ def test_golden_scene_parity(name, kernel):
     _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
 
 
-@pytest.mark.parametrize("flags,tiles", LAUNCHES)
-def test_c3_full_frame_matches_reference(flags, tiles):
+@pytest.mark.parametrize("flags,tiles,tpb", LAUNCHES)
+def test_c3_full_frame_matches_reference(flags, tiles, tpb, monkeypatch):
     """1920x1080x16 frog (config c3) against the reference's own full-size outputs, for every
-    launch shape (one block per tile / persistent blocks; tile orders; culling on/off)."""
+    launch shape (tile orders, tiles per render block, culling on/off)."""
+    if tpb is not None:
+        monkeypatch.setenv("RT_TILES_PER_BLOCK", tpb)
     meta = golden_meta("c3_full")
     hs = host_scene("frog.json")
     cam = hs.camera(1920, 1080)
@@ -87,14 +88,14 @@ def test_c3_full_frame_matches_reference(flags, tiles):
     assert diff.max() <= 1
 
 
-@pytest.mark.parametrize("flags", [0, rt._lib.RT_FLAG_PERSISTENT])
+@pytest.mark.parametrize("tiles", [rt.RT_TILES_ROWS, rt.RT_TILES_LINEAR])
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("spp,W,H", [(1, 37, 23), (3, 40, 21), (64, 9, 7), (2, 1, 1), (16, 65, 3)])
-def test_odd_shapes_against_oracle(spp, W, H, kernel, flags):
+def test_odd_shapes_against_oracle(spp, W, H, kernel, tiles):
     hs = host_scene("frog.json")
     cam = hs.camera(W, H)
     rgb, hi, ht = _device_scene("frog.json").render(cam, spp=spp, max_depth=1, aov=True, kernel=kernel,
-                                                    flags=flags)
+                                                    tile_order=tiles)
     ref, rhi, rht = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,
                                  hs.tri_object_ids, hs.materials, hs.lights, spp=spp, max_depth=1, aov=True)
     assert np.array_equal(hi, rhi)
@@ -276,15 +277,17 @@ def test_tile_culling_changes_nothing(scene):
 
 
 @pytest.mark.parametrize("spp", [3, 16])
-def test_persistent_blocks_over_many_tiles(spp):
-    """More live tiles than resident blocks (the persistent loop turns over many times), for
-    the sample-per-lane and pixel-per-lane kernels: identical to one block per tile, and rows
-    of it against the oracle."""
+def test_many_tiles_per_render_block(spp, monkeypatch):
+    """Render blocks looping over several planned tiles (RT_TILES_PER_BLOCK), for the
+    sample-per-lane and pixel-per-lane kernels: identical to one tile per block, and rows of
+    it against the oracle."""
     hs = host_scene("frog.json")
     cam = hs.camera(1280, 720)
     ds = _device_scene("frog.json")
+    monkeypatch.setenv("RT_TILES_PER_BLOCK", "1")
     a = ds.render(cam, spp=spp, max_depth=1, aov=True)
-    b = ds.render(cam, spp=spp, max_depth=1, aov=True, flags=rt._lib.RT_FLAG_PERSISTENT)
+    monkeypatch.setenv("RT_TILES_PER_BLOCK", "7")
+    b = ds.render(cam, spp=spp, max_depth=1, aov=True)
     for x, y in zip(a, b):
         assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32))
     ref = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,

@@ -11,6 +11,7 @@
 //   ibox[i]   32 B  internal node i's own AABB (pop-time re-tests)      (2 x float4)
 //   leaf[j]   64 B  v0, e1, e2, triangle index and the leaf's own AABB  (4 x float4)
 //   tnorm[t]  48 B  n0, n1, n2 of triangle t (read once per hit)        (3 x float4)
+// AABBs are stored as per-axis (min, max) pairs (BoxP), one packed FMA per axis.
 // A child ref is an internal index, LEAF_BIT | leaf index, or NO_REF.
 //
 // Two traversal kernels, both bit-exact against the reference order:
@@ -111,6 +112,17 @@ __device__ __forceinline__ uint32_t wrlane(uint32_t v, uint32_t l, uint32_t old)
     return lane_id() == l ? v : old;
 }
 
+// ---- traversal statistics (instrumented variant builds only: -DRT_STATS) -----------------
+#ifdef RT_STATS
+__device__ unsigned long long g_rt_stats[16];
+#define RT_STAT(i, n) do { if (lane_id() == 0) atomicAdd(&g_rt_stats[(i)], (unsigned long long)(n)); } while (0)
+#else
+#define RT_STAT(i, n) do { } while (0)
+#endif
+// 0/1 traversals (primary/shadow), 2/3 pops, 4/5 pops after a mask test passed, 6/7 pop-time
+// re-tests, 8/9 internal nodes, 10/11 leaves, 12 ambiguous box tests (wave-level), 13 lanes
+// active at traversal start (primary), 14 (shadow)
+
 // ---- node accessors ---------------------------------------------------------------------
 // Scene arrays are immutable while a frame renders: read them through the constant address
 // space, so wave-uniform node addresses become scalar loads even inside loops that also
@@ -134,44 +146,59 @@ __device__ __forceinline__ uint4 ldc_u(const float4* p) {
 #endif
 }
 
-struct Box {
-    float mn[3], mx[3];
-};
+__device__ __forceinline__ v2f lo2(float4 q) { return (v2f){q.x, q.y}; }
+__device__ __forceinline__ v2f hi2(float4 q) { return (v2f){q.z, q.w}; }
 
-__device__ __forceinline__ Box own_box(const SceneView& sc, uint32_t ref, bool is_root) {
-    Box b;
+// Box of a node for the pop-time re-test: the root's from the kernel arguments, a leaf's from
+// its record, an internal node's from ibox.
+__device__ __forceinline__ BoxP own_box(const SceneView& sc, uint32_t ref, bool is_root) {
+    BoxP b;
     if (is_root) {
-        b.mn[0] = sc.root_box[0]; b.mn[1] = sc.root_box[1]; b.mn[2] = sc.root_box[2];
-        b.mx[0] = sc.root_box[3]; b.mx[1] = sc.root_box[4]; b.mx[2] = sc.root_box[5];
+        b.x = (v2f){sc.root_box[0], sc.root_box[3]};
+        b.y = (v2f){sc.root_box[1], sc.root_box[4]};
+        b.z = (v2f){sc.root_box[2], sc.root_box[5]};
     } else if (ref & LEAF_BIT) {
         const float4* L = sc.leaf + 4 * (size_t)(ref & ~LEAF_BIT);
-        const float4 a = ldc(L + 1), c = ldc(L + 2), d = ldc(L + 3);
-        b.mn[0] = a.w; b.mn[1] = c.w; b.mn[2] = d.x;
-        b.mx[0] = d.y; b.mx[1] = d.z; b.mx[2] = d.w;
+        const float4 c = ldc(L + 2), d = ldc(L + 3);
+        b.x = hi2(c);
+        b.y = lo2(d);
+        b.z = hi2(d);
     } else {
         const float4* B = sc.ibox + 2 * (size_t)ref;
-        const float4 lo = ldc(B), hi = ldc(B + 1);
-        b.mn[0] = lo.x; b.mn[1] = lo.y; b.mn[2] = lo.z;
-        b.mx[0] = hi.x; b.mx[1] = hi.y; b.mx[2] = hi.z;
+        const float4 p = ldc(B), q = ldc(B + 1);
+        b.x = lo2(p);
+        b.y = hi2(p);
+        b.z = lo2(q);
     }
     return b;
 }
 
-__device__ __forceinline__ bool box_test(const RayPre& r, const Box& b, float bestT) {
-    return box_hit(r, b.mn[0], b.mn[1], b.mn[2], b.mx[0], b.mx[1], b.mx[2], kRayTMin, bestT);
+// A node's 64-byte record (inode or leaf array), wave-uniform.
+struct NodeRec {
+    float4 a, b, c;
+    uint4 d;
+};
+
+__device__ __forceinline__ NodeRec load_rec(const SceneView& sc, uint32_t ref) {
+    const float4* p = (ref & LEAF_BIT) ? sc.leaf + 4 * (size_t)(ref & ~LEAF_BIT) : sc.inode + 4 * (size_t)ref;
+    return NodeRec{ldc(p), ldc(p + 1), ldc(p + 2), ldc_u(p + 3)};
+}
+
+__device__ __forceinline__ BoxP leaf_box(const NodeRec& r) {
+    return BoxP{hi2(r.c), (v2f){__uint_as_float(r.d.x), __uint_as_float(r.d.y)},
+                (v2f){__uint_as_float(r.d.z), __uint_as_float(r.d.w)}};
 }
 
 // box_hit for the lanes in `act` of a wave (all lanes call it): the float pre-classification
 // for everyone, the exact double test only behind a wave-uniform branch taken when some lane
 // is ambiguous.
-__device__ __forceinline__ bool box_hit_wave(const RayPre& r, float mnx, float mny, float mnz, float mxx,
-                                             float mxy, float mxz, float tmax, bool act) {
-    const float mn[3] = {mnx, mny, mnz}, mx[3] = {mxx, mxy, mxz};
-    const int c = box_classify(r, mn, mx, kRayTMin, tmax);
+__device__ __forceinline__ bool box_hit_wave(const RayPre& r, const BoxP& b, float tmax, bool act) {
+    const int c = box_classify(r, b, kRayTMin, tmax);
     bool res = act && c == BOX_HIT;
     const bool amb = act && c == BOX_AMBIG;
     if (ballot(amb) != 0) {
-        if (amb) res = box_hit_exact(r, mn, mx, (double)kRayTMin, (double)tmax);
+        RT_STAT(12, 1);
+        if (amb) res = box_hit_exact(r, b, (double)kRayTMin, (double)tmax);
     }
     return res;
 }
@@ -195,6 +222,9 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
     hs.bestT = FLT_MAX;
     hs.slot = -1;
     if (alive == 0) return;
+    [[maybe_unused]] const int so = any_hit ? 1 : 0;
+    RT_STAT(0 + so, 1);
+    RT_STAT(13 + so, __popcll(alive));
     uint32_t st_ref = 0, st_mlo = 0, st_mhi = 0, st_ver = 0;  // lane k holds entry k
     int sp = 0;
     uint32_t wave_ver = 0;
@@ -209,22 +239,25 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
         uint64_t mask = ((uint64_t)rdlane(st_mhi, sp) << 32) | rdlane(st_mlo, sp);
         const uint32_t ver = rdlane(st_ver, sp);
         mask &= alive;
+        RT_STAT(2 + so, 1);
         if (mask == 0) continue;
+        RT_STAT(4 + so, 1);
         bool act = (mask & lane_bit) != 0;
+        const NodeRec rec = load_rec(sc, ref);
         if (ver != wave_ver) {  // some lane's bestT changed since the push: pop-time re-test
-            const Box b = own_box(sc, ref, ver == VER_FORCE);
-            const bool pass = box_hit_wave(r, b.mn[0], b.mn[1], b.mn[2], b.mx[0], b.mx[1], b.mx[2], hs.bestT, act);
+            RT_STAT(6 + so, 1);
+            const BoxP ob = (ref & LEAF_BIT) && ver != VER_FORCE ? leaf_box(rec) : own_box(sc, ref, ver == VER_FORCE);
+            const bool pass = box_hit_wave(r, ob, hs.bestT, act);
             mask = ballot(pass);
             act = pass;
             if (mask == 0) continue;
         }
         if (ref & LEAF_BIT) {
+            RT_STAT(10 + so, 1);
             const uint32_t slot = ref & ~LEAF_BIT;
-            const float4* L = sc.leaf + 4 * (size_t)slot;
-            const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
             float t, u, v;
-            const bool h = act && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), kRayTMin,
-                                       hs.bestT, t, u, v);
+            const bool h = act && mt_g(r, mk(rec.a.x, rec.a.y, rec.a.z), mk(rec.b.x, rec.b.y, rec.b.z),
+                                       mk(rec.b.w, rec.c.x, rec.c.y), kRayTMin, hs.bestT, t, u, v);
             if (h) {
                 hs.bestT = t;
                 hs.slot = (int32_t)slot;
@@ -236,12 +269,11 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
             }
             continue;
         }
-        const float4* N = sc.inode + 4 * (size_t)ref;
-        const float4 q0 = ldc(N), q1 = ldc(N + 1), q2 = ldc(N + 2);
-        const uint4 q3 = ldc_u(N + 3);
-        const uint32_t lref = q3.x, rref = q3.y;
+        RT_STAT(8 + so, 1);
+        const uint32_t lref = rec.d.x, rref = rec.d.y;
+        const float4 q0 = rec.a, q1 = rec.b, q2 = rec.c;
         if (lref != NO_REF) {
-            const bool pl = box_hit_wave(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, hs.bestT, act);
+            const bool pl = box_hit_wave(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, act);
             const uint64_t ml = ballot(pl);
             if (ml != 0) {
                 st_ref = wrlane(lref, sp, st_ref);
@@ -252,7 +284,7 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
             }
         }
         if (rref != NO_REF) {
-            const bool pr = box_hit_wave(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, hs.bestT, act);
+            const bool pr = box_hit_wave(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, act);
             const uint64_t mr = ballot(pr);
             if (mr != 0) {
                 st_ref = wrlane(rref, sp, st_ref);
@@ -283,15 +315,14 @@ __device__ __forceinline__ void traverse_lane(const SceneView& sc, const RayPre&
         const uint32_t ref = st_ref[sp];
         const uint32_t pv = st_ver[sp];
         if (pv != ver) {
-            const Box b = own_box(sc, ref, pv == VER_FORCE);
-            if (!box_test(r, b, hs.bestT)) continue;
+            if (!box_hit(r, own_box(sc, ref, pv == VER_FORCE), kRayTMin, hs.bestT)) continue;
         }
         if (ref & LEAF_BIT) {
             const uint32_t slot = ref & ~LEAF_BIT;
             const float4* L = sc.leaf + 4 * (size_t)slot;
             const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
             float t, u, v;
-            if (mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), kRayTMin, hs.bestT, t, u, v)) {
+            if (mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin, hs.bestT, t, u, v)) {
                 hs.bestT = t;
                 hs.slot = (int32_t)slot;
                 ++ver;
@@ -302,14 +333,12 @@ __device__ __forceinline__ void traverse_lane(const SceneView& sc, const RayPre&
         const float4* N = sc.inode + 4 * (size_t)ref;
         const float4 q0 = ldc(N), q1 = ldc(N + 1), q2 = ldc(N + 2);
         const uint4 q3 = ldc_u(N + 3);
-        if (q3.x != NO_REF &&
-            box_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, kRayTMin, hs.bestT)) {
+        if (q3.x != NO_REF && box_hit(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, kRayTMin, hs.bestT)) {
             st_ref[sp] = q3.x;
             st_ver[sp] = ver;
             ++sp;
         }
-        if (q3.y != NO_REF &&
-            box_hit(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, kRayTMin, hs.bestT)) {
+        if (q3.y != NO_REF && box_hit(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, kRayTMin, hs.bestT)) {
             st_ref[sp] = q3.y;
             st_ver[sp] = ver;
             ++sp;
@@ -334,7 +363,7 @@ struct SurfHit {
 __device__ __forceinline__ SurfHit resolve_hit(const SceneView& sc, const RayPre& r, int32_t slot) {
     const float4* L = sc.leaf + 4 * (size_t)slot;
     const float4 a = L[0], b = L[1], c = L[2];
-    const f3 v0 = mk(a.x, a.y, a.z), e1 = mk(b.x, b.y, b.z), e2 = mk(c.x, c.y, c.z);
+    const f3 v0 = mk(a.x, a.y, a.z), e1 = mk(b.x, b.y, b.z), e2 = mk(b.w, c.x, c.y);
     float t = 0.f, u = 0.f, v = 0.f;
     mt_g(r, v0, e1, e2, -FLT_MAX, FLT_MAX, t, u, v);  // same t/u/v as the accepting test
     SurfHit s;
@@ -372,8 +401,10 @@ __device__ __forceinline__ f3 eval_brdf(const DevMaterial& m, f3 N, f3 V, f3 L) 
 }
 
 // One camera sample through TraceRayIterative (query.h:156-220) + ShadeDirect (shader.h).
-// All lanes of a wave call it; `valid` marks lanes owning a sample.
-template <int MODE>
+// All lanes of a wave call it; `valid` marks lanes owning a sample.  D1: max_depth == 1 (no
+// bounce; the configuration the benchmarks run), compiled without the bounce code so the
+// shadow traversal carries less live state.
+template <int MODE, bool D1>
 __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int32_t* prim_idx,
                            float* prim_t) {
     const SceneView& sc = P.sc;
@@ -387,8 +418,9 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
 
     f3 radiance = mk(0.f, 0.f, 0.f);
     f3 thr = mk(1.f, 1.f, 1.f);
-    bool alive = valid && P.max_depth > 0;
-    for (int depth = 0; depth < P.max_depth; ++depth) {
+    const int max_depth = D1 ? 1 : P.max_depth;
+    bool alive = valid && max_depth > 0;
+    for (int depth = 0; depth < max_depth; ++depth) {
         if (ballot(alive) == 0) break;
         HitState hs;
         traverse<MODE>(sc, ray, alive, false, 0.0f, hs);
@@ -405,10 +437,9 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
             alive = false;
         }
         // ShadeDirect (shader.h:65-110)
-        DevMaterial m;
         f3 N = mk(0.f, 0.f, 1.f), V = N, Lo = mk(0.f, 0.f, 0.f);
         if (hit) {
-            m = material_of(sc, sh.tri);
+            const DevMaterial m = material_of(sc, sh.tri);
             N = unit(sh.n);
             V = unit(sub(ray.o, sh.p));
             Lo = add(Lo, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 0.05f));
@@ -417,14 +448,21 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
         for (int li = 0; li < sc.num_lights; ++li) {
             const DevLight& lt = sc.lights[li];
             const f3 lpos = mk(lt.pos[0], lt.pos[1], lt.pos[2]);
-            float NdotL = 0.f, dist = 0.f;
-            f3 L = mk(0.f, 0.f, 0.f);
-            bool need = false;
+            float dist = 0.f;
+            bool need = false, lit = false;
+            f3 contrib = mk(0.f, 0.f, 0.f);
             RayPre sray = ray;
             if (hit) {
-                L = unit(sub(lpos, sh.p));
-                NdotL = fmaxf(dot(N, L), 0.0f);
+                const f3 L = unit(sub(lpos, sh.p));
+                const float NdotL = fmaxf(dot(N, L), 0.0f);
                 if (NdotL > 0.0f) {
+                    // The light's term, added below if the shadow ray is clear (the material is
+                    // re-read per light so it is not live across the traversal).
+                    const DevMaterial m = material_of(sc, sh.tri);
+                    const f3 f = eval_brdf(m, sh.n, V, L);
+                    const f3 rad = scale(mk(lt.color[0], lt.color[1], lt.color[2]), (float)lt.intensity);
+                    contrib = scale(mul(rad, f), NdotL);
+                    lit = true;
                     // IsInShadow (shader.h:44-62)
                     const f3 toL = sub(lpos, sh.p);
                     dist = sqrtf(dot(toL, toL));
@@ -437,16 +475,13 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
             HitState shs;
             traverse<MODE>(sc, sray, need, true, dist, shs);
             const bool occluded = need && shs.slot >= 0 && shs.bestT < dist;
-            if (hit && NdotL > 0.0f && !occluded) {
-                const f3 f = eval_brdf(m, sh.n, V, L);
-                const f3 rad = scale(mk(lt.color[0], lt.color[1], lt.color[2]), (float)lt.intensity);
-                Lo = add(Lo, scale(mul(rad, f), NdotL));
-            }
+            if (lit && !occluded) Lo = add(Lo, contrib);
         }
         if (hit) {
             radiance = add(radiance, mul(thr, Lo));
             // bounce (query.h:193-216); skipped after the last depth where it has no effect
-            if (depth + 1 < P.max_depth) {
+            if (!D1 && depth + 1 < max_depth) {
+                const DevMaterial m = material_of(sc, sh.tri);
                 const float kd = m.kd, kr = m.kr, total = kd + kr;
                 if (total <= 0.0f) {
                     alive = false;
@@ -637,7 +672,7 @@ __device__ __forceinline__ int planned_tile(const RenderParams& P, int len, int 
 
 // One sample per lane: a block covers a tile_w x tile_h pixel tile x spp samples (spp a power
 // of two <= 256, tile_w*tile_h*spp == BLOCK); per-pixel sums run in sample order from LDS.
-template <int MODE>
+template <int MODE, bool D1>
 __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, float* col) {
     const int t = (int)threadIdx.x;
     const int s = t & (P.spp - 1);            // spp and tile_w are powers of two here
@@ -649,7 +684,7 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
     const int y = valid ? global_row(P, r) : 0;
     int32_t pidx = -1;
     float pt = -1.f;
-    const f3 c = trace_sample<MODE>(P, valid, x, y, s, &pidx, &pt);
+    const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, &pidx, &pt);
     if (valid && P.hit_idx) {
         const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp + (size_t)s;
         P.hit_idx[k] = pidx;
@@ -675,7 +710,7 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
 }
 
 // General spp: one pixel per lane looping over its samples in order (query.cu:146-163).
-template <int MODE>
+template <int MODE, bool D1>
 __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
     const int t = (int)threadIdx.x;
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
@@ -687,7 +722,7 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
     for (int s = 0; s < P.spp; ++s) {
         int32_t pidx = -1;
         float pt = -1.f;
-        const f3 c = trace_sample<MODE>(P, valid, x, y, s, &pidx, &pt);
+        const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, &pidx, &pt);
         if (valid && P.hit_idx) {
             const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp + (size_t)s;
             P.hit_idx[k] = pidx;
@@ -706,19 +741,34 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
 
 // Each block runs tiles_per_block virtual blocks (planned_tile): fewer, longer blocks, so
 // the dispatcher does not spend the frame launching blocks that find no live tile.
-template <int MODE, bool SAMPLES>
+template <int MODE, bool SAMPLES, bool D1>
 __global__ __launch_bounds__(BLOCK, 4) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
     const int b = (int)blockIdx.x, g = (int)gridDim.x;
     const int q = P.nqueues == 1 ? 0 : (b & 7);
     const int len = list_length(P, q);
-    for (int m = 0; m < P.tiles_per_block; ++m) {
-        const int j = b + m * g;
-        if (j >= P.tiles_virtual) break;
-        const int tile = planned_tile(P, len, q, P.nqueues == 1 ? j : (j >> 3));
-        if (tile < 0) continue;
-        if constexpr (SAMPLES) samples_tile<MODE>(P, tile, col);
-        else pixels_tile<MODE>(P, tile);
+    // Next live virtual block of this block from m on (m = tiles_per_block: none).  The block
+    // leaves before the tile loop when it has none, so blocks without work skip the loop's
+    // set-up (the compiler hoists per-sample invariants, and their spills, in front of it).
+    auto next_tile = [&](int& m) {
+        for (; m < P.tiles_per_block; ++m) {
+            const int j = b + m * g;
+            if (j >= P.tiles_virtual) break;
+            const int tile = planned_tile(P, len, q, P.nqueues == 1 ? j : (j >> 3));
+            if (tile >= 0) return tile;
+        }
+        m = P.tiles_per_block;
+        return -1;
+    };
+    int m = 0;
+    int tile = next_tile(m);
+    if (tile < 0) return;
+    for (;;) {
+        if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col);
+        else pixels_tile<MODE, D1>(P, tile);
+        ++m;
+        tile = next_tile(m);
+        if (tile < 0) break;
         if constexpr (SAMPLES) __syncthreads();  // col is rewritten by the next tile
     }
 }
@@ -1007,15 +1057,15 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
         if (!(c & LEAF_BIT)) {
             const rt_aabb lb = nd.left_idx != NO_REF ? aabbs[nd.left_idx] : rt_aabb{};
             const rt_aabb rb = nd.right_idx != NO_REF ? aabbs[nd.right_idx] : rt_aabb{};
-            float4* q = &hin[4 * c];
-            q[0] = make_float4(lb.min_corner.x, lb.min_corner.y, lb.min_corner.z, lb.max_corner.x);
-            q[1] = make_float4(lb.max_corner.y, lb.max_corner.z, rb.min_corner.x, rb.min_corner.y);
-            q[2] = make_float4(rb.min_corner.z, rb.max_corner.x, rb.max_corner.y, rb.max_corner.z);
+            float4* q = &hin[4 * c];  // per axis (min, max) pairs: left x y | left z, right x | right y z
+            q[0] = make_float4(lb.min_corner.x, lb.max_corner.x, lb.min_corner.y, lb.max_corner.y);
+            q[1] = make_float4(lb.min_corner.z, lb.max_corner.z, rb.min_corner.x, rb.max_corner.x);
+            q[2] = make_float4(rb.min_corner.y, rb.max_corner.y, rb.min_corner.z, rb.max_corner.z);
             uint32_t refs[4] = {ref_of(nd.left_idx), ref_of(nd.right_idx), 0u, 0u};
             std::memcpy(&q[3], refs, 16);
             const rt_aabb& ob = aabbs[n];
-            hib[2 * c] = make_float4(ob.min_corner.x, ob.min_corner.y, ob.min_corner.z, 0.f);
-            hib[2 * c + 1] = make_float4(ob.max_corner.x, ob.max_corner.y, ob.max_corner.z, 0.f);
+            hib[2 * c] = make_float4(ob.min_corner.x, ob.max_corner.x, ob.min_corner.y, ob.max_corner.y);
+            hib[2 * c + 1] = make_float4(ob.min_corner.z, ob.max_corner.z, 0.f, 0.f);
         } else {
             const uint32_t j = c & ~LEAF_BIT;
             const rt_triangle& t = tris[nd.object_idx];
@@ -1025,10 +1075,11 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
             float tif;
             std::memcpy(&tif, &ti, 4);
             // e1 = v1 - v0, e2 = v2 - v0 exactly as intersectTriangle computes them
+            // v0 | e1, e2.x | e2.y e2.z, box x pair | box y pair, box z pair
             q[0] = make_float4(t.v0.x, t.v0.y, t.v0.z, tif);
-            q[1] = make_float4(t.v1.x - t.v0.x, t.v1.y - t.v0.y, t.v1.z - t.v0.z, ob.min_corner.x);
-            q[2] = make_float4(t.v2.x - t.v0.x, t.v2.y - t.v0.y, t.v2.z - t.v0.z, ob.min_corner.y);
-            q[3] = make_float4(ob.min_corner.z, ob.max_corner.x, ob.max_corner.y, ob.max_corner.z);
+            q[1] = make_float4(t.v1.x - t.v0.x, t.v1.y - t.v0.y, t.v1.z - t.v0.z, t.v2.x - t.v0.x);
+            q[2] = make_float4(t.v2.y - t.v0.y, t.v2.z - t.v0.z, ob.min_corner.x, ob.max_corner.x);
+            q[3] = make_float4(ob.min_corner.y, ob.max_corner.y, ob.min_corner.z, ob.max_corner.z);
         }
     }
     for (size_t t = 0; t < P; ++t) {
@@ -1124,7 +1175,9 @@ int prepare_jitter(rt_scene* s, const rt_render_opts* o) {
 template <int MODE, bool SAMPLES>
 void launch_mode(const RenderParams& P, hipStream_t st) {
     const int g = (P.tiles_virtual + P.tiles_per_block - 1) / P.tiles_per_block;
-    hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES>), dim3((g + 7) / 8 * 8), dim3(BLOCK), 0, st, P);
+    const dim3 grid((g + 7) / 8 * 8);
+    if (P.max_depth == 1) hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES, true>), grid, dim3(BLOCK), 0, st, P);
+    else hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES, false>), grid, dim3(BLOCK), 0, st, P);
 }
 
 template <int MODE>
@@ -1266,6 +1319,18 @@ extern "C" int rt_live_tiles(const rt_scene* s, int64_t* live, int64_t* total) {
     for (int k = 0; k < 8; ++k) *live += c[k * COUNTER_STRIDE];
     return RT_OK;
 }
+
+#ifdef RT_STATS
+extern "C" int rt_debug_stats(unsigned long long* out, int reset) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_stats), sizeof(g_rt_stats)));
+    if (reset) {
+        unsigned long long z[16] = {};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rt_stats), z, sizeof(z)));
+    }
+    return RT_OK;
+}
+#endif
 
 extern "C" int rt_kernel_times(const rt_scene* s, float* ms_out, int max, int* n_out) {
     return event_times(s, s ? s->evm : nullptr, ms_out, max, n_out);
@@ -1446,9 +1511,10 @@ extern "C" int rt_box_test_host(const float* rays, const float* boxes, const flo
         const float* R = rays + 6 * i;
         const float* B = boxes + 6 * i;
         const RayPre r = make_ray(mk(R[0], R[1], R[2]), mk(R[3], R[4], R[5]));
-        out_class[i] = box_classify(r, B, B + 3, tminmax[2 * i], tminmax[2 * i + 1]);
-        out_fast[i] = box_hit(r, B[0], B[1], B[2], B[3], B[4], B[5], tminmax[2 * i], tminmax[2 * i + 1]) ? 1 : 0;
-        out_exact[i] = box_hit_exact(r, B, B + 3, (double)tminmax[2 * i], (double)tminmax[2 * i + 1]) ? 1 : 0;
+        const BoxP b = {(v2f){B[0], B[3]}, (v2f){B[1], B[4]}, (v2f){B[2], B[5]}};
+        out_class[i] = box_classify(r, b, tminmax[2 * i], tminmax[2 * i + 1]);
+        out_fast[i] = box_hit(r, b, tminmax[2 * i], tminmax[2 * i + 1]) ? 1 : 0;
+        out_exact[i] = box_hit_exact(r, b, (double)tminmax[2 * i], (double)tminmax[2 * i + 1]) ? 1 : 0;
     }
     return RT_OK;
 }

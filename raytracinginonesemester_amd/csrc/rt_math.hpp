@@ -40,13 +40,24 @@ __host__ __device__ __forceinline__ f3 cam_unit(f3 v) {
     return divf(v, len);
 }
 
+// An axis-aligned box as the kernels hold it: per axis the (min, max) pair, adjacent so one
+// packed instruction handles both slabs of an axis.
+typedef float v2f __attribute__((ext_vector_type(2)));
+struct BoxP {
+    v2f x, y, z;
+};
+
+// Relative slack of the float pre-classification (see box_classify).
+constexpr float kBoxRel = 4e-6f;
+
 // A ray as the slab test needs it.  `par` bit a: |dir[a]| < 1e-8f, where intersectAABB
 // degenerates to an exact inside test on that axis (bvh.h:90-91).  `invf` is a float
-// reciprocal of the direction (any <= 2 ulp approximation), +inf on parallel axes, used only
-// by the conservative pre-classification below, never to decide an ambiguous case.
+// reciprocal of the direction (any <= 2 ulp approximation), +inf on parallel axes; it and
+// oiv = o * invf serve the pre-classification below only, never the decision of an
+// ambiguous case.
 struct RayPre {
     f3 o, d;
-    f3 invf;
+    f3 invf, oiv;
     uint32_t par;
 };
 
@@ -66,6 +77,7 @@ __host__ __device__ __forceinline__ RayPre make_ray(f3 o, f3 d) {
     const bool px = fabsf(d.x) < eps, py = fabsf(d.y) < eps, pz = fabsf(d.z) < eps;
     r.par = (px ? 1u : 0u) | (py ? 2u : 0u) | (pz ? 4u : 0u);
     r.invf = mk(px ? INFINITY : rcp_approx(d.x), py ? INFINITY : rcp_approx(d.y), pz ? INFINITY : rcp_approx(d.z));
+    r.oiv = mk(o.x * r.invf.x, o.y * r.invf.y, o.z * r.invf.z);
     return r;
 }
 
@@ -73,10 +85,10 @@ __host__ __device__ __forceinline__ RayPre make_ray(f3 o, f3 d) {
 // per axis inv = 1.0/double(dir), tNear/tFar = (double(bound) - double(orig)) * inv,
 // reference compare/swap order.  The boolean equals the reference's early-return form
 // because t0 only grows and t1 only shrinks.
-__host__ __device__ inline bool box_hit_exact(const RayPre& r, const float mn[3], const float mx[3], double tmin,
-                                              double tmax) {
+__host__ __device__ inline bool box_hit_exact(const RayPre& r, const BoxP& b, double tmin, double tmax) {
     double t0 = tmin, t1 = tmax;
     const float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+    const float mn[3] = {b.x.x, b.y.x, b.z.x}, mx[3] = {b.x.y, b.y.y, b.z.y};
     bool ok = true;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -101,36 +113,41 @@ __host__ __device__ inline bool box_hit_exact(const RayPre& r, const float mn[3]
 
 // Conservative float pre-classification of the same test: MISS / HIT are returned only when
 // the reference's double computation is guaranteed to give that answer; AMBIG otherwise.
-// Error budget (finite inputs): the reference's tNear/tFar carry <= 3 double roundings
-// (<= 3.4e-16 relative to the exact (bound-orig)/dir), the float estimates here <= 3 float
-// roundings + a 1-ulp reciprocal (<= 3.6e-7), and the +-E adjustments below one more float
-// rounding; E = 4e-6 * max(|tn'|,|tf'|) + 1e-30 bounds their distance with > 10x slack (the
-// 1e-30 term covers subnormal absolute error).  With Lmax = max over axes of the exact
-// reference lows, Hmin = min of the highs (tmin/tmax are exact in both precisions):
+// Per axis the slab parameters are estimated as tn' = fma(bound, invf, -oiv) (one packed
+// FMA for both bounds).  Error budget (finite inputs): with invf = (1/d)(1+e1), |e1| <= 2^-23
+// (1-ulp reciprocal), oiv = o*invf*(1+e2) and the FMA's rounding e3 (|e2|,|e3| <= 2^-24),
+// |tn' - t| <= 1.8e-7 |t| + 6e-8 |oiv|, while the reference's double tNear/tFar sit within
+// 3.4e-16 |t| of the exact (bound-orig)/dir.  E = kBoxRel * (max(|tn'|,|tf'|) + |oiv|) +
+// 1e-30 (kBoxRel = 4e-6) bounds the distance between the two with > 10x slack, also covering
+// the float rounding of E and of the +-E adjustments below; the 1e-30 term covers subnormal
+// absolute error.  With Lmax = max over axes of the reference lows and Hmin = min of
+// the highs (tmin/tmax are exact in both precisions):
 //   MISS  if max(tmin, lo'-E) > min(tmax, hi'+E)      (then Lmax > Hmin: reference rejects)
 //   HIT   if max(tmin, lo'+E) <= min(tmax, hi'-E)     (then Lmax <= Hmin: reference accepts)
-// Branch-free over the axes: a parallel axis has invf = +inf, so its tn'/tf' are +-inf or
-// NaN and its E is +inf or NaN; fmaxf/fminf drop the NaN terms and +-inf - inf terms, so the
-// axis constrains nothing, and the sum of the E's (non-finite) rules HIT out.  MISS then
-// rests on the other axes alone, which is sound since the reference's t-interval is the
-// intersection over its non-parallel axes (its inside test can only reject more).  The same
-// sum rules HIT out for estimates near FLT_MAX; NaN compares false and falls to AMBIG.
+// Branch-free over the axes: a parallel axis has invf = +inf and oiv = +-inf or NaN, so its
+// tn'/tf' are +-inf or NaN and its E is +inf or NaN; fmaxf/fminf drop the NaN terms and the
+// +-inf -+ inf terms cannot tighten the bounds, so the axis constrains nothing, and the sum of
+// the E's (non-finite) rules HIT out.  MISS then rests on the other axes alone, which is
+// sound since the reference's t-interval is the intersection over its non-parallel axes (its
+// inside test can only reject more).  The same sum rules HIT out for estimates near FLT_MAX;
+// NaN compares false and falls to AMBIG.
 enum : int { BOX_MISS = 0, BOX_HIT = 1, BOX_AMBIG = 2 };
-__host__ __device__ __forceinline__ int box_classify(const RayPre& r, const float mn[3], const float mx[3],
-                                                     float tmin, float tmax) {
-    const float o[3] = {r.o.x, r.o.y, r.o.z}, iv[3] = {r.invf.x, r.invf.y, r.invf.z};
+__host__ __device__ __forceinline__ int box_classify(const RayPre& r, const BoxP& b, float tmin, float tmax) {
+    const v2f bb[3] = {b.x, b.y, b.z};
+    const float iv[3] = {r.invf.x, r.invf.y, r.invf.z}, oiv[3] = {r.oiv.x, r.oiv.y, r.oiv.z};
     float lowLo = tmin, lowHi = tmin, highLo = tmax, highHi = tmax, esum = 0.f;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const float tn = (mn[a] - o[a]) * iv[a];
-        const float tf = (mx[a] - o[a]) * iv[a];
-        const float lo = fminf(tn, tf), hi = fmaxf(tn, tf);
-        const float E = 4e-6f * fmaxf(fabsf(tn), fabsf(tf)) + 1e-30f;
-        esum = esum + E;
-        lowLo = fmaxf(lowLo, lo - E);
-        lowHi = fmaxf(lowHi, lo + E);
-        highLo = fminf(highLo, hi - E);
-        highHi = fminf(highHi, hi + E);
+        const v2f t = __builtin_elementwise_fma(bb[a], (v2f)(iv[a]), (v2f)(-oiv[a]));
+        const float lo = fminf(t.x, t.y), hi = fmaxf(t.x, t.y);
+        const float E = __builtin_fmaf(kBoxRel, fmaxf(fabsf(t.x), fabsf(t.y)) + fabsf(oiv[a]), 1e-30f);
+        esum = a == 0 ? E : esum + E;
+        const v2f lw = (v2f)(lo) + (v2f){-E, E};
+        const v2f hg = (v2f)(hi) + (v2f){-E, E};
+        lowLo = fmaxf(lowLo, lw.x);
+        lowHi = fmaxf(lowHi, lw.y);
+        highLo = fminf(highLo, hg.x);
+        highHi = fminf(highHi, hg.y);
     }
     if (lowLo > highHi) return BOX_MISS;
     if (esum < 3.0e38f && lowHi <= highLo) return BOX_HIT;
@@ -138,12 +155,10 @@ __host__ __device__ __forceinline__ int box_classify(const RayPre& r, const floa
 }
 
 // intersectAABB with the float fast path; bit-identical answer to box_hit_exact.
-__host__ __device__ __forceinline__ bool box_hit(const RayPre& r, float mnx, float mny, float mnz, float mxx,
-                                                 float mxy, float mxz, float tmin, float tmax) {
-    const float mn[3] = {mnx, mny, mnz}, mx[3] = {mxx, mxy, mxz};
-    const int c = box_classify(r, mn, mx, tmin, tmax);
+__host__ __device__ __forceinline__ bool box_hit(const RayPre& r, const BoxP& b, float tmin, float tmax) {
+    const int c = box_classify(r, b, tmin, tmax);
     if (c != BOX_AMBIG) return c == BOX_HIT;
-    return box_hit_exact(r, mn, mx, (double)tmin, (double)tmax);
+    return box_hit_exact(r, b, (double)tmin, (double)tmax);
 }
 
 // Möller–Trumbore of intersectTriangle (query.h:72-108) with e1 = v1-v0, e2 = v2-v0

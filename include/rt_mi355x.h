@@ -177,7 +177,8 @@ typedef struct {
 } rt_render_opts;
 
 enum {
-    RT_FLAG_NO_CULL = 1       /* disable tile culling against the root box (A/B; same output) */
+    RT_FLAG_NO_CULL = 1,      /* disable tile culling against the root box (A/B; same output) */
+    RT_FLAG_BINARY = 4        /* wave traversal over the binary nodes, not the 4-ary records */
 };
 
 enum {

@@ -20,6 +20,7 @@ RT_ERR = {
 RT_KERNEL_AUTO, RT_KERNEL_WAVE, RT_KERNEL_LANE, RT_KERNEL_WAVE_PIXELS = 0, 1, 2, 3
 RT_TILES_AUTO, RT_TILES_LINEAR, RT_TILES_XCD_CHUNK, RT_TILES_ROWS = 0, 1, 2, 3
 RT_FLAG_NO_CULL = 1
+RT_FLAG_BINARY = 4
 
 
 class RTError(RuntimeError):

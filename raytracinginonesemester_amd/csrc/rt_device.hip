@@ -63,6 +63,7 @@ struct DevLight {
 
 struct SceneView {
     const float4* __restrict__ inode;
+    const float4* __restrict__ wnode;  // 4-ary records (8 x float4) by internal index, if wide
     const float4* __restrict__ ibox;
     const float4* __restrict__ leaf;
     const float4* __restrict__ tnorm;
@@ -72,7 +73,11 @@ struct SceneView {
     int32_t num_tris, num_mats, num_lights;
     uint32_t root_ref;
     float root_box[6];
+    float bmax[3];  // per axis max |coordinate| over every AABB of the scene (make_ray)
+    int32_t wide;
 };
+
+__device__ __forceinline__ f3 scene_bmax(const SceneView& sc) { return mk(sc.bmax[0], sc.bmax[1], sc.bmax[2]); }
 
 struct RenderParams {
     SceneView sc;
@@ -214,8 +219,9 @@ struct HitState {
 // lanes that own a ray.  any_hit_dist > 0: shadow query — a lane stops as soon as its
 // bestT < dist (bestT only decreases, so the reference's final `hit && t < dist` is then
 // already true); the traversal order up to that point is the reference's.
-__device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre& r, bool active,
-                                              bool any_hit, float any_hit_dist, HitState& hs) {
+template <bool WIDE>
+__device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const RayPre& r, bool active,
+                                                   bool any_hit, float any_hit_dist, HitState& hs) {
     const uint32_t lane = lane_id();
     const uint64_t lane_bit = 1ull << lane;
     uint64_t alive = ballot(active);
@@ -243,21 +249,31 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
         if (mask == 0) continue;
         RT_STAT(4 + so, 1);
         bool act = (mask & lane_bit) != 0;
-        const NodeRec rec = load_rec(sc, ref);
+        const bool leaf = (ref & LEAF_BIT) != 0;
+        const float4* L = sc.leaf + 4 * (size_t)(ref & ~LEAF_BIT);
         if (ver != wave_ver) {  // some lane's bestT changed since the push: pop-time re-test
             RT_STAT(6 + so, 1);
-            const BoxP ob = (ref & LEAF_BIT) && ver != VER_FORCE ? leaf_box(rec) : own_box(sc, ref, ver == VER_FORCE);
+            BoxP ob;
+            if (ver == VER_FORCE) {
+                ob = own_box(sc, ref, true);
+            } else if (leaf) {
+                const float4 c = ldc(L + 2), d = ldc(L + 3);
+                ob = BoxP{hi2(c), lo2(d), hi2(d)};
+            } else {
+                ob = own_box(sc, ref, false);
+            }
             const bool pass = box_hit_wave(r, ob, hs.bestT, act);
             mask = ballot(pass);
             act = pass;
             if (mask == 0) continue;
         }
-        if (ref & LEAF_BIT) {
+        if (leaf) {
             RT_STAT(10 + so, 1);
             const uint32_t slot = ref & ~LEAF_BIT;
+            const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
             float t, u, v;
-            const bool h = act && mt_g(r, mk(rec.a.x, rec.a.y, rec.a.z), mk(rec.b.x, rec.b.y, rec.b.z),
-                                       mk(rec.b.w, rec.c.x, rec.c.y), kRayTMin, hs.bestT, t, u, v);
+            const bool h = act && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin,
+                                       hs.bestT, t, u, v);
             if (h) {
                 hs.bestT = t;
                 hs.slot = (int32_t)slot;
@@ -270,8 +286,32 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
             continue;
         }
         RT_STAT(8 + so, 1);
-        const uint32_t lref = rec.d.x, rref = rec.d.y;
-        const float4 q0 = rec.a, q1 = rec.b, q2 = rec.c;
+        if constexpr (WIDE) {
+            // 4-ary record: up to four entries in push order, each pushed if some lane passes.
+            const float4* W = sc.wnode + 8 * (size_t)ref;
+            const uint4 wr = ldc_u(W + 6);
+            const uint32_t refs[4] = {wr.x, wr.y, wr.z, wr.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (refs[k] == NO_REF) continue;
+                const float4 p = ldc(W + (3 * k) / 2), q = ldc(W + (3 * k) / 2 + 1);
+                const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
+                const bool pk = box_hit_wave(r, bk, hs.bestT, act);
+                const uint64_t mk_ = ballot(pk);
+                if (mk_ != 0) {
+                    st_ref = wrlane(refs[k], sp, st_ref);
+                    st_mlo = wrlane((uint32_t)mk_, sp, st_mlo);
+                    st_mhi = wrlane((uint32_t)(mk_ >> 32), sp, st_mhi);
+                    st_ver = wrlane(wave_ver, sp, st_ver);
+                    ++sp;
+                }
+            }
+            continue;
+        }
+        const float4* N = sc.inode + 4 * (size_t)ref;
+        const float4 q0 = ldc(N), q1 = ldc(N + 1), q2 = ldc(N + 2);
+        const uint4 q3 = ldc_u(N + 3);
+        const uint32_t lref = q3.x, rref = q3.y;
         if (lref != NO_REF) {
             const bool pl = box_hit_wave(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, act);
             const uint64_t ml = ballot(pl);
@@ -295,6 +335,12 @@ __device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre&
             }
         }
     }
+}
+
+__device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre& r, bool active,
+                                              bool any_hit, float any_hit_dist, HitState& hs) {
+    if (sc.wide) traverse_wave_impl<true>(sc, r, active, any_hit, any_hit_dist, hs);
+    else traverse_wave_impl<false>(sc, r, active, any_hit, any_hit_dist, hs);
 }
 
 // ---- LANE traversal (private stack per lane; the reference's shape) ---------------------
@@ -400,25 +446,100 @@ __device__ __forceinline__ f3 eval_brdf(const DevMaterial& m, f3 N, f3 V, f3 L) 
     return add(fd, fs);
 }
 
-// One camera sample through TraceRayIterative (query.h:156-220) + ShadeDirect (shader.h).
-// All lanes of a wave call it; `valid` marks lanes owning a sample.  D1: max_depth == 1 (no
-// bounce; the configuration the benchmarks run), compiled without the bounce code so the
-// shadow traversal carries less live state.
-template <int MODE, bool D1>
-__device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int32_t* prim_idx,
-                           float* prim_t) {
-    const SceneView& sc = P.sc;
-    // Camera::get_ray(float, float) (camera.h:49-53) with the jittered_samples offsets
+// Camera::get_ray(float, float) (camera.h:49-53) with the jittered_samples offsets.
+__device__ __forceinline__ RayPre camera_ray(const RenderParams& P, bool valid, int x, int y, int s) {
     const float jx = valid ? P.jitter[2 * s] : 0.f;
     const float jy = valid ? P.jitter[2 * s + 1] : 0.f;
     const float px = (float)x + jx, py = (float)y + jy;
     const f3 pix = add(add(P.cam_p00, scale(P.cam_du, px)), scale(P.cam_dv, py));
-    RayPre ray = make_ray(P.cam_center, cam_unit(sub(pix, P.cam_center)));
+    return make_ray(P.cam_center, cam_unit(sub(pix, P.cam_center)), scene_bmax(P.sc));
+}
+
+// The rest of TraceRayIterative at maxDepth 1 once the camera ray's closest hit is known:
+// missColor on a miss (query.h:181-183), else ShadeDirect (shader.h:65-110) with one shadow
+// ray per light; the bounce has no effect at depth 1 and is not traced.  All lanes of a wave
+// call it (the shadow traversals are wave-wide).
+template <int MODE>
+__device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid, const RayPre& ray, const HitState& hs) {
+    const SceneView& sc = P.sc;
+    const bool hit = valid && hs.slot >= 0;
+    f3 radiance = mk(0.f, 0.f, 0.f);
+    if (valid && !hit) radiance = add(radiance, mul(mk(1.f, 1.f, 1.f), P.miss));
+    if (ballot(hit) == 0) return clamp01(radiance);
+    SurfHit sh;
+    sh.tri = -1;
+    if (hit) sh = resolve_hit(sc, ray, hs.slot);
+    f3 N = mk(0.f, 0.f, 1.f), V = N, Lo = mk(0.f, 0.f, 0.f);
+    if (hit) {
+        const DevMaterial m = material_of(sc, sh.tri);
+        N = unit(sh.n);
+        V = unit(sub(ray.o, sh.p));
+        Lo = add(Lo, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 0.05f));
+        Lo = add(Lo, mk(m.emission[0], m.emission[1], m.emission[2]));
+    }
+    for (int li = 0; li < sc.num_lights; ++li) {
+        const DevLight& lt = sc.lights[li];
+        const f3 lpos = mk(lt.pos[0], lt.pos[1], lt.pos[2]);
+        float dist = 0.f;
+        bool need = false, lit = false;
+        f3 contrib = mk(0.f, 0.f, 0.f);
+        RayPre sray = ray;
+        if (hit) {
+            const f3 L = unit(sub(lpos, sh.p));
+            const float NdotL = fmaxf(dot(N, L), 0.0f);
+            if (NdotL > 0.0f) {
+                // The light's term, added below if the shadow ray is clear (the material is
+                // re-read per light so it is not live across the traversal).
+                const DevMaterial m = material_of(sc, sh.tri);
+                const f3 f = eval_brdf(m, sh.n, V, L);
+                const f3 rad = scale(mk(lt.color[0], lt.color[1], lt.color[2]), (float)lt.intensity);
+                contrib = scale(mul(rad, f), NdotL);
+                lit = true;
+                // IsInShadow (shader.h:44-62)
+                const f3 toL = sub(lpos, sh.p);
+                dist = sqrtf(dot(toL, toL));
+                if (dist > 0.0f) {
+                    need = true;
+                    sray = make_ray(add(sh.p, scale(N, RT_EPS)), divf(toL, dist), scene_bmax(sc));
+                }
+            }
+        }
+        HitState shs;
+        traverse<MODE>(sc, sray, need, true, dist, shs);
+        const bool occluded = need && shs.slot >= 0 && shs.bestT < dist;
+        if (lit && !occluded) Lo = add(Lo, contrib);
+    }
+    if (hit) radiance = add(radiance, mul(mk(1.f, 1.f, 1.f), Lo));
+    return clamp01(radiance);
+}
+
+// Triangle index of a leaf (the primary-hit AOV).
+__device__ __forceinline__ int32_t leaf_tri(const SceneView& sc, int32_t slot) {
+    return __float_as_int(sc.leaf[4 * (size_t)slot].w);
+}
+
+// One camera sample through TraceRayIterative (query.h:156-220) + ShadeDirect (shader.h).
+// All lanes of a wave call it; `valid` marks lanes owning a sample.  D1: max_depth == 1 (no
+// bounce; the configuration the benchmarks run).
+template <int MODE, bool D1>
+__device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int32_t* prim_idx,
+                           float* prim_t) {
+    const SceneView& sc = P.sc;
+    RayPre ray = camera_ray(P, valid, x, y, s);
+    if constexpr (D1) {
+        HitState hs;
+        traverse<MODE>(sc, ray, valid, false, 0.0f, hs);
+        if (valid) {
+            *prim_idx = hs.slot >= 0 ? leaf_tri(sc, hs.slot) : -1;
+            *prim_t = hs.slot >= 0 ? hs.bestT : -1.0f;
+        }
+        return shade_d1<MODE>(P, valid, ray, hs);
+    }
     uint32_t rng = make_rng_seed(x, y, s);
 
     f3 radiance = mk(0.f, 0.f, 0.f);
     f3 thr = mk(1.f, 1.f, 1.f);
-    const int max_depth = D1 ? 1 : P.max_depth;
+    const int max_depth = P.max_depth;
     bool alive = valid && max_depth > 0;
     for (int depth = 0; depth < max_depth; ++depth) {
         if (ballot(alive) == 0) break;
@@ -468,7 +589,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
                     dist = sqrtf(dot(toL, toL));
                     if (dist > 0.0f) {
                         need = true;
-                        sray = make_ray(add(sh.p, scale(N, RT_EPS)), divf(toL, dist));
+                        sray = make_ray(add(sh.p, scale(N, RT_EPS)), divf(toL, dist), scene_bmax(sc));
                     }
                 }
             }
@@ -480,7 +601,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
         if (hit) {
             radiance = add(radiance, mul(thr, Lo));
             // bounce (query.h:193-216); skipped after the last depth where it has no effect
-            if (!D1 && depth + 1 < max_depth) {
+            if (depth + 1 < max_depth) {
                 const DevMaterial m = material_of(sc, sh.tri);
                 const float kd = m.kd, kr = m.kr, total = kd + kr;
                 if (total <= 0.0f) {
@@ -491,13 +612,13 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
                     if (P.diffuse_bounce && xi < kd / total) {
                         f3 dd = random_unit_vector(rng);
                         if (!(dot(dd, Nb) > 0.0f)) dd = mk(-dd.x, -dd.y, -dd.z);
-                        ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), dd);
+                        ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), dd, scene_bmax(sc));
                         const float nl = fmaxf(dot(Nb, dd), 0.0f);
                         thr = mul(thr, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 2.0f * nl));
                     } else {
                         const f3 I = unit(ray.d);
                         const f3 refl = sub(I, scale(Nb, 2.0f * dot(I, Nb)));
-                        ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), refl);
+                        ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), refl, scene_bmax(sc));
                         thr = mul(thr, scale(mk(m.spec[0], m.spec[1], m.spec[2]), kr));
                     }
                     if (thr.x < 1e-4f && thr.y < 1e-4f && thr.z < 1e-4f) alive = false;
@@ -884,7 +1005,7 @@ __global__ __launch_bounds__(BLOCK) void intersect_kernel(f3 v0, f3 e1, f3 e2, f
         d = unit(d);
         h = mt_hw1(o, d, v0, e1, e2, t, u, v);
     } else {
-        const RayPre r = make_ray(o, d);
+        const RayPre r = make_ray_mt(o, d);
         h = mt_g(r, v0, e1, e2, tmin, tmax, t, u, v);
     }
     hit[i] = h ? 1 : 0;
@@ -960,7 +1081,9 @@ struct rt_scene {
     int nmat = 0, nlights = 0;
     uint32_t root_ref = 0;
     float root_box[6] = {0, 0, 0, 0, 0, 0};
-    DevBuf inode, ibox, leaf, tnorm, objids, mats, lights, jitter;
+    float bmax[3] = {0, 0, 0};
+    DevBuf inode, wnode, ibox, leaf, tnorm, objids, mats, lights, jitter;
+    bool wide = false;
     DevBuf work;  // live tile list counters + the lists
     int64_t last_tiles_total = 0;
     int cus = 256;
@@ -1013,9 +1136,36 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
             cid[n] = LEAF_BIT | uint32_t(n_leaf++);
         }  // leaves naming no valid triangle are skipped by SearchBVH (query.h:263): NO_REF
     }
+    // Wide (4-ary) records: internal node n lists the children of its children in SearchBVH's
+    // push order (a leaf child stands for itself), so one visit tests and pushes what the
+    // reference reaches in two.  The result is the same provided every internal child's box
+    // contains its children's boxes (the pass the skipped test would give is then implied,
+    // slab tests being monotone in the box), checked here; the wave path falls back to the
+    // binary records otherwise, or when the 4-ary DFS stack would exceed 64 entries.
+    auto ref_of0 = [&](uint32_t n) -> uint32_t { return n == NO_REF ? NO_REF : cid[n]; };
+    auto wide_entries = [&](const rt_bvh_node& nd, uint32_t* e) {
+        int k = 0;
+        for (const uint32_t c : {nd.left_idx, nd.right_idx}) {
+            if (ref_of0(c) == NO_REF) continue;
+            if (ref_of0(c) & LEAF_BIT) {
+                e[k++] = c;
+                continue;
+            }
+            const rt_bvh_node& cn = nodes[c];
+            if (ref_of0(cn.left_idx) != NO_REF) e[k++] = cn.left_idx;
+            if (ref_of0(cn.right_idx) != NO_REF) e[k++] = cn.right_idx;
+        }
+        return k;
+    };
+    auto contains = [](const rt_aabb& o, const rt_aabb& i) {
+        return o.min_corner.x <= i.min_corner.x && o.min_corner.y <= i.min_corner.y &&
+               o.min_corner.z <= i.min_corner.z && o.max_corner.x >= i.max_corner.x &&
+               o.max_corner.y >= i.max_corner.y && o.max_corner.z >= i.max_corner.z;
+    };
+    bool wide_ok = true;
     {
         std::vector<uint8_t> state(NN, 0);  // 0 new, 1 on path, 2 done
-        std::vector<int> S(NN, 0);
+        std::vector<int> S(NN, 0), SW(NN, 0);
         std::vector<std::pair<uint32_t, bool>> st{{0u, false}};
         while (!st.empty()) {
             auto [v, post] = st.back();
@@ -1041,13 +1191,26 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
                     if (nd.right_idx != NO_REF) s = std::max(s, (nd.left_idx != NO_REF ? 1 : 0) + sr);
                     if (nd.left_idx != NO_REF) s = std::max(s, sl);
                     S[v] = s;
+                    for (const uint32_t c : {nd.left_idx, nd.right_idx}) {
+                        if (c == NO_REF || nodes[c].object_idx != 0xFFFFFFFFu) continue;
+                        for (const uint32_t g : {nodes[c].left_idx, nodes[c].right_idx})
+                            if (g != NO_REF && !contains(aabbs[c], aabbs[g])) wide_ok = false;
+                    }
+                    uint32_t e[4];
+                    const int k = wide_entries(nd, e);
+                    int sw = k;
+                    for (int i = 0; i < k; ++i)
+                        if (!(ref_of0(e[i]) & LEAF_BIT)) sw = std::max(sw, i + SW[e[i]]);
+                    SW[v] = sw;
                 }
             }
         }
         if (std::max(1, S[0]) > STACK_CAP)
             return set_error(RT_ERR_UNSUPPORTED, "BVH needs a DFS stack deeper than 64 entries");
+        if (std::max(1, SW[0]) > STACK_CAP) wide_ok = false;
     }
     std::vector<float4> hin(4 * std::max<size_t>(n_int, 1)), hib(2 * std::max<size_t>(n_int, 1));
+    std::vector<float4> hwn(wide_ok ? 8 * std::max<size_t>(n_int, 1) : 0);
     std::vector<float4> hlf(4 * std::max<size_t>(n_leaf, 1)), hnm(3 * P);
     auto ref_of = [&](uint32_t n) -> uint32_t { return n == NO_REF ? NO_REF : cid[n]; };
     for (size_t n = 0; n < NN; ++n) {
@@ -1066,6 +1229,20 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
             const rt_aabb& ob = aabbs[n];
             hib[2 * c] = make_float4(ob.min_corner.x, ob.max_corner.x, ob.min_corner.y, ob.max_corner.y);
             hib[2 * c + 1] = make_float4(ob.min_corner.z, ob.max_corner.z, 0.f, 0.f);
+            if (wide_ok) {  // 4 x (x pair, y pair, z pair) | 4 refs | unused
+                float w[32] = {};
+                uint32_t e[4], wr[4] = {NO_REF, NO_REF, NO_REF, NO_REF};
+                const int k = wide_entries(nd, e);
+                for (int i = 0; i < k; ++i) {
+                    const rt_aabb& bb = aabbs[e[i]];
+                    const float v6[6] = {bb.min_corner.x, bb.max_corner.x, bb.min_corner.y,
+                                         bb.max_corner.y, bb.min_corner.z, bb.max_corner.z};
+                    std::memcpy(&w[6 * i], v6, sizeof(v6));
+                    wr[i] = ref_of(e[i]);
+                }
+                std::memcpy(&w[24], wr, sizeof(wr));
+                std::memcpy(&hwn[8 * c], w, sizeof(w));
+            }
         } else {
             const uint32_t j = c & ~LEAF_BIT;
             const rt_triangle& t = tris[nd.object_idx];
@@ -1098,6 +1275,14 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     s->nlights = nlights;
     s->root_ref = cid[0];
     if (s->root_ref == NO_REF) s->root_ref = LEAF_BIT | 0u;  // degenerate: unreachable leaf
+    for (size_t n = 0; n < NN; ++n) {
+        const rt_aabb& bb = aabbs[n];
+        s->bmax[0] = std::max({s->bmax[0], std::fabs(bb.min_corner.x), std::fabs(bb.max_corner.x)});
+        s->bmax[1] = std::max({s->bmax[1], std::fabs(bb.min_corner.y), std::fabs(bb.max_corner.y)});
+        s->bmax[2] = std::max({s->bmax[2], std::fabs(bb.min_corner.z), std::fabs(bb.max_corner.z)});
+    }
+    for (float& v : s->bmax)
+        if (!(v <= FLT_MAX)) v = INFINITY;  // NaN or infinite boxes: no finite bound, tests fall back
     s->root_box[0] = aabbs[0].min_corner.x; s->root_box[1] = aabbs[0].min_corner.y; s->root_box[2] = aabbs[0].min_corner.z;
     s->root_box[3] = aabbs[0].max_corner.x; s->root_box[4] = aabbs[0].max_corner.y; s->root_box[5] = aabbs[0].max_corner.z;
     if (cid[0] == NO_REF) {  // root names no triangle: nothing can be hit; empty box
@@ -1105,6 +1290,8 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
         s->root_box[3] = s->root_box[4] = s->root_box[5] = -INFINITY;
     }
     if ((rc = s->inode.upload(hin.data(), hin.size() * sizeof(float4))) != RT_OK) return rc;
+    if (wide_ok && (rc = s->wnode.upload(hwn.data(), hwn.size() * sizeof(float4))) != RT_OK) return rc;
+    s->wide = wide_ok && !(s->root_ref & LEAF_BIT);
     if ((rc = s->ibox.upload(hib.data(), hib.size() * sizeof(float4))) != RT_OK) return rc;
     if ((rc = s->leaf.upload(hlf.data(), hlf.size() * sizeof(float4))) != RT_OK) return rc;
     if ((rc = s->tnorm.upload(hnm.data(), hnm.size() * sizeof(float4))) != RT_OK) return rc;
@@ -1116,7 +1303,7 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
         HIP_TRY(hipEventCreate(&s->evm[i]));
         HIP_TRY(hipEventCreate(&s->ev1[i]));
     }
-    s->bytes = s->inode.n + s->ibox.n + s->leaf.n + s->tnorm.n + s->objids.n + s->mats.n + s->lights.n;
+    s->bytes = s->inode.n + s->wnode.n + s->ibox.n + s->leaf.n + s->tnorm.n + s->objids.n + s->mats.n + s->lights.n;
     *out = s.release();
     return RT_OK;
 }
@@ -1218,6 +1405,8 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     RenderParams P;
     std::memset(&P, 0, sizeof(P));
     P.sc.inode = static_cast<const float4*>(s->inode.p);
+    P.sc.wnode = static_cast<const float4*>(s->wnode.p);
+    P.sc.wide = s->wide && !(o->flags & RT_FLAG_BINARY) ? 1 : 0;
     P.sc.ibox = static_cast<const float4*>(s->ibox.p);
     P.sc.leaf = static_cast<const float4*>(s->leaf.p);
     P.sc.tnorm = static_cast<const float4*>(s->tnorm.p);
@@ -1229,6 +1418,7 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     P.sc.num_lights = s->nlights;
     P.sc.root_ref = s->root_ref;
     std::memcpy(P.sc.root_box, s->root_box, sizeof(P.sc.root_box));
+    std::memcpy(P.sc.bmax, s->bmax, sizeof(P.sc.bmax));
     P.cam_center = f3{cam->center.x, cam->center.y, cam->center.z};
     P.cam_p00 = f3{cam->pixel00_loc.x, cam->pixel00_loc.y, cam->pixel00_loc.z};
     P.cam_du = f3{cam->pixel_delta_u.x, cam->pixel_delta_u.y, cam->pixel_delta_u.z};
@@ -1510,7 +1700,9 @@ extern "C" int rt_box_test_host(const float* rays, const float* boxes, const flo
     for (int i = 0; i < n; ++i) {
         const float* R = rays + 6 * i;
         const float* B = boxes + 6 * i;
-        const RayPre r = make_ray(mk(R[0], R[1], R[2]), mk(R[3], R[4], R[5]));
+        const f3 bm = mk(fmaxf(fabsf(B[0]), fabsf(B[3])), fmaxf(fabsf(B[1]), fabsf(B[4])),
+                         fmaxf(fabsf(B[2]), fabsf(B[5])));
+        const RayPre r = make_ray(mk(R[0], R[1], R[2]), mk(R[3], R[4], R[5]), bm);
         const BoxP b = {(v2f){B[0], B[3]}, (v2f){B[1], B[4]}, (v2f){B[2], B[5]}};
         out_class[i] = box_classify(r, b, tminmax[2 * i], tminmax[2 * i + 1]);
         out_fast[i] = box_hit(r, b, tminmax[2 * i], tminmax[2 * i + 1]) ? 1 : 0;

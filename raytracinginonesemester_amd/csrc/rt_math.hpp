@@ -51,13 +51,15 @@ struct BoxP {
 constexpr float kBoxRel = 4e-6f;
 
 // A ray as the slab test needs it.  `par` bit a: |dir[a]| < 1e-8f, where intersectAABB
-// degenerates to an exact inside test on that axis (bvh.h:90-91).  `invf` is a float
-// reciprocal of the direction (any <= 2 ulp approximation), +inf on parallel axes; it and
-// oiv = o * invf serve the pre-classification below only, never the decision of an
-// ambiguous case.
+// degenerates to an exact inside test on that axis (bvh.h:90-91).  iv is a float reciprocal
+// of the direction (any <= 2 ulp approximation), +inf on parallel axes, split by sign into
+// ivp = max(iv, 0) and ivn = min(iv, 0); c1 = -o*iv - E and c2 = -o*iv + E with a per-ray
+// error bound E (box_classify); hit_lim = 1e38, or -inf when some axis is parallel.  They
+// serve the pre-classification only, never the decision of an ambiguous case.
 struct RayPre {
     f3 o, d;
-    f3 invf, oiv;
+    f3 ivp, ivn, c1, c2;
+    float hit_lim;
     uint32_t par;
 };
 
@@ -69,17 +71,38 @@ __host__ __device__ __forceinline__ float rcp_approx(float x) {
 #endif
 }
 
-__host__ __device__ __forceinline__ RayPre make_ray(f3 o, f3 d) {
+// bmax: per axis, an upper bound of |coordinate| over every box the ray will be tested
+// against (the scene's; make_ray_mt for rays that meet no box).
+__host__ __device__ __forceinline__ RayPre make_ray(f3 o, f3 d, f3 bmax) {
     RayPre r;
     r.o = o;
     r.d = d;
     const float eps = 1e-8f;
     const bool px = fabsf(d.x) < eps, py = fabsf(d.y) < eps, pz = fabsf(d.z) < eps;
     r.par = (px ? 1u : 0u) | (py ? 2u : 0u) | (pz ? 4u : 0u);
-    r.invf = mk(px ? INFINITY : rcp_approx(d.x), py ? INFINITY : rcp_approx(d.y), pz ? INFINITY : rcp_approx(d.z));
-    r.oiv = mk(o.x * r.invf.x, o.y * r.invf.y, o.z * r.invf.z);
+    const float iv[3] = {px ? INFINITY : rcp_approx(d.x), py ? INFINITY : rcp_approx(d.y),
+                         pz ? INFINITY : rcp_approx(d.z)};
+    const float oc[3] = {o.x, o.y, o.z}, bm[3] = {bmax.x, bmax.y, bmax.z};
+    float ivp[3], ivn[3], c1[3], c2[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float oiv = oc[a] * iv[a];
+        const float E = kBoxRel * (2.0f * fabsf(oiv) + bm[a] * fabsf(iv[a])) + 1e-30f;
+        ivp[a] = iv[a] >= 0.0f ? iv[a] : 0.0f;
+        ivn[a] = iv[a] >= 0.0f ? 0.0f : iv[a];
+        c1[a] = -oiv - E;
+        c2[a] = -oiv + E;
+    }
+    r.ivp = mk(ivp[0], ivp[1], ivp[2]);
+    r.ivn = mk(ivn[0], ivn[1], ivn[2]);
+    r.c1 = mk(c1[0], c1[1], c1[2]);
+    r.c2 = mk(c2[0], c2[1], c2[2]);
+    r.hit_lim = r.par ? -INFINITY : 1e38f;
     return r;
 }
+
+// A ray used only for triangle tests (origin and direction).
+__host__ __device__ __forceinline__ RayPre make_ray_mt(f3 o, f3 d) { return make_ray(o, d, mk(0.f, 0.f, 0.f)); }
 
 // intersectAABB(ray, box, tmin, tmax) exactly as the reference evaluates it (bvh.h:81-129):
 // per axis inv = 1.0/double(dir), tNear/tFar = (double(bound) - double(orig)) * inv,
@@ -113,44 +136,68 @@ __host__ __device__ inline bool box_hit_exact(const RayPre& r, const BoxP& b, do
 
 // Conservative float pre-classification of the same test: MISS / HIT are returned only when
 // the reference's double computation is guaranteed to give that answer; AMBIG otherwise.
-// Per axis the slab parameters are estimated as tn' = fma(bound, invf, -oiv) (one packed
-// FMA for both bounds).  Error budget (finite inputs): with invf = (1/d)(1+e1), |e1| <= 2^-23
-// (1-ulp reciprocal), oiv = o*invf*(1+e2) and the FMA's rounding e3 (|e2|,|e3| <= 2^-24),
-// |tn' - t| <= 1.8e-7 |t| + 6e-8 |oiv|, while the reference's double tNear/tFar sit within
-// 3.4e-16 |t| of the exact (bound-orig)/dir.  E = kBoxRel * (max(|tn'|,|tf'|) + |oiv|) +
-// 1e-30 (kBoxRel = 4e-6) bounds the distance between the two with > 10x slack, also covering
-// the float rounding of E and of the +-E adjustments below; the 1e-30 term covers subnormal
-// absolute error.  With Lmax = max over axes of the reference lows and Hmin = min of
-// the highs (tmin/tmax are exact in both precisions):
-//   MISS  if max(tmin, lo'-E) > min(tmax, hi'+E)      (then Lmax > Hmin: reference rejects)
-//   HIT   if max(tmin, lo'+E) <= min(tmax, hi'-E)     (then Lmax <= Hmin: reference accepts)
-// Branch-free over the axes: a parallel axis has invf = +inf and oiv = +-inf or NaN, so its
-// tn'/tf' are +-inf or NaN and its E is +inf or NaN; fmaxf/fminf drop the NaN terms and the
-// +-inf -+ inf terms cannot tighten the bounds, so the axis constrains nothing, and the sum of
-// the E's (non-finite) rules HIT out.  MISS then rests on the other axes alone, which is
-// sound since the reference's t-interval is the intersection over its non-parallel axes (its
-// inside test can only reject more).  The same sum rules HIT out for estimates near FLT_MAX;
-// NaN compares false and falls to AMBIG.
+// Per axis, with the near bound (min if iv >= 0, else max) and the far one, the slab
+// parameters' padded ends are FMAs against the per-ray constants:
+//   lo' -+ E = fma(near, iv, c1 / c2),   hi' -+ E = fma(far, iv, c1 / c2),
+// written sign-free as near*iv + c = fma(min, ivp, fma(max, ivn, c)) (one of ivp/ivn is 0, so
+// the inner FMA returns c exactly) and far*iv + c = fma(max, ivp, fma(min, ivn, c)).
+// Error budget (finite inputs): with iv = (1/d)(1+e1), |e1| <= 2^-23 (1-ulp reciprocal),
+// oiv = o*iv rounded, c1/c2 rounded and the FMA's rounding (each <= 2^-24 relative), the
+// distance between fma(b, iv, -oiv -+ E) and t -+ E, t = (b - o)/d exactly, is at most
+// 1.8e-7 |t| + 2.4e-7 |oiv| + 1.2e-7 E; the reference's double tNear/tFar are within
+// 3.4e-16 |t| of t.  E = kBoxRel (2 |oiv| + bmax |iv|) + 1e-30 >= kBoxRel (|t| + |oiv|)
+// (|t| <= |b| |iv| + |oiv|) with kBoxRel = 4e-6 covers both with > 10x slack; the 1e-30 term
+// covers subnormal absolute error.  So lowLo <= exact lo <= lowHi and highLo <= exact hi <=
+// highHi per axis, and with Lmax / Hmin the reference's max of lows / min of highs (tmin and
+// tmax exact in both precisions):
+//   MISS  if max(tmin, lowLo) > min(tmax, highHi)     (then Lmax > Hmin: reference rejects)
+//   HIT   if max(tmin, lowHi) <= min(tmax, highLo)    (then Lmax <= Hmin: reference accepts)
+// An estimate that overflows to +-inf could break the bracket near FLT_MAX: MISS also needs
+// max(lowLo) < 1e38 and HIT max(lowHi) < hit_lim = 1e38.  A parallel axis has iv = +inf and
+// E = +inf, so c1 is -inf or NaN and c2 +inf or NaN: its lowLo/highLo are -inf or NaN and its
+// lowHi/highHi +inf or NaN, which the max/min drop or which cannot tighten the bounds, so the
+// axis constrains nothing; such a ray has hit_lim = -inf (no HIT).  MISS then rests on the
+// other axes alone, sound since the reference's t-interval is the intersection over its
+// non-parallel axes (its inside test can only reject more).  NaN compares false (AMBIG).
+// tmin/tmax enter through comparisons rather than max/min (cheaper on the VALU).
 enum : int { BOX_MISS = 0, BOX_HIT = 1, BOX_AMBIG = 2 };
+struct BoxBounds {
+    float lowLo, lowHi, highLo, highHi;  // max / min over the axes, without tmin / tmax
+};
+__host__ __device__ __forceinline__ BoxBounds box_bounds(const RayPre& r, const BoxP& b) {
+    // x axis
+    const float lLx = __builtin_fmaf(b.x.x, r.ivp.x, __builtin_fmaf(b.x.y, r.ivn.x, r.c1.x));
+    const float lHx = __builtin_fmaf(b.x.x, r.ivp.x, __builtin_fmaf(b.x.y, r.ivn.x, r.c2.x));
+    const float hLx = __builtin_fmaf(b.x.y, r.ivp.x, __builtin_fmaf(b.x.x, r.ivn.x, r.c1.x));
+    const float hHx = __builtin_fmaf(b.x.y, r.ivp.x, __builtin_fmaf(b.x.x, r.ivn.x, r.c2.x));
+    // y axis
+    const float lLy = __builtin_fmaf(b.y.x, r.ivp.y, __builtin_fmaf(b.y.y, r.ivn.y, r.c1.y));
+    const float lHy = __builtin_fmaf(b.y.x, r.ivp.y, __builtin_fmaf(b.y.y, r.ivn.y, r.c2.y));
+    const float hLy = __builtin_fmaf(b.y.y, r.ivp.y, __builtin_fmaf(b.y.x, r.ivn.y, r.c1.y));
+    const float hHy = __builtin_fmaf(b.y.y, r.ivp.y, __builtin_fmaf(b.y.x, r.ivn.y, r.c2.y));
+    // z axis
+    const float lLz = __builtin_fmaf(b.z.x, r.ivp.z, __builtin_fmaf(b.z.y, r.ivn.z, r.c1.z));
+    const float lHz = __builtin_fmaf(b.z.x, r.ivp.z, __builtin_fmaf(b.z.y, r.ivn.z, r.c2.z));
+    const float hLz = __builtin_fmaf(b.z.y, r.ivp.z, __builtin_fmaf(b.z.x, r.ivn.z, r.c1.z));
+    const float hHz = __builtin_fmaf(b.z.y, r.ivp.z, __builtin_fmaf(b.z.x, r.ivn.z, r.c2.z));
+    BoxBounds k;
+    k.lowLo = fmaxf(fmaxf(lLx, lLy), lLz);
+    k.lowHi = fmaxf(fmaxf(lHx, lHy), lHz);
+    k.highLo = fminf(fminf(hLx, hLy), hLz);
+    k.highHi = fminf(fminf(hHx, hHy), hHz);
+    return k;
+}
+__host__ __device__ __forceinline__ bool box_miss(const RayPre& r, const BoxBounds& k, float tmin, float tmax) {
+    return (k.lowLo > k.highHi || k.lowLo > tmax || tmin > k.highHi) && k.lowLo < 1e38f;
+}
+__host__ __device__ __forceinline__ bool box_sure_hit(const RayPre& r, const BoxBounds& k, float tmin, float tmax) {
+    return k.lowHi <= k.highLo && k.lowHi <= tmax && tmin <= k.highLo && tmin <= tmax && k.lowHi < r.hit_lim;
+}
+
 __host__ __device__ __forceinline__ int box_classify(const RayPre& r, const BoxP& b, float tmin, float tmax) {
-    const v2f bb[3] = {b.x, b.y, b.z};
-    const float iv[3] = {r.invf.x, r.invf.y, r.invf.z}, oiv[3] = {r.oiv.x, r.oiv.y, r.oiv.z};
-    float lowLo = tmin, lowHi = tmin, highLo = tmax, highHi = tmax, esum = 0.f;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const v2f t = __builtin_elementwise_fma(bb[a], (v2f)(iv[a]), (v2f)(-oiv[a]));
-        const float lo = fminf(t.x, t.y), hi = fmaxf(t.x, t.y);
-        const float E = __builtin_fmaf(kBoxRel, fmaxf(fabsf(t.x), fabsf(t.y)) + fabsf(oiv[a]), 1e-30f);
-        esum = a == 0 ? E : esum + E;
-        const v2f lw = (v2f)(lo) + (v2f){-E, E};
-        const v2f hg = (v2f)(hi) + (v2f){-E, E};
-        lowLo = fmaxf(lowLo, lw.x);
-        lowHi = fmaxf(lowHi, lw.y);
-        highLo = fminf(highLo, hg.x);
-        highHi = fminf(highHi, hg.y);
-    }
-    if (lowLo > highHi) return BOX_MISS;
-    if (esum < 3.0e38f && lowHi <= highLo) return BOX_HIT;
+    const BoxBounds k = box_bounds(r, b);
+    if (box_miss(r, k, tmin, tmax)) return BOX_MISS;
+    if (box_sure_hit(r, k, tmin, tmax)) return BOX_HIT;
     return BOX_AMBIG;
 }
 

@@ -27,7 +27,8 @@ ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--kernels", default="wave,lane")
 ap.add_argument("--tiles", default="linear,xcd_chunk,rows")
-ap.add_argument("--cull", default="on", help="on,off")
+ap.add_argument("--flags", default="0", help="RT_FLAG_* values to compare, e.g. 0,2,4 "
+                "(1 no cull, 2 megakernel, 4 binary nodes)")
 ap.add_argument("--tpb", default="2", help="tiles per render block (RT_TILES_PER_BLOCK), e.g. 1,2,4,8")
 a = ap.parse_args()
 
@@ -38,7 +39,7 @@ cam = hs.camera(cfg["width"], cfg["height"])
 ds = rt.DeviceScene.from_host(hs)
 K = {"wave": rt.RT_KERNEL_WAVE, "lane": rt.RT_KERNEL_LANE, "wavepix": rt._lib.RT_KERNEL_WAVE_PIXELS}
 T = {"linear": rt.RT_TILES_LINEAR, "xcd_chunk": rt.RT_TILES_XCD_CHUNK, "rows": rt.RT_TILES_ROWS}
-variants = list(itertools.product(a.kernels.split(","), a.tiles.split(","), a.cull.split(","),
+variants = list(itertools.product(a.kernels.split(","), a.tiles.split(","), a.flags.split(","),
                                   a.tpb.split(",")))
 times = {v: [] for v in variants}
 ref = None
@@ -48,7 +49,7 @@ for r in range(a.rounds):
         for _ in range(a.reps):
             img = ds.render(cam, spp=cfg["spp"], max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
                             kernel=K[v[0]], tile_order=T[v[1]],
-                            flags=0 if v[2] == "on" else rt._lib.RT_FLAG_NO_CULL)
+                            flags=int(v[2]))
         times[v] += list(ds.kernel_times(a.reps))
         if ref is None:
             ref = img
@@ -56,7 +57,7 @@ for r in range(a.rounds):
 samples = cfg["width"] * cfg["height"] * cfg["spp"]
 for v in variants:
     t = np.array(times[v])
-    print(json.dumps({"config": a.config, "kernel": v[0], "tiles": v[1], "cull": v[2], "tpb": v[3],
+    print(json.dumps({"config": a.config, "kernel": v[0], "tiles": v[1], "flags": int(v[2]), "tpb": v[3],
                       "median_ms": round(float(np.median(t)), 4),
                       "min_ms": round(float(t.min()), 4), "Gsamples_s": round(float(samples / np.median(t) / 1e6), 3)}),
           flush=True)

@@ -29,8 +29,10 @@ pytestmark = pytest.mark.gpu
 RGB_TOL = 2e-6
 KERNELS = [rt.RT_KERNEL_WAVE, rt.RT_KERNEL_LANE]
 # (flags, tile order, tiles per render block): launch shapes, all of which must give the same frame
-LAUNCHES = [(0, rt.RT_TILES_AUTO, None), (0, rt.RT_TILES_LINEAR, "1"), (0, rt.RT_TILES_ROWS, "5"),
-            (0, rt.RT_TILES_XCD_CHUNK, "3"), (rt._lib.RT_FLAG_NO_CULL, rt.RT_TILES_XCD_CHUNK, "2")]
+BIN = rt._lib.RT_FLAG_BINARY
+LAUNCHES = [(0, rt.RT_TILES_AUTO, None), (BIN, rt.RT_TILES_AUTO, None), (0, rt.RT_TILES_LINEAR, "1"),
+            (BIN, rt.RT_TILES_ROWS, "5"), (0, rt.RT_TILES_XCD_CHUNK, "3"),
+            (rt._lib.RT_FLAG_NO_CULL, rt.RT_TILES_XCD_CHUNK, "2"), (BIN | rt._lib.RT_FLAG_NO_CULL, rt.RT_TILES_LINEAR, "2")]
 
 
 def _device_scene(scene):
@@ -50,9 +52,10 @@ def _check_fb(rgb, ref, exact_frac=1.0):
     assert (rgb.view(np.uint32) == ref.view(np.uint32)).mean() >= exact_frac
 
 
+@pytest.mark.parametrize("flags", [0, rt._lib.RT_FLAG_BINARY])
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("name", ["c3_small", "frog_bounce", "sphere_single", "cornell", "c5_small"])
-def test_golden_scene_parity(name, kernel):
+def test_golden_scene_parity(name, kernel, flags):
     meta = golden_meta(name)
     scene = G_SCENES[name]
     hs = host_scene(scene)
@@ -60,7 +63,7 @@ def test_golden_scene_parity(name, kernel):
     ds = _device_scene(scene)
     rgb, hi, ht = ds.render(cam, spp=meta["spp"], max_depth=meta["max_depth"],
                             diffuse_bounce=bool(meta["diffuse_bounce"]), miss_color=hexv(meta["miss_color"]),
-                            aov=True, kernel=kernel)
+                            aov=True, kernel=kernel, flags=flags)
     assert np.array_equal(hi.reshape(-1), golden_array(name, "hits.i32.gz", np.int32))
     assert np.array_equal(ht.reshape(-1).view(np.uint32),
                           golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))

@@ -194,18 +194,17 @@ __device__ __forceinline__ BoxP leaf_box(const NodeRec& r) {
                 (v2f){__uint_as_float(r.d.z), __uint_as_float(r.d.w)}};
 }
 
-// box_hit for the lanes in `act` of a wave (all lanes call it): the float pre-classification
-// for everyone, the exact double test only behind a wave-uniform branch taken when some lane
-// is ambiguous.
-__device__ __forceinline__ bool box_hit_wave(const RayPre& r, const BoxP& b, float tmax, bool act) {
-    const int c = box_classify(r, b, kRayTMin, tmax);
-    bool res = act && c == BOX_HIT;
-    const bool amb = act && c == BOX_AMBIG;
-    if (ballot(amb) != 0) {
-        RT_STAT(12, 1);
-        if (amb) res = box_hit_exact(r, b, (double)kRayTMin, (double)tmax);
-    }
-    return res;
+// box_hit for the lanes in `act` (a wave mask; all lanes call it), as the mask of lanes that
+// pass: the float pre-classification for everyone, the exact double test only behind a
+// wave-uniform branch taken when some lane is ambiguous.
+__device__ __forceinline__ uint64_t box_hit_mask(const RayPre& r, const BoxP& b, float tmax, uint64_t act) {
+    const BoxBounds k = box_bounds(r, b);
+    const uint64_t hit = ballot(box_sure_hit(r, k, kRayTMin, tmax)) & act;
+    const uint64_t miss = ballot(box_miss(r, k, kRayTMin, tmax));
+    const uint64_t amb = act & ~(hit | miss);
+    if (amb == 0) return hit;
+    RT_STAT(12, 1);
+    return hit | (ballot(box_hit_exact(r, b, (double)kRayTMin, (double)tmax)) & amb);
 }
 
 // Result of one closest-hit query.
@@ -262,10 +261,9 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
             } else {
                 ob = own_box(sc, ref, false);
             }
-            const bool pass = box_hit_wave(r, ob, hs.bestT, act);
-            mask = ballot(pass);
-            act = pass;
+            mask = box_hit_mask(r, ob, hs.bestT, mask);
             if (mask == 0) continue;
+            act = (mask & lane_bit) != 0;
         }
         if (leaf) {
             RT_STAT(10 + so, 1);
@@ -296,8 +294,7 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
                 if (refs[k] == NO_REF) continue;
                 const float4 p = ldc(W + (3 * k) / 2), q = ldc(W + (3 * k) / 2 + 1);
                 const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
-                const bool pk = box_hit_wave(r, bk, hs.bestT, act);
-                const uint64_t mk_ = ballot(pk);
+                const uint64_t mk_ = box_hit_mask(r, bk, hs.bestT, mask);
                 if (mk_ != 0) {
                     st_ref = wrlane(refs[k], sp, st_ref);
                     st_mlo = wrlane((uint32_t)mk_, sp, st_mlo);
@@ -313,8 +310,7 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
         const uint4 q3 = ldc_u(N + 3);
         const uint32_t lref = q3.x, rref = q3.y;
         if (lref != NO_REF) {
-            const bool pl = box_hit_wave(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, act);
-            const uint64_t ml = ballot(pl);
+            const uint64_t ml = box_hit_mask(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
             if (ml != 0) {
                 st_ref = wrlane(lref, sp, st_ref);
                 st_mlo = wrlane((uint32_t)ml, sp, st_mlo);
@@ -324,8 +320,7 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
             }
         }
         if (rref != NO_REF) {
-            const bool pr = box_hit_wave(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, act);
-            const uint64_t mr = ballot(pr);
+            const uint64_t mr = box_hit_mask(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
             if (mr != 0) {
                 st_ref = wrlane(rref, sp, st_ref);
                 st_mlo = wrlane((uint32_t)mr, sp, st_mlo);
@@ -483,7 +478,9 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid, const 
         float dist = 0.f;
         bool need = false, lit = false;
         f3 contrib = mk(0.f, 0.f, 0.f);
-        RayPre sray = ray;
+        // Lanes without a shadow ray leave sray unset: the traversal masks them out (their
+        // results are never read), and copying the camera ray in would keep it live.
+        RayPre sray;
         if (hit) {
             const f3 L = unit(sub(lpos, sh.p));
             const float NdotL = fmaxf(dot(N, L), 0.0f);
@@ -572,7 +569,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
             float dist = 0.f;
             bool need = false, lit = false;
             f3 contrib = mk(0.f, 0.f, 0.f);
-            RayPre sray = ray;
+            RayPre sray;  // unset for lanes without a shadow ray (masked out by the traversal)
             if (hit) {
                 const f3 L = unit(sub(lpos, sh.p));
                 const float NdotL = fmaxf(dot(N, L), 0.0f);
@@ -1281,8 +1278,17 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
         s->bmax[1] = std::max({s->bmax[1], std::fabs(bb.min_corner.y), std::fabs(bb.max_corner.y)});
         s->bmax[2] = std::max({s->bmax[2], std::fabs(bb.min_corner.z), std::fabs(bb.max_corner.z)});
     }
+    // The pre-classification takes min <= max per axis (near/far bounds by the ray's sign); a
+    // scene with an inverted, NaN or infinite box gets bmax = inf, which turns every float
+    // classification ambiguous (make_ray: E = inf), so all its box tests take the exact path.
+    bool sorted_boxes = true;
+    for (size_t n = 0; n < NN; ++n) {
+        const rt_aabb& bb = aabbs[n];
+        sorted_boxes = sorted_boxes && bb.min_corner.x <= bb.max_corner.x && bb.min_corner.y <= bb.max_corner.y &&
+                       bb.min_corner.z <= bb.max_corner.z;
+    }
     for (float& v : s->bmax)
-        if (!(v <= FLT_MAX)) v = INFINITY;  // NaN or infinite boxes: no finite bound, tests fall back
+        if (!(v <= FLT_MAX) || !sorted_boxes) v = INFINITY;
     s->root_box[0] = aabbs[0].min_corner.x; s->root_box[1] = aabbs[0].min_corner.y; s->root_box[2] = aabbs[0].min_corner.z;
     s->root_box[3] = aabbs[0].max_corner.x; s->root_box[4] = aabbs[0].max_corner.y; s->root_box[5] = aabbs[0].max_corner.z;
     if (cid[0] == NO_REF) {  // root names no triangle: nothing can be hit; empty box
@@ -1700,8 +1706,8 @@ extern "C" int rt_box_test_host(const float* rays, const float* boxes, const flo
     for (int i = 0; i < n; ++i) {
         const float* R = rays + 6 * i;
         const float* B = boxes + 6 * i;
-        const f3 bm = mk(fmaxf(fabsf(B[0]), fabsf(B[3])), fmaxf(fabsf(B[1]), fabsf(B[4])),
-                         fmaxf(fabsf(B[2]), fabsf(B[5])));
+        f3 bm = mk(fmaxf(fabsf(B[0]), fabsf(B[3])), fmaxf(fabsf(B[1]), fabsf(B[4])), fmaxf(fabsf(B[2]), fabsf(B[5])));
+        if (!(B[0] <= B[3] && B[1] <= B[4] && B[2] <= B[5])) bm = mk(INFINITY, INFINITY, INFINITY);  // as rt_scene_create
         const RayPre r = make_ray(mk(R[0], R[1], R[2]), mk(R[3], R[4], R[5]), bm);
         const BoxP b = {(v2f){B[0], B[3]}, (v2f){B[1], B[4]}, (v2f){B[2], B[5]}};
         out_class[i] = box_classify(r, b, tminmax[2 * i], tminmax[2 * i + 1]);

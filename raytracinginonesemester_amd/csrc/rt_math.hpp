@@ -53,12 +53,12 @@ constexpr float kBoxRel = 4e-6f;
 // A ray as the slab test needs it.  `par` bit a: |dir[a]| < 1e-8f, where intersectAABB
 // degenerates to an exact inside test on that axis (bvh.h:90-91).  iv is a float reciprocal
 // of the direction (any <= 2 ulp approximation), +inf on parallel axes, split by sign into
-// ivp = max(iv, 0) and ivn = min(iv, 0); c1 = -o*iv - E and c2 = -o*iv + E with a per-ray
-// error bound E (box_classify); hit_lim = 1e38, or -inf when some axis is parallel.  They
-// serve the pre-classification only, never the decision of an ambiguous case.
+// ivp = max(iv, 0) and ivn = min(iv, 0); c1 = -o*iv - E, c2 = -o*iv + E and e2 = 2E with a
+// per-ray error bound E (box_classify); hit_lim = 1e38, or -inf when some axis is parallel.
+// They serve the pre-classification only, never the decision of an ambiguous case.
 struct RayPre {
     f3 o, d;
-    f3 ivp, ivn, c1, c2;
+    f3 ivp, ivn, c1, c2, e2;
     float hit_lim;
     uint32_t par;
 };
@@ -83,7 +83,8 @@ __host__ __device__ __forceinline__ RayPre make_ray(f3 o, f3 d, f3 bmax) {
     const float iv[3] = {px ? INFINITY : rcp_approx(d.x), py ? INFINITY : rcp_approx(d.y),
                          pz ? INFINITY : rcp_approx(d.z)};
     const float oc[3] = {o.x, o.y, o.z}, bm[3] = {bmax.x, bmax.y, bmax.z};
-    float ivp[3], ivn[3], c1[3], c2[3];
+    float ivp[3], ivn[3], c1[3], c2[3], e2[3];
+    bool finite = true;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float oiv = oc[a] * iv[a];
@@ -92,12 +93,15 @@ __host__ __device__ __forceinline__ RayPre make_ray(f3 o, f3 d, f3 bmax) {
         ivn[a] = iv[a] >= 0.0f ? 0.0f : iv[a];
         c1[a] = -oiv - E;
         c2[a] = -oiv + E;
+        e2[a] = 2.0f * E;
+        finite = finite && e2[a] <= FLT_MAX;
     }
     r.ivp = mk(ivp[0], ivp[1], ivp[2]);
     r.ivn = mk(ivn[0], ivn[1], ivn[2]);
     r.c1 = mk(c1[0], c1[1], c1[2]);
     r.c2 = mk(c2[0], c2[1], c2[2]);
-    r.hit_lim = r.par ? -INFINITY : 1e38f;
+    r.e2 = mk(e2[0], e2[1], e2[2]);
+    r.hit_lim = r.par || !finite ? -INFINITY : 1e38f;
     return r;
 }
 
@@ -138,13 +142,16 @@ __host__ __device__ inline bool box_hit_exact(const RayPre& r, const BoxP& b, do
 // the reference's double computation is guaranteed to give that answer; AMBIG otherwise.
 // Per axis, with the near bound (min if iv >= 0, else max) and the far one, the slab
 // parameters' padded ends are FMAs against the per-ray constants:
-//   lo' -+ E = fma(near, iv, c1 / c2),   hi' -+ E = fma(far, iv, c1 / c2),
+//   lo' - E = fma(near, iv, c1),   hi' + E = fma(far, iv, c2),
 // written sign-free as near*iv + c = fma(min, ivp, fma(max, ivn, c)) (one of ivp/ivn is 0, so
-// the inner FMA returns c exactly) and far*iv + c = fma(max, ivp, fma(min, ivn, c)).
+// the inner FMA returns c exactly) and far*iv + c = fma(max, ivp, fma(min, ivn, c)); then
+// lo' + E = (lo' - E) + 2E and hi' - E = (hi' + E) - 2E, one more rounding each (in the
+// slack below).
 // Error budget (finite inputs): with iv = (1/d)(1+e1), |e1| <= 2^-23 (1-ulp reciprocal),
 // oiv = o*iv rounded, c1/c2 rounded and the FMA's rounding (each <= 2^-24 relative), the
 // distance between fma(b, iv, -oiv -+ E) and t -+ E, t = (b - o)/d exactly, is at most
-// 1.8e-7 |t| + 2.4e-7 |oiv| + 1.2e-7 E; the reference's double tNear/tFar are within
+// 1.8e-7 |t| + 2.4e-7 |oiv| + 1.2e-7 E (+ 6e-8 (|t| + 3E) for the +-2E steps); the reference's
+// double tNear/tFar are within
 // 3.4e-16 |t| of t.  E = kBoxRel (2 |oiv| + bmax |iv|) + 1e-30 >= kBoxRel (|t| + |oiv|)
 // (|t| <= |b| |iv| + |oiv|) with kBoxRel = 4e-6 covers both with > 10x slack; the 1e-30 term
 // covers subnormal absolute error.  So lowLo <= exact lo <= lowHi and highLo <= exact hi <=
@@ -153,7 +160,8 @@ __host__ __device__ inline bool box_hit_exact(const RayPre& r, const BoxP& b, do
 //   MISS  if max(tmin, lowLo) > min(tmax, highHi)     (then Lmax > Hmin: reference rejects)
 //   HIT   if max(tmin, lowHi) <= min(tmax, highLo)    (then Lmax <= Hmin: reference accepts)
 // An estimate that overflows to +-inf could break the bracket near FLT_MAX: MISS also needs
-// max(lowLo) < 1e38 and HIT max(lowHi) < hit_lim = 1e38.  A parallel axis has iv = +inf and
+// max(lowLo) < 1e38 and HIT max(lowHi) < hit_lim = 1e38 (-inf, no HIT, when a 2E overflows:
+// lo' + E = -inf + inf would drop out of the max).  A parallel axis has iv = +inf and
 // E = +inf, so c1 is -inf or NaN and c2 +inf or NaN: its lowLo/highLo are -inf or NaN and its
 // lowHi/highHi +inf or NaN, which the max/min drop or which cannot tighten the bounds, so the
 // axis constrains nothing; such a ray has hit_lim = -inf (no HIT).  MISS then rests on the
@@ -165,25 +173,16 @@ struct BoxBounds {
     float lowLo, lowHi, highLo, highHi;  // max / min over the axes, without tmin / tmax
 };
 __host__ __device__ __forceinline__ BoxBounds box_bounds(const RayPre& r, const BoxP& b) {
-    // x axis
     const float lLx = __builtin_fmaf(b.x.x, r.ivp.x, __builtin_fmaf(b.x.y, r.ivn.x, r.c1.x));
-    const float lHx = __builtin_fmaf(b.x.x, r.ivp.x, __builtin_fmaf(b.x.y, r.ivn.x, r.c2.x));
-    const float hLx = __builtin_fmaf(b.x.y, r.ivp.x, __builtin_fmaf(b.x.x, r.ivn.x, r.c1.x));
     const float hHx = __builtin_fmaf(b.x.y, r.ivp.x, __builtin_fmaf(b.x.x, r.ivn.x, r.c2.x));
-    // y axis
     const float lLy = __builtin_fmaf(b.y.x, r.ivp.y, __builtin_fmaf(b.y.y, r.ivn.y, r.c1.y));
-    const float lHy = __builtin_fmaf(b.y.x, r.ivp.y, __builtin_fmaf(b.y.y, r.ivn.y, r.c2.y));
-    const float hLy = __builtin_fmaf(b.y.y, r.ivp.y, __builtin_fmaf(b.y.x, r.ivn.y, r.c1.y));
     const float hHy = __builtin_fmaf(b.y.y, r.ivp.y, __builtin_fmaf(b.y.x, r.ivn.y, r.c2.y));
-    // z axis
     const float lLz = __builtin_fmaf(b.z.x, r.ivp.z, __builtin_fmaf(b.z.y, r.ivn.z, r.c1.z));
-    const float lHz = __builtin_fmaf(b.z.x, r.ivp.z, __builtin_fmaf(b.z.y, r.ivn.z, r.c2.z));
-    const float hLz = __builtin_fmaf(b.z.y, r.ivp.z, __builtin_fmaf(b.z.x, r.ivn.z, r.c1.z));
     const float hHz = __builtin_fmaf(b.z.y, r.ivp.z, __builtin_fmaf(b.z.x, r.ivn.z, r.c2.z));
     BoxBounds k;
     k.lowLo = fmaxf(fmaxf(lLx, lLy), lLz);
-    k.lowHi = fmaxf(fmaxf(lHx, lHy), lHz);
-    k.highLo = fminf(fminf(hLx, hLy), hLz);
+    k.lowHi = fmaxf(fmaxf(lLx + r.e2.x, lLy + r.e2.y), lLz + r.e2.z);
+    k.highLo = fminf(fminf(hHx - r.e2.x, hHy - r.e2.y), hHz - r.e2.z);
     k.highHi = fminf(fminf(hHx, hHy), hHz);
     return k;
 }

@@ -88,3 +88,22 @@ def test_extreme_magnitudes():
         tmm = np.stack([np.full(n, 1e-4), np.full(n, 3.4028235e38)], axis=1)
         fast, exact, _ = _run(np.concatenate([o, d], axis=1), boxes, tmm)
         assert np.array_equal(fast, exact)
+
+
+def test_near_parallel_and_overflow_scales():
+    """Directions with one tiny (but not parallel) component, and coordinates up to the top of
+    the float range, where the float estimates overflow: the classification must stay sound."""
+    rng = np.random.default_rng(4)
+    n = 60000
+    for scale in (1.0, 1e30, 1e37, 1.5e38):
+        boxes = _boxes(rng, n, scale)
+        o = (rng.normal(size=(n, 3)) * scale * 1.5).astype(np.float32)
+        d = rng.normal(size=(n, 3)).astype(np.float32)
+        ax = rng.integers(0, 3, size=n)
+        d[np.arange(n), ax] = rng.choice([1.01e-8, -1.01e-8, 1e-7, 3e-6, -1e-5], size=n)
+        with np.errstate(over="ignore", invalid="ignore"):
+            boxes = np.where(np.isfinite(boxes), boxes, 0).astype(np.float32)
+            o = np.where(np.isfinite(o), o, 0).astype(np.float32)
+        tmm = np.stack([np.full(n, 1e-4), rng.choice([3.4028235e38, 1.0, 1e30], size=n)], axis=1)
+        fast, exact, _ = _run(np.concatenate([o, d], axis=1), boxes, tmm)
+        assert np.array_equal(fast, exact), scale

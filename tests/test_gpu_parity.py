@@ -168,6 +168,26 @@ def test_single_triangle_scene(tmp_path):
     _check_fb(rgb, ref)
 
 
+@pytest.mark.parametrize("flags", [0, rt._lib.RT_FLAG_BINARY])
+def test_inverted_boxes_follow_the_reference(flags):
+    """AABBs with min > max on an axis (malformed input the reference still traverses, its
+    slab test swapping the two parameters): the float pre-classification is switched off for
+    such a scene and every box test takes the exact path, so hits match the oracle."""
+    hs = host_scene("frog.json")
+    aabbs = hs.aabbs.copy()
+    rng = np.random.default_rng(5)
+    pick = rng.choice(np.arange(1, len(aabbs)), size=len(aabbs) // 50, replace=False)
+    aabbs[pick, 0], aabbs[pick, 3] = aabbs[pick, 3].copy(), aabbs[pick, 0].copy()  # swap x min/max
+    ds = rt.DeviceScene(hs.num_triangles, hs.nodes, aabbs, hs.triangles, hs.tri_object_ids, hs.materials, hs.lights)
+    cam = hs.camera(160, 90)
+    rgb, hi, ht = ds.render(cam, spp=4, max_depth=1, aov=True, flags=flags)
+    ref, rhi, rht = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, aabbs, hs.triangles,
+                                 hs.tri_object_ids, hs.materials, hs.lights, spp=4, max_depth=1, aov=True)
+    assert np.array_equal(hi, rhi) and (hi >= 0).any()
+    assert np.array_equal(ht.view(np.uint32), rht.view(np.uint32))
+    _check_fb(rgb, ref)
+
+
 def test_malformed_bvh_is_rejected():
     hs = host_scene("frog.json")
     nodes = hs.nodes.copy()

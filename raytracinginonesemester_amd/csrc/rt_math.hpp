@@ -54,12 +54,14 @@ constexpr float kBoxRel = 4e-6f;
 // degenerates to an exact inside test on that axis (bvh.h:90-91).  iv is a float reciprocal
 // of the direction (any <= 2 ulp approximation), +inf on parallel axes, split by sign into
 // ivp = max(iv, 0) and ivn = min(iv, 0); c1 = -o*iv - E, c2 = -o*iv + E and e2 = 2E with a
-// per-ray error bound E (box_classify); hit_lim = 1e38, or -inf when some axis is parallel.
-// They serve the pre-classification only, never the decision of an ambiguous case.
+// per-ray error bound E (box_classify).  A ray with a parallel axis, or whose slab parameters
+// could come near the float range ((bmax + |o|) |iv| >= 1e37 on some axis, or not finite),
+// gets c1 = c2 = NaN and hit_lim = -inf: every test of it is ambiguous (exact path).  They
+// serve the pre-classification only, never the decision of an ambiguous case.
 struct RayPre {
     f3 o, d;
     f3 ivp, ivn, c1, c2, e2;
-    float hit_lim;
+    float hit_lim;  // +inf, or -inf for a ray the pre-classification does not handle
     uint32_t par;
 };
 
@@ -84,24 +86,26 @@ __host__ __device__ __forceinline__ RayPre make_ray(f3 o, f3 d, f3 bmax) {
                          pz ? INFINITY : rcp_approx(d.z)};
     const float oc[3] = {o.x, o.y, o.z}, bm[3] = {bmax.x, bmax.y, bmax.z};
     float ivp[3], ivn[3], c1[3], c2[3], e2[3];
-    bool finite = true;
+    bool safe = !(px || py || pz);
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float oiv = oc[a] * iv[a];
+        const float S = fabsf(oiv) + bm[a] * fabsf(iv[a]);  // >= |slab parameter| of any box
+        safe = safe && S < 1e37f;
         const float E = kBoxRel * (2.0f * fabsf(oiv) + bm[a] * fabsf(iv[a])) + 1e-30f;
         ivp[a] = iv[a] >= 0.0f ? iv[a] : 0.0f;
         ivn[a] = iv[a] >= 0.0f ? 0.0f : iv[a];
         c1[a] = -oiv - E;
         c2[a] = -oiv + E;
         e2[a] = 2.0f * E;
-        finite = finite && e2[a] <= FLT_MAX;
     }
+    if (!safe) c1[0] = c1[1] = c1[2] = c2[0] = c2[1] = c2[2] = NAN;
     r.ivp = mk(ivp[0], ivp[1], ivp[2]);
     r.ivn = mk(ivn[0], ivn[1], ivn[2]);
     r.c1 = mk(c1[0], c1[1], c1[2]);
     r.c2 = mk(c2[0], c2[1], c2[2]);
     r.e2 = mk(e2[0], e2[1], e2[2]);
-    r.hit_lim = r.par || !finite ? -INFINITY : 1e38f;
+    r.hit_lim = safe ? INFINITY : -INFINITY;
     return r;
 }
 
@@ -159,15 +163,12 @@ __host__ __device__ inline bool box_hit_exact(const RayPre& r, const BoxP& b, do
 // tmax exact in both precisions):
 //   MISS  if max(tmin, lowLo) > min(tmax, highHi)     (then Lmax > Hmin: reference rejects)
 //   HIT   if max(tmin, lowHi) <= min(tmax, highLo)    (then Lmax <= Hmin: reference accepts)
-// An estimate that overflows to +-inf could break the bracket near FLT_MAX: MISS also needs
-// max(lowLo) < 1e38 and HIT max(lowHi) < hit_lim = 1e38 (-inf, no HIT, when a 2E overflows:
-// lo' + E = -inf + inf would drop out of the max).  A parallel axis has iv = +inf and
-// E = +inf, so c1 is -inf or NaN and c2 +inf or NaN: its lowLo/highLo are -inf or NaN and its
-// lowHi/highHi +inf or NaN, which the max/min drop or which cannot tighten the bounds, so the
-// axis constrains nothing; such a ray has hit_lim = -inf (no HIT).  MISS then rests on the
-// other axes alone, sound since the reference's t-interval is the intersection over its
-// non-parallel axes (its inside test can only reject more).  NaN compares false (AMBIG).
-// tmin/tmax enter through comparisons rather than max/min (cheaper on the VALU).
+// For a safe ray (make_ray) every estimate is finite and below 1e37 in magnitude, far from
+// overflow.  An unsafe ray's estimates are NaN, which the max/min drop: MISS reads
+// tmin > tmax (true only when the reference rejects anyway), and HIT is ruled out by folding
+// hit_lim = -inf into its min.  The
+// reference's parallel-axis inside test is only taken by unsafe rays, so it never needs a
+// float counterpart.
 enum : int { BOX_MISS = 0, BOX_HIT = 1, BOX_AMBIG = 2 };
 struct BoxBounds {
     float lowLo, lowHi, highLo, highHi;  // max / min over the axes, without tmin / tmax
@@ -187,10 +188,10 @@ __host__ __device__ __forceinline__ BoxBounds box_bounds(const RayPre& r, const 
     return k;
 }
 __host__ __device__ __forceinline__ bool box_miss(const RayPre& r, const BoxBounds& k, float tmin, float tmax) {
-    return (k.lowLo > k.highHi || k.lowLo > tmax || tmin > k.highHi) && k.lowLo < 1e38f;
+    return fmaxf(k.lowLo, tmin) > fminf(k.highHi, tmax);
 }
 __host__ __device__ __forceinline__ bool box_sure_hit(const RayPre& r, const BoxBounds& k, float tmin, float tmax) {
-    return k.lowHi <= k.highLo && k.lowHi <= tmax && tmin <= k.highLo && tmin <= tmax && k.lowHi < r.hit_lim;
+    return fmaxf(k.lowHi, tmin) <= fminf(fminf(k.highLo, tmax), r.hit_lim);
 }
 
 __host__ __device__ __forceinline__ int box_classify(const RayPre& r, const BoxP& b, float tmin, float tmax) {

@@ -198,10 +198,14 @@ __device__ __forceinline__ BoxP leaf_box(const NodeRec& r) {
 // pass: the float pre-classification for everyone, the exact double test only behind a
 // wave-uniform branch taken when some lane is ambiguous.
 __device__ __forceinline__ uint64_t box_hit_mask(const RayPre& r, const BoxP& b, float tmax, uint64_t act) {
-    const BoxBounds k = box_bounds(r, b);
-    const uint64_t hit = ballot(box_sure_hit(r, k, kRayTMin, tmax)) & act;
-    const uint64_t miss = ballot(box_miss(r, k, kRayTMin, tmax));
-    const uint64_t amb = act & ~(hit | miss);
+    const AxisEnds e = box_ends(r, b);
+    const BoxEnds c = box_lc_hc(e, kRayTMin, tmax);
+    uint64_t hit = ballot(box_sure_hit1(r, c)) & act;
+    uint64_t amb = act & ~(hit | ballot(box_miss(c)));
+    if (amb == 0) return hit;
+    const uint64_t h2 = ballot(box_sure_hit2(r, e, kRayTMin, tmax)) & amb;
+    hit |= h2;
+    amb &= ~h2;
     if (amb == 0) return hit;
     RT_STAT(12, 1);
     return hit | (ballot(box_hit_exact(r, b, (double)kRayTMin, (double)tmax)) & amb);

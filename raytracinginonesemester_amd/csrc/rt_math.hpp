@@ -61,6 +61,7 @@ constexpr float kBoxRel = 4e-6f;
 struct RayPre {
     f3 o, d;
     f3 ivp, ivn, c1, c2, e2;
+    float m2;       // 2 max(e2): the one-margin HIT test's (box_sure_hit1); +inf if unsafe
     float hit_lim;  // +inf, or -inf for a ray the pre-classification does not handle
     uint32_t par;
 };
@@ -105,6 +106,7 @@ __host__ __device__ __forceinline__ RayPre make_ray(f3 o, f3 d, f3 bmax) {
     r.c1 = mk(c1[0], c1[1], c1[2]);
     r.c2 = mk(c2[0], c2[1], c2[2]);
     r.e2 = mk(e2[0], e2[1], e2[2]);
+    r.m2 = safe ? 2.0f * fmaxf(fmaxf(e2[0], e2[1]), e2[2]) : INFINITY;
     r.hit_lim = safe ? INFINITY : -INFINITY;
     return r;
 }
@@ -170,34 +172,44 @@ __host__ __device__ inline bool box_hit_exact(const RayPre& r, const BoxP& b, do
 // reference's parallel-axis inside test is only taken by unsafe rays, so it never needs a
 // float counterpart.
 enum : int { BOX_MISS = 0, BOX_HIT = 1, BOX_AMBIG = 2 };
-struct BoxBounds {
-    float lowLo, lowHi, highLo, highHi;  // max / min over the axes, without tmin / tmax
+// The per-axis padded ends lo' - E (lL) and hi' + E (hH).
+struct AxisEnds {
+    float lLx, lLy, lLz, hHx, hHy, hHz;
 };
-__host__ __device__ __forceinline__ BoxBounds box_bounds(const RayPre& r, const BoxP& b) {
-    const float lLx = __builtin_fmaf(b.x.x, r.ivp.x, __builtin_fmaf(b.x.y, r.ivn.x, r.c1.x));
-    const float hHx = __builtin_fmaf(b.x.y, r.ivp.x, __builtin_fmaf(b.x.x, r.ivn.x, r.c2.x));
-    const float lLy = __builtin_fmaf(b.y.x, r.ivp.y, __builtin_fmaf(b.y.y, r.ivn.y, r.c1.y));
-    const float hHy = __builtin_fmaf(b.y.y, r.ivp.y, __builtin_fmaf(b.y.x, r.ivn.y, r.c2.y));
-    const float lLz = __builtin_fmaf(b.z.x, r.ivp.z, __builtin_fmaf(b.z.y, r.ivn.z, r.c1.z));
-    const float hHz = __builtin_fmaf(b.z.y, r.ivp.z, __builtin_fmaf(b.z.x, r.ivn.z, r.c2.z));
-    BoxBounds k;
-    k.lowLo = fmaxf(fmaxf(lLx, lLy), lLz);
-    k.lowHi = fmaxf(fmaxf(lLx + r.e2.x, lLy + r.e2.y), lLz + r.e2.z);
-    k.highLo = fminf(fminf(hHx - r.e2.x, hHy - r.e2.y), hHz - r.e2.z);
-    k.highHi = fminf(fminf(hHx, hHy), hHz);
-    return k;
+__host__ __device__ __forceinline__ AxisEnds box_ends(const RayPre& r, const BoxP& b) {
+    AxisEnds e;
+    e.lLx = __builtin_fmaf(b.x.x, r.ivp.x, __builtin_fmaf(b.x.y, r.ivn.x, r.c1.x));
+    e.hHx = __builtin_fmaf(b.x.y, r.ivp.x, __builtin_fmaf(b.x.x, r.ivn.x, r.c2.x));
+    e.lLy = __builtin_fmaf(b.y.x, r.ivp.y, __builtin_fmaf(b.y.y, r.ivn.y, r.c1.y));
+    e.hHy = __builtin_fmaf(b.y.y, r.ivp.y, __builtin_fmaf(b.y.x, r.ivn.y, r.c2.y));
+    e.lLz = __builtin_fmaf(b.z.x, r.ivp.z, __builtin_fmaf(b.z.y, r.ivn.z, r.c1.z));
+    e.hHz = __builtin_fmaf(b.z.y, r.ivp.z, __builtin_fmaf(b.z.x, r.ivn.z, r.c2.z));
+    return e;
 }
-__host__ __device__ __forceinline__ bool box_miss(const RayPre& r, const BoxBounds& k, float tmin, float tmax) {
-    return fmaxf(k.lowLo, tmin) > fminf(k.highHi, tmax);
+// Lc = max(tmin, lowLo) and Hc = min(tmax, highHi): MISS iff Lc > Hc.
+struct BoxEnds {
+    float Lc, Hc;
+};
+__host__ __device__ __forceinline__ BoxEnds box_lc_hc(const AxisEnds& e, float tmin, float tmax) {
+    return BoxEnds{fmaxf(fmaxf(fmaxf(e.lLx, e.lLy), e.lLz), tmin), fminf(fminf(fminf(e.hHx, e.hHy), e.hHz), tmax)};
 }
-__host__ __device__ __forceinline__ bool box_sure_hit(const RayPre& r, const BoxBounds& k, float tmin, float tmax) {
-    return fmaxf(k.lowHi, tmin) <= fminf(fminf(k.highLo, tmax), r.hit_lim);
+__host__ __device__ __forceinline__ bool box_miss(const BoxEnds& c) { return c.Lc > c.Hc; }
+// HIT with one margin for all axes: lowHi <= lowLo + max(e2) and highLo >= highHi - max(e2), so
+// Lc + 2 max(e2) <= Hc implies the per-axis HIT test (the rounding of the add is far inside
+// the slack of E).  Cheap; ambiguous cases go on to box_sure_hit2.
+__host__ __device__ __forceinline__ bool box_sure_hit1(const RayPre& r, const BoxEnds& c) { return c.Lc + r.m2 <= c.Hc; }
+// HIT with the per-axis margins.
+__host__ __device__ __forceinline__ bool box_sure_hit2(const RayPre& r, const AxisEnds& e, float tmin, float tmax) {
+    const float lowHi = fmaxf(fmaxf(e.lLx + r.e2.x, e.lLy + r.e2.y), e.lLz + r.e2.z);
+    const float highLo = fminf(fminf(e.hHx - r.e2.x, e.hHy - r.e2.y), e.hHz - r.e2.z);
+    return fmaxf(lowHi, tmin) <= fminf(fminf(highLo, tmax), r.hit_lim);
 }
 
 __host__ __device__ __forceinline__ int box_classify(const RayPre& r, const BoxP& b, float tmin, float tmax) {
-    const BoxBounds k = box_bounds(r, b);
-    if (box_miss(r, k, tmin, tmax)) return BOX_MISS;
-    if (box_sure_hit(r, k, tmin, tmax)) return BOX_HIT;
+    const AxisEnds e = box_ends(r, b);
+    const BoxEnds c = box_lc_hc(e, tmin, tmax);
+    if (box_miss(c)) return BOX_MISS;
+    if (box_sure_hit1(r, c) || box_sure_hit2(r, e, tmin, tmax)) return BOX_HIT;
     return BOX_AMBIG;
 }
 

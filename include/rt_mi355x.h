@@ -141,6 +141,23 @@ int rt_ppm_encode(const float* rgb, int width, int height, const rt_ppm_options*
 /* read_p6 (ppm_p6.cpp:303-372): rgb_out may be NULL to query W/H first. */
 int rt_ppm_read(const char* path, float* rgb_out, size_t cap_floats, int* width, int* height, int* maxval);
 
+/* ---- frame epilogue on the device --------------------------------- */
+/* write_p6's header ("P6\n<W> <H>\n<maxval>\n", ppm_p6.cpp:275-277); buf may be NULL to
+ * query the size. */
+int rt_ppm_header(int width, int height, int maxval, char* buf, size_t cap, size_t* written);
+/* write_p6's sample loop (ppm_p6.cpp:284-299 with float_to_sample :137-155) on the device:
+ * rgb_dev = rows*W*3 floats (device), out_dev = rows*W*3*(maxval<256 ? 1 : 2) bytes (device),
+ * the P6 body without its header; flip_y reverses the given rows.  Asynchronous on
+ * hip_stream.  Byte-identical to rt_ppm_encode's body. */
+int rt_ppm_quantize_device(const float* rgb_dev, int width, int rows, const rt_ppm_options* opt,
+                           uint8_t* out_dev, void* hip_stream);
+/* Band un-permute after a gather: strips_dev holds band_count strips back to back, strip r =
+ * strip_rows rows of row_bytes bytes in the layout rt_render_device writes for
+ * (band_rows, r, band_count) — float rows (W*12 B) or quantised P6 rows.  Writes the
+ * height-row frame in image order (flip_y: bottom row first) to frame_dev.  Asynchronous. */
+int rt_unpermute_strips_device(const void* strips_dev, int strip_rows, size_t row_bytes, int height,
+                               int band_rows, int band_count, int flip_y, void* frame_dev, void* hip_stream);
+
 /* ---- the hot path: device-resident scene + HIP render ---------------------------------- */
 typedef struct rt_scene rt_scene;
 

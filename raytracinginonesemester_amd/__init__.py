@@ -7,5 +7,6 @@ from ._lib import (RTError, RT_KERNEL_AUTO, RT_KERNEL_LANE, RT_KERNEL_WAVE, RT_T
                    RT_TILES_LINEAR, RT_TILES_ROWS, RT_TILES_XCD_CHUNK)
 from .api import (  # noqa: F401
     LIGHT_DTYPE, Camera, DeviceScene, HostScene, MeshHW1, build_bvh, default_material, device_count,
-    encode_p6, intersect_rays, jittered_samples, read_p6, render, render_hw1, write_p6,
+    encode_p6, encode_p6_device, intersect_rays, jittered_samples, p6_header, quantize_p6_device, read_p6,
+    render, render_hw1, unpermute_strips_device, write_p6,
 )

@@ -119,6 +119,9 @@ SIGNATURES = {
     "rt_ppm_write": (I, [C.c_char_p, P, I, I, P]),
     "rt_ppm_encode": (I, [P, I, I, P, P, SZ, P]),
     "rt_ppm_read": (I, [C.c_char_p, P, SZ, P, P, P]),
+    "rt_ppm_header": (I, [I, I, I, P, SZ, P]),
+    "rt_ppm_quantize_device": (I, [P, I, I, P, P, P]),
+    "rt_unpermute_strips_device": (I, [P, I, SZ, I, I, I, I, P, P]),
     "rt_scene_create": (I, [I, SZ, P, P, P, P, P, I, P, I, P]),
     "rt_scene_destroy": (None, [P]),
     "rt_scene_device": (I, [P]),

@@ -377,6 +377,47 @@ def read_p6(path) -> np.ndarray:
     return out
 
 
+def p6_header(width: int, height: int, maxval: int = 255) -> bytes:
+    """write_p6's header bytes (ppm_p6.cpp:275-277)."""
+    n = C.c_size_t()
+    check(lib().rt_ppm_header(width, height, maxval, None, 0, C.byref(n)))
+    buf = C.create_string_buffer(n.value)
+    check(lib().rt_ppm_header(width, height, maxval, buf, n.value, C.byref(n)))
+    return buf.raw[:n.value]
+
+
+def quantize_p6_device(rgb_dev, width: int, rows: int, out_dev, maxval=255, clamp=True, gamma2=True,
+                       flip_y=False, stream=None) -> None:
+    """P6 body of a device framebuffer on the device (rt_ppm_quantize_device).  rgb_dev / out_dev
+    are device addresses (ints, e.g. tensor.data_ptr()); asynchronous on `stream`."""
+    o = _ppm_opts(maxval, clamp, gamma2, flip_y)
+    check(lib().rt_ppm_quantize_device(rgb_dev, width, rows, C.byref(o), out_dev, stream))
+
+
+def unpermute_strips_device(strips_dev, strip_rows: int, row_bytes: int, height: int, band_rows: int,
+                            band_count: int, frame_dev, flip_y=False, stream=None) -> None:
+    """Band un-permute of back-to-back gathered strips into an image-order frame on the device."""
+    check(lib().rt_unpermute_strips_device(strips_dev, strip_rows, row_bytes, height, band_rows, band_count,
+                                           1 if flip_y else 0, frame_dev, stream))
+
+
+def encode_p6_device(rgb, maxval=255, clamp=True, gamma2=True, flip_y=False):
+    """P6 file bytes of an (H, W, 3) float32 CUDA tensor, quantised on the device (only the
+    quantised body crosses PCIe).  Same bytes as encode_p6 on the host copy."""
+    import torch
+
+    if not (isinstance(rgb, torch.Tensor) and rgb.is_cuda and rgb.dtype == torch.float32 and rgb.dim() == 3
+            and rgb.shape[2] == 3):
+        raise ValueError("encode_p6_device: expects an (H, W, 3) float32 device tensor")
+    rgb = rgb.contiguous()
+    H, W = rgb.shape[0], rgb.shape[1]
+    bps = 1 if maxval < 256 else 2
+    body = torch.empty(H * W * 3 * bps, dtype=torch.uint8, device=rgb.device)
+    stream = torch.cuda.current_stream(rgb.device).cuda_stream
+    quantize_p6_device(rgb.data_ptr(), W, H, body.data_ptr(), maxval, clamp, gamma2, flip_y, stream)
+    return p6_header(W, H, maxval) + body.cpu().numpy().tobytes()
+
+
 def device_count() -> int:
     n = C.c_int()
     rc = lib().rt_device_count(C.byref(n))

@@ -54,6 +54,45 @@ def gather_frame(strip, height: int, band_rows: int, world: int, rank: int, gath
     return frame
 
 
+def gather_p6(strip, height: int, band_rows: int, world: int, rank: int, maxval: int = 255, clamp: bool = True,
+              gamma2: bool = True, flip_y: bool = False, stream=None):
+    """The frame epilogue on the devices: every rank quantises its float
+    strip to P6 samples on its GPU (3 B instead of 12 B per pixel at maxval < 256), one gather of
+    the byte strips to rank 0, and rank 0 un-permutes the bands (flipping if asked) on its GPU.
+    Returns the P6 file bytes on rank 0, None elsewhere; identical to
+    ``encode_p6(gather_frame(...))`` (write_p6, HW1/ppm_p6_lib/src/ppm_p6.cpp:257-301)."""
+    import torch
+    import torch.distributed as dist
+
+    from . import api
+
+    if not (strip.is_cuda and strip.dtype == torch.float32 and strip.dim() == 3 and strip.shape[2] == 3):
+        raise ValueError("gather_p6: expects a (rows, W, 3) float32 device strip")
+    strip = strip.contiguous()
+    rows, W = strip.shape[0], strip.shape[1]
+    bps = 1 if maxval < 256 else 2
+    rb = W * 3 * bps
+    if stream is None:
+        stream = torch.cuda.current_stream(strip.device).cuda_stream
+    q = torch.empty((rows, rb), dtype=torch.uint8, device=strip.device)
+    api.quantize_p6_device(strip.data_ptr(), W, rows, q.data_ptr(), maxval, clamp, gamma2, False, stream)
+    if world > 1:
+        on_host = dist.get_backend() == "gloo"
+        src = q.cpu() if on_host else q
+        buf = torch.empty((world, rows, rb), dtype=torch.uint8, device="cpu" if on_host else strip.device) \
+            if rank == 0 else None
+        dist.gather(src, gather_list=list(buf.unbind(0)) if rank == 0 else None, dst=0)
+        if rank != 0:
+            return None
+        strips = buf.to(strip.device)
+    else:
+        strips = q
+    frame = torch.empty((height, rb), dtype=torch.uint8, device=strip.device)
+    api.unpermute_strips_device(strips.data_ptr(), rows, rb, height, band_rows, max(world, 1), frame.data_ptr(),
+                                flip_y, stream)
+    return api.p6_header(W, height, maxval) + frame.cpu().numpy().tobytes()
+
+
 def unpermute(strips: List[np.ndarray], height: int, band_rows: int) -> np.ndarray:
     """Host-side inverse of the band assignment for already-gathered strips."""
     world = len(strips)

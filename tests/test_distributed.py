@@ -75,3 +75,50 @@ def test_band_assignment_partitions_rows():
         assert seen == list(range(1080))
         idx = rdist.strip_index(1080, 8, world)
         assert idx[:, 0].max() == world - 1
+
+
+def _gpu_p6_worker(rank, world, port, q):
+    """One rank of a gloo group sharing cuda:0: render this rank's bands with the HIP kernel in
+    strip layout, then the device frame epilogue (quantise, gather bytes, un-permute)."""
+    import torch
+    import torch.distributed as dist
+
+    import raytracinginonesemester_amd as rt
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hs = host_scene("frog.json")
+        cam = hs.camera(W, H)
+        ds = rt.DeviceScene.from_host(hs, device=0)
+        opts, _jit = ds.make_opts(spp=SPP, max_depth=1, band_rows=BAND, band_index=rank, band_count=world)
+        strip = torch.zeros((rdist.max_strip_rows(H, BAND, world), W, 3), dtype=torch.float32, device="cuda:0")
+        stream = torch.cuda.current_stream().cuda_stream
+        ds.render_device(cam, opts, strip.data_ptr(), stream=stream)
+        p6 = rdist.gather_p6(strip, H, BAND, world, rank, stream=stream)
+        flipped = rdist.gather_p6(strip, H, BAND, world, rank, flip_y=True, stream=stream)
+        if rank == 0:
+            q.put((p6, flipped))
+        ds.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_p6_epilogue_on_one_gpu(world):
+    import raytracinginonesemester_amd as rt
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_p6_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    p6, flipped = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full = _render_rows(0, H)
+    assert p6 == rt.encode_p6(full)
+    assert flipped == rt.encode_p6(full, flip_y=True)

@@ -176,3 +176,22 @@ def test_render_entry_points_fail_loudly_without_device():
     hs = host_scene("frog.json")
     with pytest.raises(rt.RTError, match="NODEVICE"):
         rt.DeviceScene.from_host(hs)
+
+
+def test_p6_header_matches_writer_and_device_epilogue_checks_arguments():
+    """rt_ppm_header is write_p6's header; the device epilogue's argument checks run on the host
+    (no device touched) and return RT_ERR_ARG like write_p6's checks (ppm_p6.cpp:258-266)."""
+    rgb = np.zeros((3, 5, 3), np.float32)
+    assert rt.encode_p6(rgb)[:len(rt.p6_header(5, 3))] == rt.p6_header(5, 3) == b"P6\n5 3\n255\n"
+    assert rt.p6_header(1920, 1080, 65535) == b"P6\n1920 1080\n65535\n"
+    for bad in [(0, 3, 255), (5, -1, 255), (5, 3, 0), (5, 3, 65536)]:
+        with pytest.raises(rt.RTError):
+            rt.p6_header(*bad)
+    with pytest.raises(rt.RTError):
+        rt.quantize_p6_device(0, 5, 3, 0)
+    with pytest.raises(rt.RTError):
+        rt.quantize_p6_device(16, 5, 3, 16, maxval=70000)
+    with pytest.raises(rt.RTError):
+        rt.unpermute_strips_device(16, 2, 60, 16, 8, 4, 0)
+    with pytest.raises(rt.RTError):  # 16 rows over 4 ranks of 4-row bands need 4 rows per strip
+        rt.unpermute_strips_device(16, 3, 60, 16, 4, 4, 32)

@@ -119,6 +119,14 @@ void rt_host_scene_free(rt_host_scene* s);
  * nodes/aabbs must hold 2P-1 entries. */
 int rt_build_bvh(const rt_vec3* positions, size_t num_vertices, const uint32_t* indices,
                  size_t num_triangles, rt_bvh_node* nodes, rt_aabb* aabbs);
+/* The same build on the GPU (the reference's CUDA build bvh.cu:34-206 and
+ * its CPU build bvh.cu:209-317): positions_dev (num_vertices Vec3), indices_dev (3*P u32),
+ * nodes_dev / aabbs_dev (2P-1 each) are device pointers on `device`.  The arrays are
+ * byte-identical to rt_build_bvh's.  Runs on hip_stream and synchronises it before returning
+ * (out-of-range vertex indices are reported as RT_ERR_ARG). */
+int rt_build_bvh_device(int device, const rt_vec3* positions_dev, size_t num_vertices,
+                        const uint32_t* indices_dev, size_t num_triangles, rt_bvh_node* nodes_dev,
+                        rt_aabb* aabbs_dev, void* hip_stream);
 
 /* HW1 mesh: LoadOBJ_ToMeshSOA (HW1/src/MeshOBJ.cpp:143-281). */
 typedef struct rt_mesh rt_mesh;

@@ -6,7 +6,7 @@ include/rt_mi355x.h); this package is the host-side mirror of the reference inte
 from ._lib import (RTError, RT_KERNEL_AUTO, RT_KERNEL_LANE, RT_KERNEL_WAVE, RT_TILES_AUTO,  # noqa: F401
                    RT_TILES_LINEAR, RT_TILES_ROWS, RT_TILES_XCD_CHUNK)
 from .api import (  # noqa: F401
-    LIGHT_DTYPE, Camera, DeviceScene, HostScene, MeshHW1, build_bvh, default_material, device_count,
+    LIGHT_DTYPE, Camera, DeviceScene, HostScene, MeshHW1, build_bvh, build_bvh_device, default_material, device_count,
     encode_p6, encode_p6_device, intersect_rays, jittered_samples, p6_header, quantize_p6_device, read_p6,
     render, render_hw1, unpermute_strips_device, write_p6,
 )

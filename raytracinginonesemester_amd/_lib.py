@@ -112,6 +112,7 @@ SIGNATURES = {
     "rt_host_scene_arrays": (I, [P, P]),
     "rt_host_scene_free": (None, [P]),
     "rt_build_bvh": (I, [P, SZ, P, SZ, P, P]),
+    "rt_build_bvh_device": (I, [I, P, SZ, P, SZ, P, P, P]),
     "rt_mesh_load_obj_hw1": (I, [C.c_char_p, P]),
     "rt_mesh_view_get": (I, [P, P]),
     "rt_mesh_free": (None, [P]),
@@ -153,6 +154,13 @@ def lib() -> C.CDLL:
     if _lib is None:
         if not LIB_PATH.exists():
             raise RTError(-6, f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        # One HIP runtime per process: when torch is installed, its bundled HIP runtime must be
+        # the one this library binds to (device pointers and streams are shared with torch), so
+        # torch is loaded first.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(str(LIB_PATH))
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)

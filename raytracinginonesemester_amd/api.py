@@ -348,6 +348,34 @@ def build_bvh(positions, indices):
     return nodes, aabbs
 
 
+def build_bvh_device(positions, indices, device: int = 0, stream=None, tensors: bool = False):
+    """The LBVH build on the GPU (rt_build_bvh_device): the same (nodes (2P-1,4), aabbs (2P-1,6))
+    as build_bvh.  positions (nv,3) float32 / indices (P,3) uint32 may be numpy arrays or device
+    tensors; tensors=True returns device tensors (nodes as int32 bit patterns) instead of numpy."""
+    import torch
+
+    dev = torch.device("cuda", device)
+
+    def on_dev(a, dt_np):
+        if isinstance(a, torch.Tensor):
+            return a.to(dev).contiguous()
+        return torch.from_numpy(np.ascontiguousarray(a, dt_np).view(np.int32 if dt_np == np.uint32 else dt_np)
+                                .copy()).to(dev)
+
+    pos = on_dev(positions, np.float32).reshape(-1, 3)
+    idx = on_dev(indices, np.uint32).reshape(-1, 3)
+    P = idx.shape[0]
+    nodes = torch.empty((max(2 * P - 1, 1), 4), dtype=torch.int32, device=dev)
+    aabbs = torch.empty((max(2 * P - 1, 1), 6), dtype=torch.float32, device=dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    check(lib().rt_build_bvh_device(device, pos.data_ptr(), pos.shape[0], idx.data_ptr(), P, nodes.data_ptr(),
+                                    aabbs.data_ptr(), stream))
+    if tensors:
+        return nodes, aabbs
+    return nodes.cpu().numpy().view(np.uint32), aabbs.cpu().numpy()
+
+
 def _ppm_opts(maxval=255, clamp=True, gamma2=True, flip_y=False) -> L.PPMOptions:
     return L.PPMOptions(int(maxval), 1 if clamp else 0, 1 if gamma2 else 0, 1 if flip_y else 0)
 

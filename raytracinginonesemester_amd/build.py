@@ -4,7 +4,7 @@
 
 * librt_mi355x.so — rt_host.cpp (g++) + the device translation units (hipcc
   --offload-arch=gfx950): rt_device.hip (scene + render), rt_frame.hip (P6 quantisation and
-  strip un-permute on the device).
+  strip un-permute on the device), rt_lbvh.hip (LBVH build on the device).
   Every float path is compiled with -ffp-contract=off and without fast-math; HIP's default
   correctly rounded f32 division / sqrt stay on (parity with the reference CPU build).
 * rt_render_cli   — C++ CLI over the C ABI (scene JSON in, P6 out), G/src/main.cu's role.
@@ -26,7 +26,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 FP = ["-ffp-contract=off", "-fno-fast-math"]
-DEVICE_UNITS = ["rt_device", "rt_frame"]
+DEVICE_UNITS = ["rt_device", "rt_frame", "rt_lbvh"]
 
 
 def _run(cmd):

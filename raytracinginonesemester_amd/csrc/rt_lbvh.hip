@@ -31,7 +31,6 @@
 
 using rt::set_error;
 using rt::hip_msg;
-using rt::DevBuf;
 using rt::DeviceGuard;
 
 namespace {
@@ -226,7 +225,7 @@ __device__ __forceinline__ int cub(unsigned long long a, unsigned long long b) {
 // One internal node per lane: determine_range (bvh.h:303-361) + find_split (:363-394); the
 // node writes its own children and their parent links (each node has one parent: no races).
 __global__ __launch_bounds__(BLOCK) void internal_kernel(const unsigned long long* __restrict__ key, uint32_t P,
-                                                         rt_bvh_node* __restrict__ nodes) {
+                                                         rt_bvh_node* __restrict__ nodes, uint2* __restrict__ range) {
     const uint32_t idx = blockIdx.x * BLOCK + threadIdx.x;
     if (idx + 1 >= P) return;
     uint32_t first, last;
@@ -278,6 +277,7 @@ __global__ __launch_bounds__(BLOCK) void internal_kernel(const unsigned long lon
     uint32_t left = gamma, right = gamma + 1;
     if (first == gamma) left += P - 1;  // min(first, last) == gamma: a leaf
     if (last == gamma + 1) right += P - 1;
+    range[idx] = make_uint2(first, last);
     nodes[idx].object_idx = NONE;
     nodes[idx].left_idx = left;
     nodes[idx].right_idx = right;
@@ -285,33 +285,64 @@ __global__ __launch_bounds__(BLOCK) void internal_kernel(const unsigned long lon
     nodes[right].parent_idx = idx;
 }
 
-// Bottom-up refit: one lane per leaf climbs while it is the second child to arrive.  The box
-// store is released by the fence before the flag update and acquired by the fence after it
-// (agent scope: the loads below miss in a stale L1/K-cache).
-__global__ __launch_bounds__(BLOCK) void refit_kernel(const rt_bvh_node* __restrict__ nodes, uint32_t P,
-                                                      rt_aabb* aabbs, uint32_t* flags) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= P) return;
-    uint32_t parent = nodes[(P - 1) + i].parent_idx;
-    while (parent != NONE) {
-        __threadfence();
-        if (atomicAdd(&flags[parent], 1u) == 0) return;
-        __threadfence();
-        const uint32_t l = nodes[parent].left_idx, r = nodes[parent].right_idx;
-        const Box lb = {{__hip_atomic_load(&aabbs[l].min_corner.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __hip_atomic_load(&aabbs[l].min_corner.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __hip_atomic_load(&aabbs[l].min_corner.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)},
-                        {__hip_atomic_load(&aabbs[l].max_corner.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __hip_atomic_load(&aabbs[l].max_corner.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __hip_atomic_load(&aabbs[l].max_corner.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)}};
-        const Box rb = {{__hip_atomic_load(&aabbs[r].min_corner.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __hip_atomic_load(&aabbs[r].min_corner.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __hip_atomic_load(&aabbs[r].min_corner.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)},
-                        {__hip_atomic_load(&aabbs[r].max_corner.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __hip_atomic_load(&aabbs[r].max_corner.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __hip_atomic_load(&aabbs[r].max_corner.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)}};
-        store_box(aabbs, parent, merge(lb, rb));
-        parent = nodes[parent].parent_idx;
+// Bottom-up refit, one lane per leaf climbing while it is the second child to arrive at a
+// node.  Agent-scope ordering on this chip means an L2 write-back + invalidate per fence (the
+// XCDs' L2s are not coherent), so the climb is split where it needs no such fence:
+//  * refit_chunk_kernel: workgroup b owns leaves [b*CHUNK, (b+1)*CHUNK) and refits every node
+//    whose leaf range [first, last] lies inside its chunk — both children of such a node are
+//    finished by the same workgroup, so workgroup-scope acq_rel atomics on the arrival flags
+//    order the box stores (one CU, one L1).  A finished node whose parent's range crosses the
+//    chunk is appended to the top list.
+//  * refit_top_kernel: one workgroup climbs from the top-list entries through the nodes whose
+//    ranges cross chunks (a few per chunk), again with workgroup-scope flags; phase-1 boxes
+//    are visible across the kernel boundary.
+// merge(left, right) has a fixed argument order, so which lane merges a node does not matter.
+constexpr uint32_t CHUNK = 2048;
+constexpr int TOP_BLOCK = 1024;
+
+__device__ __forceinline__ uint32_t arrive(uint32_t* flag) {
+    return __hip_atomic_fetch_add(flag, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void merge_node(const rt_bvh_node* nodes, rt_aabb* aabbs, uint32_t p) {
+    const rt_bvh_node nd = nodes[p];
+    store_box(aabbs, p, merge(load_box(aabbs, nd.left_idx), load_box(aabbs, nd.right_idx)));
+}
+
+__global__ __launch_bounds__(BLOCK) void refit_chunk_kernel(const rt_bvh_node* __restrict__ nodes, uint32_t P,
+                                                            const uint2* __restrict__ range, rt_aabb* aabbs,
+                                                            uint32_t* flags, uint32_t* top_count,
+                                                            uint32_t* __restrict__ top_list) {
+    const uint32_t c0 = blockIdx.x * CHUNK, c1 = min(c0 + CHUNK, P);
+    for (uint32_t i = c0 + threadIdx.x; i < c1; i += BLOCK) {
+        uint32_t x = (P - 1) + i;
+        uint32_t p = nodes[x].parent_idx;
+        while (p != NONE) {
+            const uint2 rg = range[p];
+            if (rg.x < c0 || rg.y >= c1) {
+                top_list[atomicAdd(top_count, 1u)] = x;
+                break;
+            }
+            if (arrive(&flags[p]) == 0) break;
+            merge_node(nodes, aabbs, p);
+            x = p;
+            p = nodes[p].parent_idx;
+        }
+    }
+}
+
+__global__ __launch_bounds__(TOP_BLOCK) void refit_top_kernel(const rt_bvh_node* __restrict__ nodes,
+                                                              rt_aabb* aabbs, uint32_t* flags,
+                                                              const uint32_t* top_count,
+                                                              const uint32_t* __restrict__ top_list) {
+    const uint32_t n = *top_count;
+    for (uint32_t k = threadIdx.x; k < n; k += TOP_BLOCK) {
+        uint32_t p = nodes[top_list[k]].parent_idx;
+        while (p != NONE) {
+            if (arrive(&flags[p]) == 0) break;
+            merge_node(nodes, aabbs, p);
+            p = nodes[p].parent_idx;
+        }
     }
 }
 
@@ -333,42 +364,57 @@ extern "C" int rt_build_bvh_device(int device, const rt_vec3* positions_dev, siz
     DeviceGuard g(device);
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
     const uint32_t n = (uint32_t)P;
-    // scratch: unsorted leaf boxes, Morton codes + triangle ids (double-buffered for the sort),
-    // 64-bit keys, refit flags, reduction keys + error flag, sort temporary storage
-    DevBuf boxes, code, tri, code2, tri2, key64, flags, misc, tmp;
-    if ((rc = boxes.alloc(P * sizeof(rt_aabb))) || (rc = code.alloc(P * 4)) || (rc = tri.alloc(P * 4)) ||
-        (rc = code2.alloc(P * 4)) || (rc = tri2.alloc(P * 4)) || (rc = key64.alloc(P * 8)) ||
-        (rc = flags.alloc(P * 4)) || (rc = misc.alloc(sizeof(BoundKeys) + 16)))
-        return rc;
+    // One stream-ordered workspace (pooled by the runtime across builds): unsorted leaf boxes,
+    // Morton codes + triangle ids (double-buffered for the sort), 64-bit keys, node ranges,
+    // arrival flags, top list, reduction keys + error flag + top count, sort storage.
+    size_t tmp_bytes = 0;
+    HIP_TRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                      (uint32_t*)nullptr, (uint32_t*)nullptr, n, 0u, 30u, st));
+    size_t off = 0;
+    auto carve = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
+    const size_t o_box = carve(P * sizeof(rt_aabb)), o_c0 = carve(P * 4), o_t0 = carve(P * 4), o_c1 = carve(P * 4),
+                 o_t1 = carve(P * 4), o_k64 = carve(P * 8), o_rng = carve(P * 8), o_fl = carve(P * 4),
+                 o_top = carve(2 * P * 4), o_misc = carve(sizeof(BoundKeys) + 16), o_tmp = carve(tmp_bytes);
+    void* ws = nullptr;
+    HIP_TRY(hipMallocAsync(&ws, off, st));
+    struct WsFree {
+        void* p; hipStream_t s;
+        ~WsFree() { if (p) (void)hipFreeAsync(p, s); }
+    } ws_free{ws, st};
+    char* W = static_cast<char*>(ws);
+    auto* bx = reinterpret_cast<rt_aabb*>(W + o_box);
+    auto* c0 = reinterpret_cast<uint32_t*>(W + o_c0);
+    auto* t0 = reinterpret_cast<uint32_t*>(W + o_t0);
+    auto* c1 = reinterpret_cast<uint32_t*>(W + o_c1);
+    auto* t1 = reinterpret_cast<uint32_t*>(W + o_t1);
+    auto* k64 = reinterpret_cast<unsigned long long*>(W + o_k64);
+    auto* rng = reinterpret_cast<uint2*>(W + o_rng);
+    auto* fl = reinterpret_cast<uint32_t*>(W + o_fl);
+    auto* top = reinterpret_cast<uint32_t*>(W + o_top);
+    auto* keys = reinterpret_cast<BoundKeys*>(W + o_misc);
+    int* err = reinterpret_cast<int*>(W + o_misc + sizeof(BoundKeys));
+    uint32_t* top_count = reinterpret_cast<uint32_t*>(W + o_misc + sizeof(BoundKeys) + 4);
     BoundKeys init;
     for (int k = 0; k < 3; ++k) { init.k[k] = ~0ull; init.k[3 + k] = 0ull; }
-    auto* keys = static_cast<BoundKeys*>(misc.p);
-    int* err = reinterpret_cast<int*>(static_cast<char*>(misc.p) + sizeof(BoundKeys));
     HIP_TRY(hipMemcpyAsync(keys, &init, sizeof(init), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(err, 0, sizeof(int), st));
-    auto* bx = static_cast<rt_aabb*>(boxes.p);
+    HIP_TRY(hipMemsetAsync(err, 0, 8, st));  // err + top_count
     hipLaunchKernelGGL(leaf_boxes_kernel, dim3(grid_of(P)), dim3(BLOCK), 0, st, positions_dev,
                        (uint32_t)num_vertices, indices_dev, n, bx, keys, err);
     HIP_TRY(hipGetLastError());
-    auto* c0 = static_cast<uint32_t*>(code.p);
-    auto* t0 = static_cast<uint32_t*>(tri.p);
-    auto* c1 = static_cast<uint32_t*>(code2.p);
-    auto* t1 = static_cast<uint32_t*>(tri2.p);
     hipLaunchKernelGGL(morton_kernel, dim3(grid_of(P)), dim3(BLOCK), 0, st, bx, n, keys, c0, t0);
     HIP_TRY(hipGetLastError());
-    size_t tmp_bytes = 0;
-    HIP_TRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, c0, c1, t0, t1, n, 0u, 30u, st));
-    if ((rc = tmp.alloc(tmp_bytes ? tmp_bytes : 4))) return rc;
-    HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tmp_bytes, c0, c1, t0, t1, n, 0u, 30u, st));
-    auto* k64 = static_cast<unsigned long long*>(key64.p);
-    auto* fl = static_cast<uint32_t*>(flags.p);
+    HIP_TRY(rocprim::radix_sort_pairs(W + o_tmp, tmp_bytes, c0, c1, t0, t1, n, 0u, 30u, st));
     hipLaunchKernelGGL(leaves_kernel, dim3(grid_of(P)), dim3(BLOCK), 0, st, bx, n, c1, t1, k64, nodes_dev,
                        aabbs_dev, fl);
     HIP_TRY(hipGetLastError());
     if (P > 1) {
-        hipLaunchKernelGGL(internal_kernel, dim3(grid_of(P - 1)), dim3(BLOCK), 0, st, k64, n, nodes_dev);
+        hipLaunchKernelGGL(internal_kernel, dim3(grid_of(P - 1)), dim3(BLOCK), 0, st, k64, n, nodes_dev, rng);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(refit_kernel, dim3(grid_of(P)), dim3(BLOCK), 0, st, nodes_dev, n, aabbs_dev, fl);
+        hipLaunchKernelGGL(refit_chunk_kernel, dim3((unsigned)((P + CHUNK - 1) / CHUNK)), dim3(BLOCK), 0, st,
+                           nodes_dev, n, rng, aabbs_dev, fl, top_count, top);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(refit_top_kernel, dim3(1), dim3(TOP_BLOCK), 0, st, nodes_dev, aabbs_dev, fl, top_count,
+                           top);
         HIP_TRY(hipGetLastError());
     }
     int herr = 0;

@@ -51,6 +51,9 @@ constexpr uint32_t NO_REF = 0xFFFFFFFFu;
 constexpr uint32_t VER_FORCE = 0xFFFFFFFFu;   // pop must re-test (root)
 constexpr int STACK_CAP = 64;                 // one entry per lane of the wave stack
 constexpr int BLOCK = 256;
+// Kernel instantiation flag on top of RT_KERNEL_WAVE: traverse the 4-ary records (SceneView::wide).
+// A compile-time choice, so each kernel holds one traversal loop per ray kind.
+constexpr int MODE_WIDE = 16;
 constexpr float kRayTMin = 1e-4f;             // query.h:233
 constexpr float RT_EPS = 1e-3f;               // shader.h:22
 
@@ -337,11 +340,6 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
     }
 }
 
-__device__ __forceinline__ void traverse_wave(const SceneView& sc, const RayPre& r, bool active,
-                                              bool any_hit, float any_hit_dist, HitState& hs) {
-    if (sc.wide) traverse_wave_impl<true>(sc, r, active, any_hit, any_hit_dist, hs);
-    else traverse_wave_impl<false>(sc, r, active, any_hit, any_hit_dist, hs);
-}
 
 // ---- LANE traversal (private stack per lane; the reference's shape) ---------------------
 __device__ __forceinline__ void traverse_lane(const SceneView& sc, const RayPre& r, bool active,
@@ -397,7 +395,7 @@ template <int MODE>
 __device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, bool active, bool any_hit,
                                          float any_hit_dist, HitState& hs) {
     if constexpr (MODE == RT_KERNEL_LANE) traverse_lane(sc, r, active, any_hit, any_hit_dist, hs);
-    else traverse_wave(sc, r, active, any_hit, any_hit_dist, hs);
+    else traverse_wave_impl<(MODE & MODE_WIDE) != 0>(sc, r, active, any_hit, any_hit_dist, hs);
 }
 
 // Full hit record of the winning leaf (intersectTriangle's tail, query.h:110-130).
@@ -1432,6 +1430,7 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(s->evm[slot], st));
     if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, st);
+    else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, st);
     else launch<RT_KERNEL_WAVE>(P, samples, st);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(s->ev1[slot], st));

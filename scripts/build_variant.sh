@@ -12,5 +12,6 @@ python3 -c "import sys; sys.path.insert(0, '$ROOT'); from raytracinginonesemeste
     -mcode-object-version=5 -Wno-unused-function "$@" -I"$ROOT/include" -I"$ROOT/raytracinginonesemester_amd/csrc" \
     -c "$ROOT/raytracinginonesemester_amd/csrc/rt_device.hip" -o "$OUT/rt_device.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$ROOT/build/obj/rt_host.o" "$OUT/rt_device.o" \
+    "$ROOT/build/obj/rt_frame.o" "$ROOT/build/obj/rt_lbvh.o" \
     -o "$OUT/librt_mi355x.so"
 echo "$OUT/librt_mi355x.so"

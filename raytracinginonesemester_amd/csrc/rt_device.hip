@@ -238,13 +238,17 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
     [[maybe_unused]] const int so = any_hit ? 1 : 0;
     RT_STAT(0 + so, 1);
     RT_STAT(13 + so, __popcll(alive));
+    // The root's pop-time test (SearchBVH tests every popped node, query.h:252-254) is made
+    // here with the initial bestT, before the loop, so the loop never needs the root box.
+    const uint64_t root_mask = box_hit_mask(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
+    if (root_mask == 0) return;
     uint32_t st_ref = 0, st_mlo = 0, st_mhi = 0, st_ver = 0;  // lane k holds entry k
     int sp = 0;
     uint32_t wave_ver = 0;
     st_ref = wrlane(sc.root_ref, 0, st_ref);
-    st_mlo = wrlane((uint32_t)alive, 0, st_mlo);
-    st_mhi = wrlane((uint32_t)(alive >> 32), 0, st_mhi);
-    st_ver = wrlane(VER_FORCE, 0, st_ver);
+    st_mlo = wrlane((uint32_t)root_mask, 0, st_mlo);
+    st_mhi = wrlane((uint32_t)(root_mask >> 32), 0, st_mhi);
+    st_ver = wrlane(wave_ver, 0, st_ver);
     sp = 1;
     while (sp > 0) {
         --sp;
@@ -261,9 +265,7 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
         if (ver != wave_ver) {  // some lane's bestT changed since the push: pop-time re-test
             RT_STAT(6 + so, 1);
             BoxP ob;
-            if (ver == VER_FORCE) {
-                ob = own_box(sc, ref, true);
-            } else if (leaf) {
+            if (leaf) {
                 const float4 c = ldc(L + 2), d = ldc(L + 3);
                 ob = BoxP{hi2(c), lo2(d), hi2(d)};
             } else {

@@ -116,9 +116,11 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
-// v_writelane equivalent (no clang builtin on this toolchain): lane l takes v.
+// v_writelane_b32 (the LLVM intrinsic; clang has no builtin for it on this toolchain): lane l
+// takes v.  v and l are wave-uniform at every call.
+extern "C" __device__ int rt_llvm_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
 __device__ __forceinline__ uint32_t wrlane(uint32_t v, uint32_t l, uint32_t old) {
-    return lane_id() == l ? v : old;
+    return (uint32_t)rt_llvm_writelane((int)v, (int)l, (int)old);
 }
 
 // ---- traversal statistics (instrumented variant builds only: -DRT_STATS) -----------------
@@ -144,6 +146,13 @@ __device__ __forceinline__ float4 ldc(const float4* p) {
     return make_float4(v.x, v.y, v.z, v.w);
 #else
     return *p;
+#endif
+}
+__device__ __forceinline__ vf4 ldc_v(const float4* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *(const __attribute__((address_space(4))) vf4*)p;
+#else
+    return *reinterpret_cast<const vf4*>(p);
 #endif
 }
 __device__ __forceinline__ uint4 ldc_u(const float4* p) {
@@ -242,6 +251,9 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
     // here with the initial bestT, before the loop, so the loop never needs the root box.
     const uint64_t root_mask = box_hit_mask(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
     if (root_mask == 0) return;
+#ifdef RT_EXP_ROOT_ONLY  // timing experiments only (wrong output): stop after the root test
+    return;
+#endif
     uint32_t st_ref = 0, st_mlo = 0, st_mhi = 0, st_ver = 0;  // lane k holds entry k
     int sp = 0;
     uint32_t wave_ver = 0;
@@ -296,13 +308,23 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
         RT_STAT(8 + so, 1);
         if constexpr (WIDE) {
             // 4-ary record: up to four entries in push order, each pushed if some lane passes.
+            // The whole record in one round trip: the seven 16-byte scalar loads are issued
+            // together and waited for once (the empty asm keeps the compiler from sinking each
+            // load next to its child's test, one load + wait per child).
             const float4* W = sc.wnode + 8 * (size_t)ref;
-            const uint4 wr = ldc_u(W + 6);
-            const uint32_t refs[4] = {wr.x, wr.y, wr.z, wr.w};
+            vf4 wq[7];
+#pragma unroll
+            for (int k = 0; k < 7; ++k) wq[k] = ldc_v(W + k);
+            asm volatile("" ::"s"(wq[0]), "s"(wq[1]), "s"(wq[2]), "s"(wq[3]), "s"(wq[4]), "s"(wq[5]), "s"(wq[6]));
+            const uint32_t refs[4] = {__float_as_uint(wq[6].x), __float_as_uint(wq[6].y), __float_as_uint(wq[6].z),
+                                      __float_as_uint(wq[6].w)};
+            float4 wv[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) wv[k] = make_float4(wq[k].x, wq[k].y, wq[k].z, wq[k].w);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (refs[k] == NO_REF) continue;
-                const float4 p = ldc(W + (3 * k) / 2), q = ldc(W + (3 * k) / 2 + 1);
+                const float4 p = wv[(3 * k) / 2], q = wv[(3 * k) / 2 + 1];
                 const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
                 const uint64_t mk_ = box_hit_mask(r, bk, hs.bestT, mask);
                 if (mk_ != 0) {
@@ -506,6 +528,9 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid, const 
                 }
             }
         }
+#ifdef RT_EXP_NO_SHADOW  // timing experiments only (wrong output): skip the shadow traversal
+        need = false;
+#endif
         HitState shs;
         traverse<MODE>(sc, sray, need, true, dist, shs);
         const bool occluded = need && shs.slot >= 0 && shs.bestT < dist;
@@ -865,7 +890,10 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
 // Each block runs tiles_per_block virtual blocks (planned_tile): fewer, longer blocks, so
 // the dispatcher does not spend the frame launching blocks that find no live tile.
 template <int MODE, bool SAMPLES, bool D1>
-__global__ __launch_bounds__(BLOCK, 4) void render_tiles_kernel(RenderParams P) {
+#ifndef RT_RENDER_WAVES
+#define RT_RENDER_WAVES 6  // waves per SIMD the render kernel is compiled for (80 VGPRs)
+#endif
+__global__ __launch_bounds__(BLOCK, RT_RENDER_WAVES) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
     const int b = (int)blockIdx.x, g = (int)gridDim.x;
     const int q = P.nqueues == 1 ? 0 : (b & 7);

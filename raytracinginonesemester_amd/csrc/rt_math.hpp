@@ -60,7 +60,9 @@ constexpr float kBoxRel = 4e-6f;
 // serve the pre-classification only, never the decision of an ambiguous case.
 struct RayPre {
     f3 o, d;
-    f3 ivp, ivn, c1, c2, e2;
+    v2f ivx, ivy, ivz;  // per axis (ivp, ivn)
+    v2f cx, cy, cz;     // per axis (c1, c2)
+    f3 e2;
     float m2;       // 2 max(e2): the one-margin HIT test's (box_sure_hit1); +inf if unsafe
     float hit_lim;  // +inf, or -inf for a ray the pre-classification does not handle
     uint32_t par;
@@ -101,10 +103,12 @@ __host__ __device__ __forceinline__ RayPre make_ray(f3 o, f3 d, f3 bmax) {
         e2[a] = 2.0f * E;
     }
     if (!safe) c1[0] = c1[1] = c1[2] = c2[0] = c2[1] = c2[2] = NAN;
-    r.ivp = mk(ivp[0], ivp[1], ivp[2]);
-    r.ivn = mk(ivn[0], ivn[1], ivn[2]);
-    r.c1 = mk(c1[0], c1[1], c1[2]);
-    r.c2 = mk(c2[0], c2[1], c2[2]);
+    r.ivx = (v2f){ivp[0], ivn[0]};
+    r.ivy = (v2f){ivp[1], ivn[1]};
+    r.ivz = (v2f){ivp[2], ivn[2]};
+    r.cx = (v2f){c1[0], c2[0]};
+    r.cy = (v2f){c1[1], c2[1]};
+    r.cz = (v2f){c1[2], c2[2]};
     r.e2 = mk(e2[0], e2[1], e2[2]);
     r.m2 = safe ? 2.0f * fmaxf(fmaxf(e2[0], e2[1]), e2[2]) : INFINITY;
     r.hit_lim = safe ? INFINITY : -INFINITY;
@@ -178,12 +182,12 @@ struct AxisEnds {
 };
 __host__ __device__ __forceinline__ AxisEnds box_ends(const RayPre& r, const BoxP& b) {
     AxisEnds e;
-    e.lLx = __builtin_fmaf(b.x.x, r.ivp.x, __builtin_fmaf(b.x.y, r.ivn.x, r.c1.x));
-    e.hHx = __builtin_fmaf(b.x.y, r.ivp.x, __builtin_fmaf(b.x.x, r.ivn.x, r.c2.x));
-    e.lLy = __builtin_fmaf(b.y.x, r.ivp.y, __builtin_fmaf(b.y.y, r.ivn.y, r.c1.y));
-    e.hHy = __builtin_fmaf(b.y.y, r.ivp.y, __builtin_fmaf(b.y.x, r.ivn.y, r.c2.y));
-    e.lLz = __builtin_fmaf(b.z.x, r.ivp.z, __builtin_fmaf(b.z.y, r.ivn.z, r.c1.z));
-    e.hHz = __builtin_fmaf(b.z.y, r.ivp.z, __builtin_fmaf(b.z.x, r.ivn.z, r.c2.z));
+    e.lLx = __builtin_fmaf(b.x.x, r.ivx.x, __builtin_fmaf(b.x.y, r.ivx.y, r.cx.x));
+    e.hHx = __builtin_fmaf(b.x.y, r.ivx.x, __builtin_fmaf(b.x.x, r.ivx.y, r.cx.y));
+    e.lLy = __builtin_fmaf(b.y.x, r.ivy.x, __builtin_fmaf(b.y.y, r.ivy.y, r.cy.x));
+    e.hHy = __builtin_fmaf(b.y.y, r.ivy.x, __builtin_fmaf(b.y.x, r.ivy.y, r.cy.y));
+    e.lLz = __builtin_fmaf(b.z.x, r.ivz.x, __builtin_fmaf(b.z.y, r.ivz.y, r.cz.x));
+    e.hHz = __builtin_fmaf(b.z.y, r.ivz.x, __builtin_fmaf(b.z.x, r.ivz.y, r.cz.y));
     return e;
 }
 // Lc = max(tmin, lowLo) and Hc = min(tmax, highHi): MISS iff Lc > Hc.

@@ -125,14 +125,15 @@ __device__ __forceinline__ uint32_t wrlane(uint32_t v, uint32_t l, uint32_t old)
 
 // ---- traversal statistics (instrumented variant builds only: -DRT_STATS) -----------------
 #ifdef RT_STATS
-__device__ unsigned long long g_rt_stats[16];
+__device__ unsigned long long g_rt_stats[24];
 #define RT_STAT(i, n) do { if (lane_id() == 0) atomicAdd(&g_rt_stats[(i)], (unsigned long long)(n)); } while (0)
 #else
 #define RT_STAT(i, n) do { } while (0)
 #endif
 // 0/1 traversals (primary/shadow), 2/3 pops, 4/5 pops after a mask test passed, 6/7 pop-time
 // re-tests, 8/9 internal nodes, 10/11 leaves, 12 ambiguous box tests (wave-level), 13 lanes
-// active at traversal start (primary), 14 (shadow)
+// active at traversal start (primary), 14 (shadow), 15 primary traversals with no lane hitting,
+// 16 their pops, 17 primary traversals whose root test no lane passes
 
 // ---- node accessors ---------------------------------------------------------------------
 // Scene arrays are immutable while a frame renders: read them through the constant address
@@ -228,6 +229,9 @@ __device__ __forceinline__ uint64_t box_hit_mask(const RayPre& r, const BoxP& b,
 struct HitState {
     float bestT;
     int32_t slot;  // leaf index of the current best, -1 = none
+#ifdef RT_STATS
+    uint32_t pops;
+#endif
 };
 
 // ---- WAVE traversal ---------------------------------------------------------------------
@@ -243,6 +247,9 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
     uint64_t alive = ballot(active);
     hs.bestT = FLT_MAX;
     hs.slot = -1;
+#ifdef RT_STATS
+    hs.pops = 0;
+#endif
     if (alive == 0) return;
     [[maybe_unused]] const int so = any_hit ? 1 : 0;
     RT_STAT(0 + so, 1);
@@ -250,7 +257,10 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
     // The root's pop-time test (SearchBVH tests every popped node, query.h:252-254) is made
     // here with the initial bestT, before the loop, so the loop never needs the root box.
     const uint64_t root_mask = box_hit_mask(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
-    if (root_mask == 0) return;
+    if (root_mask == 0) {
+        if (!any_hit) RT_STAT(17, 1);
+        return;
+    }
 #ifdef RT_EXP_ROOT_ONLY  // timing experiments only (wrong output): stop after the root test
     return;
 #endif
@@ -269,6 +279,9 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
         const uint32_t ver = rdlane(st_ver, sp);
         mask &= alive;
         RT_STAT(2 + so, 1);
+#ifdef RT_STATS
+        ++hs.pops;
+#endif
         if (mask == 0) continue;
         RT_STAT(4 + so, 1);
         bool act = (mask & lane_bit) != 0;
@@ -556,10 +569,21 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
     if constexpr (D1) {
         HitState hs;
         traverse<MODE>(sc, ray, valid, false, 0.0f, hs);
+#ifdef RT_STATS
+        if constexpr (MODE != RT_KERNEL_LANE) {
+            if (ballot(valid) != 0 && ballot(valid && hs.slot >= 0) == 0) {
+                RT_STAT(15, 1);
+                RT_STAT(16, hs.pops);
+            }
+        }
+#endif
         if (valid) {
             *prim_idx = hs.slot >= 0 ? leaf_tri(sc, hs.slot) : -1;
             *prim_t = hs.slot >= 0 ? hs.bestT : -1.0f;
         }
+#ifdef RT_EXP_NO_SHADE  // timing experiments only (wrong output): primary traversal only
+        return mk(hs.bestT, 0.f, 0.f);
+#endif
         return shade_d1<MODE>(P, valid, ray, hs);
     }
     uint32_t rng = make_rng_seed(x, y, s);
@@ -1503,7 +1527,7 @@ extern "C" int rt_debug_stats(unsigned long long* out, int reset) {
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_stats), sizeof(g_rt_stats)));
     if (reset) {
-        unsigned long long z[16] = {};
+        unsigned long long z[24] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rt_stats), z, sizeof(z)));
     }
     return RT_OK;

@@ -1,10 +1,13 @@
-# A/B of library variants: scripts/exp_ab.sh "<variants>" [configs]; variant "default" = the in-tree library
+# Interleaved A/B of library variants in one process per config:
+#   scripts/exp_ab.sh "<variant> ..." [configs]; "default" = the in-tree library,
+#   other names = build/variants/<name>/librt_mi355x.so (scripts/build_variant.sh)
 set -e
 VARS=${1:-default}; CFGS=${2:-c3 c5}
+ARGS=""
 for v in $VARS; do
-  if [ $v = default ]; then L=""; else L="RT_MI355X_LIB=build/variants/$v/librt_mi355x.so"; fi
-  for c in $CFGS; do
-    if [ $c = c5 ]; then R="--rounds 1 --reps 3"; T=240; else R="--rounds 3 --reps 5"; T=120; fi
-    echo "== $v $c"; env $L timeout -k 10 $T python scripts/sweep.py --kernels wave --tiles rows --config $c $R
-  done
+  if [ $v = default ]; then ARGS="$ARGS default=default"; else ARGS="$ARGS $v=build/variants/$v/librt_mi355x.so"; fi
+done
+for c in $CFGS; do
+  if [ $c = c5 ]; then R="--rounds 3 --reps 2"; T=300; else R="--rounds 7 --reps 5"; T=150; fi
+  echo "== $c"; timeout -k 10 $T python scripts/ab_libs.py --config $c $R $ARGS
 done

@@ -1,9 +1,7 @@
+# Where the c3/c5 frame time goes: the default build against timing-only builds that skip parts
+# of the work (their frames are wrong by design), one process, interleaved rounds.
 set -e
-S="python scripts/sweep.py --kernels wave --tiles rows --rounds 3 --reps 5"
-for v in default noshadow rootonly; do
-  if [ $v = default ]; then L=""; else L="RT_MI355X_LIB=build/variants/$v/librt_mi355x.so"; fi
-  echo "== $v c3"; env $L timeout -k 10 120 $S --config c3
-  echo "== $v c5"; env $L timeout -k 10 200 $S --config c5 --rounds 1 --reps 2
-done
-echo "== stats c3"; RT_MI355X_LIB=build/variants/stats/librt_mi355x.so timeout -k 10 120 python scripts/stats.py c3
-echo "== stats c5"; RT_MI355X_LIB=build/variants/stats/librt_mi355x.so timeout -k 10 300 python scripts/stats.py c5
+A="default=default noshade=build/variants/noshade/librt_mi355x.so noshadow=build/variants/noshadow/librt_mi355x.so rootonly=build/variants/rootonly/librt_mi355x.so"
+echo "== c3"; timeout -k 10 200 python scripts/ab_libs.py --no-check --config c3 --rounds 7 --reps 5 $A
+echo "== c5"; timeout -k 10 300 python scripts/ab_libs.py --no-check --config c5 --rounds 2 --reps 2 $A
+echo "== tpb"; timeout -k 10 200 python scripts/sweep.py --kernels wave --tiles rows --tpb 1,2,4,8,16 --rounds 3 --reps 5

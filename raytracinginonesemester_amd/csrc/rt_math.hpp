@@ -124,13 +124,10 @@ __host__ __device__ __forceinline__ RayPre make_ray_mt(f3 o, f3 d) { return make
 // because t0 only grows and t1 only shrinks.
 __host__ __device__ inline bool box_hit_exact(const RayPre& r, const BoxP& b, double tmin, double tmax) {
     double t0 = tmin, t1 = tmax;
-    float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
-#if defined(__HIP_DEVICE_COMPILE__)
-    // Rare path (a few % of box tests): keep the compiler from hoisting double(o) and
-    // 1.0 / double(d) out of the traversal loops, twelve VGPRs live across every loop (and
-    // fewer waves per SIMD) for values this path recomputes in ~40 instructions.
-    asm volatile("" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(d[0]), "+v"(d[1]), "+v"(d[2]));
-#endif
+    // No register-pinning asm here: an empty asm "+v" on o/d (to keep the compiler from hoisting
+    // double(o) and 1/double(d) out of the traversal loops) measured no faster and, in the 6-wave
+    // build, exposed a miscompile of the bounce and binary-record kernels (golden parity failures).
+    const float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
     const float mn[3] = {b.x.x, b.y.x, b.z.x}, mx[3] = {b.x.y, b.y.y, b.z.y};
     bool ok = true;
 #pragma unroll

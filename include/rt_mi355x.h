@@ -242,6 +242,19 @@ int rt_render_hw1(int device, const rt_vec3* positions, const rt_vec3* normals,
                   rt_vec3 light_position, rt_vec3 light_color, int spp, const float* jitter,
                   float* rgb_host, int32_t* hit_idx_host, float* hit_t_host);
 
+/* rt_render_hw1 with a kernel selection and the device time of the kernels (HIP events;
+ * kernel_ms may be NULL).  flags 0: binned — a conservative per-triangle pixel rectangle
+ * (outside it ray_intersection provably rejects every camera ray), then per 16x16 block the
+ * brute-force loop over the triangles whose rectangle meets the block, in index order, so
+ * the output equals the brute-force loop's bit for bit; RT_HW1_BRUTE: every triangle for
+ * every ray (HW1/src/render.cpp:72-116 literally). */
+enum { RT_HW1_BRUTE = 1 };
+int rt_render_hw1_ex(int device, const rt_vec3* positions, const rt_vec3* normals,
+                     const uint32_t* indices, size_t num_triangles, const rt_camera* cam,
+                     rt_vec3 light_position, rt_vec3 light_color, int spp, const float* jitter,
+                     int flags, float* rgb_host, int32_t* hit_idx_host, float* hit_t_host,
+                     float* kernel_ms);
+
 /* Batched ray-triangle queries on the GPU (one triangle, n rays from `origin`), the device
  * Möller–Trumbore used by the kernels:  hw1 != 0 -> HW1 ray_intersection
  * (HW1/include/ray.h:67-117; the HW1 Ray constructor normalises each direction first, ray.h:25),

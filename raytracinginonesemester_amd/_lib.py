@@ -133,6 +133,7 @@ SIGNATURES = {
     "rt_render": (I, [P, P, P, P, P, P]),
     "rt_render_reference": (I, [SZ, I, I, P, Vec3, I, I, P, P, P, P, P, I, P, I, I, P]),
     "rt_render_hw1": (I, [I, P, P, P, SZ, P, Vec3, Vec3, I, P, P, P, P]),
+    "rt_render_hw1_ex": (I, [I, P, P, P, SZ, P, Vec3, Vec3, I, P, I, P, P, P, P]),
     "rt_intersect_rays": (I, [I, P, P, P, I, I, C.c_float, C.c_float, P, P]),
     "rt_powf_host": (C.c_float, [C.c_float, C.c_float]),
     "rt_powf_batch": (I, [I, P, P, I, P]),

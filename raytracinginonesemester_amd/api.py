@@ -307,9 +307,15 @@ def render(numTriangles, W, H, cam: Camera, missColor, max_depth, spp, nodes, aa
     return out
 
 
+RT_HW1_BRUTE = 1
+
+
 def render_hw1(positions, normals, indices, camera: Camera, light_position, light_color, spp: int = 1,
-               jitter=None, aov: bool = False, device: int = 0):
-    """HW1 brute-force path on the GPU: (H, W, 3) float32 [+ per-sample winning triangle / t]."""
+               jitter=None, aov: bool = False, device: int = 0, brute: bool = False, timing: bool = False):
+    """HW1 path on the GPU (HW1/src/render.cpp:72-116 semantics): (H, W, 3) float32 [+ per-sample
+    winning triangle / t] [+ device ms of the kernels when ``timing``].  ``brute`` runs every
+    triangle for every ray; the default skips triangles outside their conservative pixel
+    rectangle (same output bit for bit, see rt_render_hw1_ex)."""
     pos, nrm, idx = _c(positions, np.float32), _c(normals, np.float32), _c(indices, np.uint32)
     W, H = camera.pixel_width, camera.pixel_height
     rgb = np.zeros((H, W, 3), np.float32)
@@ -318,10 +324,15 @@ def render_hw1(positions, normals, indices, camera: Camera, light_position, ligh
         hi = np.zeros((H, W, spp), np.int32)
         ht = np.zeros((H, W, spp), np.float32)
     jit = None if jitter is None else _c(jitter, np.float32).reshape(-1)
-    check(lib().rt_render_hw1(int(device), ptr(pos), ptr(nrm), ptr(idx), idx.size // 3, C.byref(camera.c),
-                              _v3(light_position), _v3(light_color), int(spp), ptr(jit), ptr(rgb), ptr(hi),
-                              ptr(ht)))
-    return (rgb, hi, ht) if aov else rgb
+    ms = C.c_float(0.0)
+    check(lib().rt_render_hw1_ex(int(device), ptr(pos), ptr(nrm), ptr(idx), idx.size // 3, C.byref(camera.c),
+                                 _v3(light_position), _v3(light_color), int(spp), ptr(jit),
+                                 RT_HW1_BRUTE if brute else 0, ptr(rgb), ptr(hi), ptr(ht),
+                                 C.byref(ms) if timing else None))
+    out = (rgb, hi, ht) if aov else (rgb,)
+    if timing:
+        out = out + (ms.value,)
+    return out if len(out) > 1 else out[0]
 
 
 def intersect_rays(triangle18, dirs, origin=(0.0, 0.0, 0.0), hw1: bool = True, tmin: float = 0.0,

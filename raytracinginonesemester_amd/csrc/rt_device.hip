@@ -952,6 +952,10 @@ __global__ __launch_bounds__(BLOCK, RT_RENDER_WAVES) void render_tiles_kernel(Re
 struct Hw1Params {
     const float4* __restrict__ tri;   // 3 float4 per triangle: v0, e1, e2
     const float4* __restrict__ nrm;   // 3 float4 per triangle: n0, n1, n2
+    const int4* __restrict__ rects;   // binned path: per triangle (ix_lo, iy_lo, ix_hi, iy_hi)
+    const uint32_t* __restrict__ bin_count;   // binned path: per wave tile, triangles listed
+    const uint32_t* __restrict__ bin_offset;  // exclusive prefix sum of bin_count
+    const uint32_t* __restrict__ bin_list;    // triangle indices, per tile (any order)
     int32_t num_tris;
     f3 center, p00, du, dv;
     int32_t W, H, spp;
@@ -1037,6 +1041,318 @@ __global__ __launch_bounds__(BLOCK) void render_hw1_kernel(Hw1Params P) {
         o[0] = acc.x / fs;
         o[1] = acc.y / fs;
         o[2] = acc.z / fs;
+    }
+}
+
+// ---- HW1 binned (rt_render_hw1 default; same output as render_hw1_kernel) ---------------
+// The brute-force loop's answer is the first index among the triangles ray_intersection
+// (mt_hw1) accepts with the smallest t.  Skipping triangles that provably cannot be accepted
+// for a ray, and visiting the rest in index order with the same strict `<`, gives that answer
+// bit for bit.  hw1_rect_kernel bounds, per triangle, the integer pixel positions (ix, iy)
+// whose camera ray mt_hw1 may accept; the render kernel gives each 16x16-pixel block the
+// triangles whose rectangle meets it, in index order.
+//
+// Why the rectangle is conservative.  With tvec = o - v0 and qvec = tvec x e1 (float, exactly
+// as mt_hw1 computes them, both ray-independent), mt_hw1's float quantities are
+//   det = d.(e2 x e1) + Ed,   U = d.(e2 x tvec) + Eu,   V = d.qvec + Ev,   tnum = e2.qvec,
+// u = U * (1/det), v = V * (1/det), t = tnum * (1/det), with |Ed|, |Eu|, |Ev| bounded by the
+// standard dot/cross rounding bounds (|d_j| <= 1).  When |tnum| is not tiny its sign s must
+// be det's (else t < 0), so acceptance needs four linear inequalities in d:
+//   s U >= 0,  s V >= 0,  s (det - U - V) >= -(4u|det| rounding of u + v and the divisions),
+//   s det >= FLT_EPSILON,
+// each relaxed by its error bound and by the rounding of unit() (d = D/|D| (1 + 3u)).  With
+// D = pixel00 + ix du + iy dv - center (exact, widened per axis by the tile-cull padding
+// for its float evaluation) and |D| in [Nmin, Nmax] over the image, every inequality becomes
+// a half-plane in (ix, iy); the rectangle is the bounding box (+1 pixel) of the padded image
+// rectangle clipped by the four half-planes.  Degenerate cases (tiny tnum, huge magnitudes,
+// an image whose directions reach 0) get the whole image.
+constexpr int HW1_TILE = 16;
+__device__ __forceinline__ void hw1_cross_d(const double a[3], const double b[3], double r[3]) {
+    r[0] = a[1] * b[2] - a[2] * b[1];
+    r[1] = a[2] * b[0] - a[0] * b[2];
+    r[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+__global__ __launch_bounds__(BLOCK) void hw1_rect_kernel(Hw1Params P, int4* __restrict__ rects) {
+    const int k = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    if (k >= P.num_tris) return;
+    const int X0 = -2, X1 = P.W + 1, Y0 = -2, Y1 = P.H + 1;  // ix in [x, x+1] (truncation)
+    const int4 all = make_int4(X0, Y0, X1, Y1), none = make_int4(1, 1, 0, 0);
+    const float4 A = P.tri[3 * (size_t)k], B = P.tri[3 * (size_t)k + 1], Cq = P.tri[3 * (size_t)k + 2];
+    const f3 v0 = mk(A.x, A.y, A.z), e1 = mk(B.x, B.y, B.z), e2 = mk(Cq.x, Cq.y, Cq.z);
+    const f3 tvec = sub(P.center, v0);  // mt_hw1's own float values
+    const f3 qvec = cross(tvec, e1);
+    const float tnum = dot(e2, qvec);
+    double mag = 0.0;
+    const float mv[15] = {v0.x, v0.y, v0.z, e1.x, e1.y, e1.z, e2.x, e2.y, e2.z, tvec.x, tvec.y, tvec.z,
+                          qvec.x, qvec.y, qvec.z};
+    for (int i = 0; i < 15; ++i) mag = fmax(mag, fabs((double)mv[i]));
+    if (!(mag < 1e15) || !(fabsf(tnum) >= 1e-20f)) {
+        rects[k] = all;
+        return;
+    }
+    const double sg = tnum > 0.0f ? 1.0 : -1.0;
+    const double tv[3] = {tvec.x, tvec.y, tvec.z}, ea[3] = {e1.x, e1.y, e1.z}, eb[3] = {e2.x, e2.y, e2.z},
+                 qv[3] = {qvec.x, qvec.y, qvec.z};
+    double au[3], ad[3];
+    hw1_cross_d(eb, tv, au);  // U = tvec.(d x e2) = d.(e2 x tvec)
+    hw1_cross_d(eb, ea, ad);  // det = (d x e2).e1 = d.(e2 x e1)
+    const double uu = 0x1p-24, dm = 1.0001;
+    const double pb[3] = {fabs(eb[2]) + fabs(eb[1]), fabs(eb[0]) + fabs(eb[2]), fabs(eb[1]) + fabs(eb[0])};
+    double Eu = 0, Ed = 0, Ev = 0, dmax = 0;
+    for (int i = 0; i < 3; ++i) {
+        Eu += fabs(tv[i]) * pb[i];
+        Ed += fabs(ea[i]) * pb[i];
+        Ev += fabs(qv[i]);
+        dmax += fabs(ad[i]);
+    }
+    Eu *= 8 * uu * dm;
+    Ed *= 8 * uu * dm;
+    Ev *= 4 * uu * dm;
+    dmax = dmax * dm + Ed;
+    if (!(dmax < 1e10)) {  // keeps |t| = |tnum / det| >= 1e-30: a wrong-sign t stays negative
+        rects[k] = all;
+        return;
+    }
+    const double tiny = 1e-30;
+    double c[4][3], w[4];
+    for (int i = 0; i < 3; ++i) {
+        c[0][i] = sg * au[i];
+        c[1][i] = sg * qv[i];
+        c[2][i] = sg * (ad[i] - au[i] - qv[i]);
+        c[3][i] = sg * ad[i];
+    }
+    w[0] = -(Eu + tiny);
+    w[1] = -(Ev + tiny);
+    w[2] = -(4 * uu * dmax + Eu + Ev + Ed + tiny);
+    w[3] = (double)FLT_EPSILON - Ed;
+    // D over the image, per axis, padded as in tile_misses_root
+    const double cc[3] = {P.center.x, P.center.y, P.center.z}, p0[3] = {P.p00.x, P.p00.y, P.p00.z},
+                 du[3] = {P.du.x, P.du.y, P.du.z}, dv[3] = {P.dv.x, P.dv.y, P.dv.z};
+    const double xm = fmax(fabs((double)X0), fabs((double)X1)), ym = fmax(fabs((double)Y0), fabs((double)Y1));
+    double D00[3], Dl[3], Dh[3], pad[3], scale = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        D00[a] = p0[a] - cc[a];
+        const double u0 = X0 * du[a], u1 = X1 * du[a], w0 = Y0 * dv[a], w1 = Y1 * dv[a];
+        Dl[a] = D00[a] + fmin(u0, u1) + fmin(w0, w1);
+        Dh[a] = D00[a] + fmax(u0, u1) + fmax(w0, w1);
+        pad[a] = 8.0 * 0x1p-23 * (fabs(cc[a]) + fabs(p0[a]) + xm * fabs(du[a]) + ym * fabs(dv[a]));
+        scale = fmax(scale, fmax(fabs(Dl[a]), fabs(Dh[a])));
+    }
+    double nmin2 = 0.0, nmax2 = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        pad[a] += 1e-5 * scale;
+        Dl[a] -= pad[a];
+        Dh[a] += pad[a];
+        const double near = Dl[a] > 0 ? Dl[a] : (Dh[a] < 0 ? Dh[a] : 0.0);
+        const double far = fmax(fabs(Dl[a]), fabs(Dh[a]));
+        nmin2 += near * near;
+        nmax2 += far * far;
+    }
+    const double nmin = sqrt(nmin2) * (1 - 1e-12), nmax = sqrt(nmax2) * (1 + 1e-12);
+    if (!(nmin > 0.0) || !(nmax < 1e300)) {
+        rects[k] = all;
+        return;
+    }
+    double px[8 + 4], py[8 + 4];
+    int n = 4;
+    px[0] = X0; py[0] = Y0;
+    px[1] = X1; py[1] = Y0;
+    px[2] = X1; py[2] = Y1;
+    px[3] = X0; py[3] = Y1;
+    for (int i = 0; i < 4 && n > 0; ++i) {
+        double cs = 0.0, cdm = 0.0, cpad = 0.0, cD00 = 0.0, al = 0.0, be = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            cs += fabs(c[i][a]);
+            cdm += fabs(c[i][a]) * fmax(fabs(Dl[a]), fabs(Dh[a]));
+            cpad += fabs(c[i][a]) * pad[a];
+            cD00 += c[i][a] * D00[a];
+            al += c[i][a] * du[a];
+            be += c[i][a] * dv[a];
+        }
+        const double w1 = w[i] - 4 * uu * dm * cs;              // unit() rounding of d
+        const double g = fmin(w1 * nmin, w1 * nmax);            // c.D >= w1 |D|
+        const double ga = g - cpad - 1e-9 * cdm - tiny - cD00;  // al ix + be iy >= ga
+        if (!(fabs(al) < 1e300 && fabs(be) < 1e300 && fabs(ga) < 1e300)) {
+            rects[k] = all;
+            return;
+        }
+        double qx[12], qy[12];
+        int m = 0;
+        for (int j = 0; j < n; ++j) {
+            const int jn = (j + 1) % n;
+            const double fc = al * px[j] + be * py[j] - ga, fn = al * px[jn] + be * py[jn] - ga;
+            if (fc >= 0) {
+                qx[m] = px[j];
+                qy[m] = py[j];
+                ++m;
+            }
+            if ((fc >= 0) != (fn >= 0)) {
+                const double tt = fc / (fc - fn);
+                qx[m] = px[j] + tt * (px[jn] - px[j]);
+                qy[m] = py[j] + tt * (py[jn] - py[j]);
+                ++m;
+            }
+        }
+        n = m;
+        for (int j = 0; j < n; ++j) {
+            px[j] = qx[j];
+            py[j] = qy[j];
+        }
+    }
+    if (n == 0) {
+        rects[k] = none;
+        return;
+    }
+    double lx = px[0], hx = px[0], ly = py[0], hy = py[0];
+    for (int j = 1; j < n; ++j) {
+        lx = fmin(lx, px[j]);
+        hx = fmax(hx, px[j]);
+        ly = fmin(ly, py[j]);
+        hy = fmax(hy, py[j]);
+    }
+    rects[k] = make_int4(max(X0, (int)floor(lx) - 1), max(Y0, (int)floor(ly) - 1), min(X1, (int)ceil(hx) + 1),
+                         min(Y1, (int)ceil(hy) + 1));
+}
+
+// Binning (a tiled rasterizer's): hw1_bin_kernel counts, per 16x4-pixel wave tile, the
+// triangles whose rectangle meets the tile's (ix, iy) range (pixel x uses ix in {x, x+1});
+// hw1_scan_kernel turns the counts into offsets; hw1_fill_kernel writes the lists.  A list's
+// order is whatever the atomics give, so the render kernel keeps the lexicographic minimum of
+// (t, index): the smallest t, the smallest index among equal t — exactly the brute-force
+// loop's winner (it keeps the first index whose t is strictly below every earlier one), and
+// independent of the visiting order.  (A NaN t is never below or equal to anything, in
+// either form.)
+constexpr int HW1_TW = 16, HW1_TH = 4;  // wave tile: 16 x 4 pixels
+__device__ __forceinline__ bool hw1_tile_range(const Hw1Params& P, int4 r, int& tx0, int& tx1, int& ty0, int& ty1) {
+    const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW, tiles_y = (P.H + HW1_TH - 1) / HW1_TH;
+    if (r.x > r.z || r.y > r.w) return false;
+    tx0 = max(0, r.x - 1) / HW1_TW;
+    ty0 = max(0, r.y - 1) / HW1_TH;
+    tx1 = min(tiles_x - 1, r.z / HW1_TW);
+    ty1 = min(tiles_y - 1, r.w / HW1_TH);
+    return r.z >= 0 && r.w >= 0 && tx0 <= tx1 && ty0 <= ty1;
+}
+
+__global__ __launch_bounds__(BLOCK) void hw1_bin_kernel(Hw1Params P, uint32_t* __restrict__ counts, int fill,
+                                                        uint32_t* __restrict__ cursor, uint32_t* __restrict__ list) {
+    const int k = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    if (k >= P.num_tris) return;
+    const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
+    int tx0, tx1, ty0, ty1;
+    if (!hw1_tile_range(P, P.rects[k], tx0, tx1, ty0, ty1)) return;
+    for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) {
+            const int t = ty * tiles_x + tx;
+            if (!fill) atomicAdd(&counts[t], 1u);
+            else list[P.bin_offset[t] + atomicAdd(&cursor[t], 1u)] = (uint32_t)k;
+        }
+}
+
+// Exclusive prefix sum of n counts in one workgroup (n is the number of wave tiles, small);
+// offsets[n] = total.
+__global__ __launch_bounds__(1024) void hw1_scan_kernel(const uint32_t* __restrict__ counts, uint32_t* __restrict__ offsets,
+                                                        int n) {
+    __shared__ uint32_t part[1024];
+    const int t = (int)threadIdx.x;
+    const int per = (n + 1023) / 1024;
+    const int lo = min(n, t * per), hi = min(n, lo + per);
+    uint32_t sum = 0;
+    for (int i = lo; i < hi; ++i) sum += counts[i];
+    part[t] = sum;
+    __syncthreads();
+    for (int st = 1; st < 1024; st <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t v = t >= st ? part[t - st] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+    for (int i = lo; i < hi; ++i) {
+        offsets[i] = run;
+        run += counts[i];
+    }
+    if (t == 1023) offsets[n] = part[1023];
+}
+
+// One 16x16-pixel block per workgroup, one 16x4-pixel tile (and list) per wave; every pixel
+// lane runs mt_hw1 over the tile's list (wave-uniform triangle: scalar loads).
+__global__ __launch_bounds__(BLOCK) void render_hw1_binned_kernel(Hw1Params P) {
+    const int blocks_x = (P.W + HW1_TILE - 1) / HW1_TILE;
+    const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
+    const int wave = (int)threadIdx.x / 64;
+    const uint32_t lane = lane_id();
+    const int tx = (int)blockIdx.x % blocks_x, ty = ((int)blockIdx.x / blocks_x) * (HW1_TILE / HW1_TH) + wave;
+    const int x = tx * HW1_TW + (int)(lane % HW1_TW);
+    const int y = ty * HW1_TH + (int)(lane / HW1_TW);
+    const bool valid = x < P.W && y < P.H;
+    const bool tile_ok = ty * HW1_TH < P.H;  // wave-uniform
+    const int tidx = ty * tiles_x + tx;
+    const uint32_t cnt = tile_ok ? uni(P.bin_count[tidx]) : 0u;
+    const uint32_t off = tile_ok ? uni(P.bin_offset[tidx]) : 0u;
+    f3 acc = mk(0.f, 0.f, 0.f);
+    for (int s = 0; s < P.spp; ++s) {
+        const float pxs = (float)x + P.jitter[2 * s];
+        const float pys = (float)y + P.jitter[2 * s + 1];
+        const int ix = (int)pxs, iy = (int)pys;  // get_pixel_position(int, int) truncates
+        const f3 pix = add(add(P.p00, scale(P.du, (float)ix)), scale(P.dv, (float)iy));
+        const f3 d = unit(sub(pix, P.center));  // HW1 Ray normalises (ray.h:25)
+        const f3 o = P.center;
+        float best = FLT_MAX;
+        int32_t besti = -1;
+        // Four list entries per round trip: their indices, then their twelve 16-byte records are
+        // all in flight before the first test (the list order does not matter, see above).
+        for (uint32_t i = 0; i < cnt; i += 4) {
+            int kk[4];
+            float4 tq[12];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) kk[j] = i + j < cnt ? (int)ldc_u32(P.bin_list + off + i + j) : -1;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float4* T = P.tri + 3 * (size_t)(kk[j] < 0 ? kk[0] : kk[j]);
+                tq[3 * j] = ldc(T);
+                tq[3 * j + 1] = ldc(T + 1);
+                tq[3 * j + 2] = ldc(T + 2);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float4 a = tq[3 * j], b = tq[3 * j + 1], cq = tq[3 * j + 2];
+                float t, u, v;
+                if (valid && kk[j] >= 0 &&
+                    mt_hw1(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(cq.x, cq.y, cq.z), t, u, v)) {
+                    if (t < best || (t == best && kk[j] < besti)) {  // lexicographic (t, index)
+                        best = t;
+                        besti = kk[j];
+                    }
+                }
+            }
+        }
+        f3 p = mk(0.f, 0.f, 0.f), n = p;
+        const bool hit = besti >= 0;
+        if (hit) {
+            const float4* T = P.tri + 3 * (size_t)besti;
+            const float4 a = T[0], b = T[1], cq = T[2];
+            float t, u, v;
+            mt_hw1(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(cq.x, cq.y, cq.z), t, u, v);
+            p = add(o, scale(d, t));
+            const float4* N = P.nrm + 3 * (size_t)besti;
+            const float wgt = 1.0f - u - v;
+            n = add(add(scale(mk(N[0].x, N[0].y, N[0].z), wgt), scale(mk(N[1].x, N[1].y, N[1].z), u)),
+                    scale(mk(N[2].x, N[2].y, N[2].z), v));
+        }
+        acc = add(acc, shade_hw1(o, d, hit, p, n, P.lpos, P.lcol));
+        if (valid && P.hit_idx) {
+            const size_t kk = ((size_t)y * P.W + x) * (size_t)P.spp + (size_t)s;
+            P.hit_idx[kk] = besti;
+            P.hit_t[kk] = hit ? best : -1.0f;
+        }
+    }
+    if (valid) {
+        const float fs = (float)P.spp;
+        float* out = P.rgb + ((size_t)y * P.W + x) * 3;
+        out[0] = acc.x / fs;
+        out[1] = acc.y / fs;
+        out[2] = acc.z / fs;
     }
 }
 
@@ -1597,6 +1913,14 @@ extern "C" int rt_render_reference(size_t P, int W, int H, const rt_camera* cam,
 extern "C" int rt_render_hw1(int device, const rt_vec3* pos, const rt_vec3* nrm, const uint32_t* idx, size_t P,
                              const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp, const float* jitter,
                              float* rgb_host, int32_t* hit_idx_host, float* hit_t_host) {
+    return rt_render_hw1_ex(device, pos, nrm, idx, P, cam, lpos, lcol, spp, jitter, 0, rgb_host, hit_idx_host,
+                            hit_t_host, nullptr);
+}
+
+extern "C" int rt_render_hw1_ex(int device, const rt_vec3* pos, const rt_vec3* nrm, const uint32_t* idx, size_t P,
+                                const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp, const float* jitter,
+                                int flags, float* rgb_host, int32_t* hit_idx_host, float* hit_t_host,
+                                float* kernel_ms) {
     if (!pos || !nrm || !idx || !cam || !rgb_host || spp < 1 || P == 0)
         return set_error(RT_ERR_ARG, "rt_render_hw1: bad argument (HW1 requires per-vertex normals)");
     if (P > 0x7FFFFFFFull) return set_error(RT_ERR_UNSUPPORTED, "too many triangles");
@@ -1648,10 +1972,51 @@ extern "C" int rt_render_hw1(int device, const rt_vec3* pos, const rt_vec3* nrm,
     hp.rgb = static_cast<float*>(drgb.p);
     hp.hit_idx = static_cast<int32_t*>(dhi.p);
     hp.hit_t = static_cast<float*>(dht.p);
+    const bool brute = (flags & RT_HW1_BRUTE) != 0;
+    DevBuf drect, dbin, dlist;
+    if (!brute && (rc = drect.alloc(P * sizeof(int4))) != RT_OK) return rc;
+    hp.rects = static_cast<const int4*>(drect.p);
+    hp.bin_count = hp.bin_offset = hp.bin_list = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (kernel_ms) {
+        HIP_TRY(hipEventCreate(&e0));
+        HIP_TRY(hipEventCreate(&e1));
+        HIP_TRY(hipEventRecord(e0, nullptr));
+    }
     const int blocks = ((W + 15) / 16) * ((H + 15) / 16);
-    hipLaunchKernelGGL(render_hw1_kernel, dim3(blocks), dim3(BLOCK), 0, nullptr, hp);
+    if (brute) {
+        hipLaunchKernelGGL(render_hw1_kernel, dim3(blocks), dim3(BLOCK), 0, nullptr, hp);
+    } else {
+        const dim3 tgrid(unsigned((P + BLOCK - 1) / BLOCK));
+        const int ntiles = ((W + HW1_TW - 1) / HW1_TW) * ((H + HW1_TH - 1) / HW1_TH);
+        if ((rc = dbin.alloc(size_t(3 * ntiles + 1) * sizeof(uint32_t))) != RT_OK) return rc;
+        uint32_t* counts = static_cast<uint32_t*>(dbin.p);
+        uint32_t* cursor = counts + ntiles;
+        uint32_t* offsets = cursor + ntiles;  // ntiles + 1 entries
+        HIP_TRY(hipMemsetAsync(counts, 0, size_t(2 * ntiles) * sizeof(uint32_t), nullptr));
+        hipLaunchKernelGGL(hw1_rect_kernel, tgrid, dim3(BLOCK), 0, nullptr, hp, static_cast<int4*>(drect.p));
+        hipLaunchKernelGGL(hw1_bin_kernel, tgrid, dim3(BLOCK), 0, nullptr, hp, counts, 0, cursor,
+                           static_cast<uint32_t*>(nullptr));
+        hipLaunchKernelGGL(hw1_scan_kernel, dim3(1), dim3(1024), 0, nullptr, counts, offsets, ntiles);
+        HIP_TRY(hipGetLastError());
+        uint32_t total = 0;
+        HIP_TRY(hipMemcpy(&total, offsets + ntiles, sizeof(total), hipMemcpyDeviceToHost));
+        if ((rc = dlist.alloc(std::max<size_t>(total, 1) * sizeof(uint32_t))) != RT_OK) return rc;
+        hp.bin_count = counts;
+        hp.bin_offset = offsets;
+        hp.bin_list = static_cast<const uint32_t*>(dlist.p);
+        hipLaunchKernelGGL(hw1_bin_kernel, tgrid, dim3(BLOCK), 0, nullptr, hp, counts, 1, cursor,
+                           static_cast<uint32_t*>(dlist.p));
+        hipLaunchKernelGGL(render_hw1_binned_kernel, dim3(blocks), dim3(BLOCK), 0, nullptr, hp);
+    }
     HIP_TRY(hipGetLastError());
+    if (kernel_ms) HIP_TRY(hipEventRecord(e1, nullptr));
     HIP_TRY(hipDeviceSynchronize());
+    if (kernel_ms) {
+        HIP_TRY(hipEventElapsedTime(kernel_ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
     HIP_TRY(hipMemcpy(rgb_host, drgb.p, npx * 3 * sizeof(float), hipMemcpyDeviceToHost));
     if (hit_idx_host) {
         HIP_TRY(hipMemcpy(hit_idx_host, dhi.p, npx * size_t(spp) * sizeof(int32_t), hipMemcpyDeviceToHost));

@@ -64,6 +64,8 @@ def hw1(cfg, threads, reps, cpu_rows):
     args = (mesh.positions, mesh.normals, mesh.indices, cam, c["light_pos"], c["light_color"])
     rgb, hi, _ = rt.render_hw1(*args, spp=spp, aov=True)
     t_gpu = median_time(lambda: rt.render_hw1(*args, spp=spp), reps)
+    k_ms = float(np.median([rt.render_hw1(*args, spp=spp, timing=True)[1] for _ in range(reps)]))
+    kb_ms = float(np.median([rt.render_hw1(*args, spp=spp, timing=True, brute=True)[1] for _ in range(reps)]))
     oc = orc.camera_from_basis(*(cam.basis()[k] for k in ("center", "pixel00_loc", "pixel_delta_u",
                                                           "pixel_delta_v")), W, H)
     rows = (0, H) if cpu_rows is None else (H // 2 - cpu_rows // 2, H // 2 + cpu_rows // 2)
@@ -79,6 +81,9 @@ def hw1(cfg, threads, reps, cpu_rows):
     return {"config": cfg, "gpus": 1, "Mrays_s": samples / t_gpu / 1e6, "total_rays_s": samples / t_gpu,
             "timing": "synchronous rt_render_hw1 call (mesh upload + kernel + read-back), median",
             "ms": t_gpu * 1e3, "cpu_Mrays_s": {str(k): v for k, v in cpu.items()},
+            "device_Mrays_s": samples / k_ms / 1e3, "device_ms": k_ms,
+            "device_timing": "HIP events around the binned pipeline (rect, bin, scan, fill, render kernels)",
+            "brute_device_Mrays_s": samples / kb_ms / 1e3, "brute_device_ms": kb_ms,
             "cpu_sample": f"oracle HW1 restatement rows {rows[0]}..{rows[1]}",
             "hit_idx_mismatches": int((hi.reshape(-1) != gold(name, "hits.i32.gz", np.int32)).sum()),
             "rgb_maxabs": float(np.abs(rgb.reshape(-1) - gold(name, "fb.f32.gz", np.float32)).max()),

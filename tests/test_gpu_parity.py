@@ -228,14 +228,16 @@ def test_device_intersect_g_against_oracle():
 HW1_CASES = {"c1_full": ("c1", 256, 256), "c2_small": ("c2", 160, 120), "c2_full": ("c2", 640, 480)}
 
 
+@pytest.mark.parametrize("brute", [False, True])
 @pytest.mark.parametrize("name", list(HW1_CASES))
-def test_hw1_brute_force_parity(name):
+def test_hw1_brute_force_parity(name, brute):
+    """HW1 path against the reference's own outputs, binned (default) and brute force."""
     cfg, W, H = HW1_CASES[name]
     c = configs.HW1_CONFIGS[cfg]
     mesh = rt.MeshHW1(configs.MESHES / c["mesh"])
     cam = rt.Camera(c["position"], c["look_at"], c["up"], c["focal_mm"], c["sensor_mm"], W, H, hw1=True)
     rgb, hi, ht = rt.render_hw1(mesh.positions, mesh.normals, mesh.indices, cam, c["light_pos"], c["light_color"],
-                                spp=c["spp"], aov=True)
+                                spp=c["spp"], aov=True, brute=brute)
     assert np.array_equal(hi.reshape(-1), golden_array(name, "hits.i32.gz", np.int32))
     assert np.array_equal(ht.reshape(-1).view(np.uint32), golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
     _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
@@ -245,6 +247,54 @@ def test_hw1_brute_force_parity(name):
         n = len(f"P6\n{W} {H}\n255\n")
         d = np.abs(np.frombuffer(mine[n:], np.uint8).astype(int) - np.frombuffer(ppm[n:], np.uint8).astype(int))
         assert d.max() <= 1
+
+
+def _soup(rng, n, kind):
+    """Adversarial triangle soups for the binned HW1 path: mixed sizes and orientations, edge-on
+    triangles whose plane passes (nearly) through the camera, triangles straddling the camera
+    plane or behind it, slivers and huge triangles."""
+    cam_pos = np.array([0.3, -2.0, 0.7], np.float32)
+    if kind == "mixed":
+        c = rng.normal(size=(n, 1, 3)) * np.array([1.0, 1.0, 0.6])
+        size = np.exp(rng.uniform(np.log(1e-3), np.log(2.0), size=(n, 1, 1)))
+        v = c + rng.normal(size=(n, 3, 3)) * size
+    elif kind == "edge_on":
+        # planes through (or 1e-7 .. 1e-3 off) the camera centre
+        a = rng.normal(size=(n, 1, 3)) * 1.5
+        b = rng.normal(size=(n, 1, 3)) * 1.5
+        s, t = rng.uniform(0.2, 1.5, size=(n, 3, 1)), rng.uniform(-0.5, 0.5, size=(n, 3, 1))
+        v = cam_pos + s * a + t * b
+        off = np.where(rng.uniform(size=(n, 1, 1)) < 0.5, 0.0, 10 ** rng.uniform(-7, -3, size=(n, 1, 1)))
+        v = v + off * rng.normal(size=(n, 1, 3))
+    elif kind == "around":
+        # large triangles around / behind / through the camera
+        v = cam_pos + rng.normal(size=(n, 3, 3)) * 3.0
+    else:  # slivers
+        p0 = rng.normal(size=(n, 1, 3))
+        dirn = rng.normal(size=(n, 1, 3))
+        v = np.concatenate([p0, p0 + dirn, p0 + dirn * rng.uniform(0.3, 0.7, size=(n, 1, 1))
+                            + 1e-5 * rng.normal(size=(n, 1, 3))], axis=1)
+    pos = v.reshape(-1, 3).astype(np.float32)
+    nrm = rng.normal(size=pos.shape).astype(np.float32)
+    idx = np.arange(len(pos), dtype=np.uint32)
+    return pos, nrm, idx, cam_pos
+
+
+@pytest.mark.parametrize("kind", ["mixed", "edge_on", "around", "slivers"])
+@pytest.mark.parametrize("spp", [1, 4])
+def test_hw1_binned_equals_brute_force_fuzz(kind, spp):
+    """The binned HW1 kernel skips triangles by a conservative pixel rectangle: it must return
+    the brute-force loop's winner (first index with the smallest t) bit for bit."""
+    rng = np.random.default_rng({"mixed": 1, "edge_on": 2, "around": 3, "slivers": 4}[kind] * 10 + spp)
+    pos, nrm, idx, cam_pos = _soup(rng, 3000, kind)
+    cam = rt.Camera(tuple(cam_pos), (0.0, 0.0, 0.2), (0.0, 0.0, 1.0), 30.0, 24.0, 96, 72, hw1=True)
+    args = (pos, nrm, idx, cam, (-3.0, 0.0, 1.0), (1.0, 0.0, 1.0))
+    a_rgb, a_hi, a_ht = rt.render_hw1(*args, spp=spp, aov=True)
+    b_rgb, b_hi, b_ht = rt.render_hw1(*args, spp=spp, aov=True, brute=True)
+    assert (b_hi >= 0).mean() > {"mixed": 0.05, "around": 0.05, "edge_on": 5e-4, "slivers": 5e-4}[kind]
+    assert np.array_equal(a_hi, b_hi)
+    assert np.array_equal(a_ht.view(np.uint32), b_ht.view(np.uint32))
+    assert np.array_equal(a_rgb.view(np.uint32), b_rgb.view(np.uint32))
 
 
 def test_hw1_multisample_against_oracle():

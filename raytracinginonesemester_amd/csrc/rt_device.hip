@@ -33,6 +33,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <functional>
 #include <memory>
 #include <new>
 #include <string>
@@ -79,6 +80,8 @@ struct SceneView {
     float root_box[6];
     float bmax[3];  // per axis max |coordinate| over every AABB of the scene (make_ray)
     int32_t wide;
+    const float* __restrict__ cut;  // tile culling: boxes of a cut of the tree (6 floats each)
+    int32_t ncut;
 };
 
 __device__ __forceinline__ f3 scene_bmax(const SceneView& sc) { return mk(sc.bmax[0], sc.bmax[1], sc.bmax[2]); }
@@ -98,6 +101,8 @@ struct RenderParams {
     f3 miss_pixel;                                    // pixel value when all spp samples miss
     uint32_t* live_count;                             // [k * COUNTER_STRIDE], tile_cull_kernel
     int32_t* live_tiles;                              // nqueues lists of queue_cap entries
+    int32_t* cand_tiles;  // tiles the root test keeps, for tile_cut_kernel (counter: live_count[8 * stride])
+    int32_t cut_force;    // test every candidate in tile_cut_kernel (no pass-through)
     int32_t nqueues;
     int32_t queue_cap;
     int32_t tiles_per_block;                          // virtual blocks per render block
@@ -165,6 +170,13 @@ __device__ __forceinline__ uint4 ldc_u(const float4* p) {
 #endif
 }
 
+__device__ __forceinline__ uint32_t ldc_u32(const uint32_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *(const __attribute__((address_space(4))) uint32_t*)p;
+#else
+    return *p;
+#endif
+}
 __device__ __forceinline__ v2f lo2(float4 q) { return (v2f){q.x, q.y}; }
 __device__ __forceinline__ v2f hi2(float4 q) { return (v2f){q.z, q.w}; }
 
@@ -683,62 +695,157 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
 }
 
 // ---- tile culling ---------------------------------------------------------------------
-// True only if every camera ray of pixels [x0,x1] x rows [y0,y1] provably fails the root
-// test of SearchBVH (intersectAABB(ray, root box, 1e-4, FLT_MAX), bvh.h:81-129), so the whole
-// tile's samples are misses.  Ray directions are positive multiples of
-// D(px,py) = pixel00 + px*du + py*dv - center with px in [x0-0.5, x1+0.5) (jitter), an affine
-// map: its per-component range over the (1-pixel-padded) tile comes from the corners, widened
-// by 1e-5*|D| plus 8 float ulps of every term to cover the float rounding of the per-sample
-// computation (pixel position, difference, cam_unit).  Scaling d by k > 0 scales every slab
-// parameter by 1/k, so "some axis's entry > another axis's exit" is scale-free.  An axis whose
-// component can come near 0 (|d_a| < 1e-6 |d|, far above the 1e-8 parallel threshold) is
-// ignored (no constraint): conservative.  Culled iff, with 1e-9 relative slack (the
-// reference's doubles carry ~1e-15), some axis's smallest entry exceeds some axis's largest
-// exit, or some axis's largest exit is < 0 (< tmin).  The camera inside the padded box never
-// culls.
-__device__ __forceinline__ bool tile_misses_root(const RenderParams& P, int x0, int x1, int y0, int y1) {
-    const double c[3] = {P.cam_center.x, P.cam_center.y, P.cam_center.z};
+// A tile is culled only if every camera ray of pixels [x0,x1] x rows [y0,y1] provably fails
+// intersectAABB(ray, B, 1e-4, FLT_MAX) (bvh.h:81-129) for every box B of a cut of the tree (a
+// set of nodes holding every leaf exactly once: the root alone, or the cut the scene keeps in
+// sc.cut).  SearchBVH only tests a triangle after its ancestors' box tests passed, with tmax =
+// bestT <= FLT_MAX (a smaller tmax only fails more), so such a ray tests no triangle: a miss.
+// Ray directions are positive multiples of D(px,py) = pixel00 + px*du + py*dv - center with
+// px in [x0-0.5, x1+0.5) (jitter), an affine map: its per-component range over the
+// (1-pixel-padded) tile comes from the corners, widened by 1e-5*|D| plus 8 float ulps of every
+// term to cover the float rounding of the per-sample computation (pixel position, difference,
+// cam_unit).  Scaling d by k > 0 scales every slab parameter by 1/k, so "some axis's entry >
+// another axis's exit" is scale-free.  An axis whose component can come near 0
+// (|d_a| < 1e-6 |d|, far above the 1e-8 parallel threshold) is ignored (no constraint):
+// conservative.  A box is missed iff, with 1e-9 relative slack (the reference's doubles carry
+// ~1e-15; the reciprocals below add ~1e-16), some axis's smallest entry exceeds some axis's
+// largest exit, or some axis's largest exit is < 0 (< tmin).  The camera inside a padded box
+// never culls.
+struct TileDirs {
+    double c[3], Dl[3], Dh[3], iDl[3], iDh[3], scale;
+    bool usable;
+};
+__device__ __forceinline__ TileDirs tile_dirs(const RenderParams& P, int x0, int x1, int y0, int y1) {
+    TileDirs T;
     const double p0[3] = {P.cam_p00.x, P.cam_p00.y, P.cam_p00.z};
     const double du[3] = {P.cam_du.x, P.cam_du.y, P.cam_du.z};
     const double dv[3] = {P.cam_dv.x, P.cam_dv.y, P.cam_dv.z};
+    T.c[0] = P.cam_center.x;
+    T.c[1] = P.cam_center.y;
+    T.c[2] = P.cam_center.z;
     const double pxl = x0 - 1.0, pxh = x1 + 1.0, pyl = y0 - 1.0, pyh = y1 + 1.0;
     const double pxm = fmax(fabs(pxl), fabs(pxh)), pym = fmax(fabs(pyl), fabs(pyh));
-    double Dl[3], Dh[3], scale = 0.0;
+    T.scale = 0.0;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const double base = p0[a] - c[a];
+        const double base = p0[a] - T.c[a];
         const double u0 = pxl * du[a], u1 = pxh * du[a], v0 = pyl * dv[a], v1 = pyh * dv[a];
-        const double ulp = 8.0 * 1.1920928955078125e-7 * (fabs(c[a]) + fabs(p0[a]) + pxm * fabs(du[a]) + pym * fabs(dv[a]));
-        Dl[a] = base + fmin(u0, u1) + fmin(v0, v1) - ulp;
-        Dh[a] = base + fmax(u0, u1) + fmax(v0, v1) + ulp;
-        scale = fmax(scale, fmax(fabs(Dl[a]), fabs(Dh[a])));
+        const double ulp = 8.0 * 1.1920928955078125e-7 * (fabs(T.c[a]) + fabs(p0[a]) + pxm * fabs(du[a]) + pym * fabs(dv[a]));
+        T.Dl[a] = base + fmin(u0, u1) + fmin(v0, v1) - ulp;
+        T.Dh[a] = base + fmax(u0, u1) + fmax(v0, v1) + ulp;
+        T.scale = fmax(T.scale, fmax(fabs(T.Dl[a]), fabs(T.Dh[a])));
     }
-    const float* rb = P.sc.root_box;
-    const double mn[3] = {rb[0], rb[1], rb[2]}, mx[3] = {rb[3], rb[4], rb[5]};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        T.Dl[a] -= 1e-5 * T.scale;
+        T.Dh[a] += 1e-5 * T.scale;
+        T.iDl[a] = 1.0 / T.Dl[a];
+        T.iDh[a] = 1.0 / T.Dh[a];
+    }
+    T.usable = T.scale > 0.0;
+    return T;
+}
+
+__device__ __forceinline__ bool tile_misses_box(const TileDirs& T, const float* bx) {
+    const double mn[3] = {bx[0], bx[1], bx[2]}, mx[3] = {bx[3], bx[4], bx[5]};
     bool inside = true;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        Dl[a] -= 1e-5 * scale;
-        Dh[a] += 1e-5 * scale;
-        const double tol = 1e-6 * (fabs(mn[a]) + fabs(mx[a]) + fabs(c[a])) + 1e-30;
-        inside = inside && c[a] >= mn[a] - tol && c[a] <= mx[a] + tol;
+        const double tol = 1e-6 * (fabs(mn[a]) + fabs(mx[a]) + fabs(T.c[a])) + 1e-30;
+        inside = inside && T.c[a] >= mn[a] - tol && T.c[a] <= mx[a] + tol;
     }
-    if (inside || !(scale > 0.0) || !(mn[0] <= mx[0] && mn[1] <= mx[1] && mn[2] <= mx[2])) return false;
+    if (inside || !T.usable || !(mn[0] <= mx[0] && mn[1] <= mx[1] && mn[2] <= mx[2])) return false;
     double entry_min = -INFINITY, exit_max = INFINITY;  // max over axes of min entry; min of max exit
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        if (!(Dl[a] > 1e-6 * scale || Dh[a] < -1e-6 * scale)) continue;  // may be ~parallel
-        const double nA = mn[a] - c[a], xA = mx[a] - c[a];
+        if (!(T.Dl[a] > 1e-6 * T.scale || T.Dh[a] < -1e-6 * T.scale)) continue;  // may be ~parallel
+        const double nA = mn[a] - T.c[a], xA = mx[a] - T.c[a];
         // d > 0: entry (mn-c)/d, exit (mx-c)/d; d < 0: swapped.  Over d in [Dl, Dh] each
         // quotient is monotone in d, so its range sits at the endpoints.
-        const double e0 = (Dl[a] > 0 ? nA : xA) / Dl[a], e1 = (Dl[a] > 0 ? nA : xA) / Dh[a];
-        const double f0 = (Dl[a] > 0 ? xA : nA) / Dl[a], f1 = (Dl[a] > 0 ? xA : nA) / Dh[a];
+        const double ne = T.Dl[a] > 0 ? nA : xA, nx = T.Dl[a] > 0 ? xA : nA;
+        const double e0 = ne * T.iDl[a], e1 = ne * T.iDh[a];
+        const double f0 = nx * T.iDl[a], f1 = nx * T.iDh[a];
         entry_min = fmax(entry_min, fmin(e0, e1));
         exit_max = fmin(exit_max, fmax(f0, f1));
     }
     if (!(exit_max == exit_max) || !(entry_min == entry_min)) return false;
     if (exit_max < -1e-9 * fabs(exit_max) - 1e-30) return true;
     return entry_min - exit_max > 1e-9 * (fabs(entry_min) + fabs(exit_max)) + 1e-30;
+}
+
+// Float form of tile_dirs / tile_misses_box for tile_cut_kernel (a wave-uniform computation
+// per tile, made 64 times more often than the root test).  Every bound carries its own float
+// rounding on top of the double version's margins: the tile corners are padded by twice the
+// per-sample ulp term (the corner sums are themselves float), and the miss decisions keep a
+// 1e-4 relative slack (the float entry/exit bounds are within ~5 float ulps of the exact
+// quotients), so a culled tile is still one whose every ray fails the reference's double test.
+struct TileDirsF {
+    float c[3], Dl[3], Dh[3], iDl[3], iDh[3], scale;
+    bool usable;
+};
+__device__ __forceinline__ TileDirsF tile_dirs_f(const RenderParams& P, int x0, int x1, int y0, int y1) {
+    TileDirsF T;
+    const float p0[3] = {P.cam_p00.x, P.cam_p00.y, P.cam_p00.z};
+    const float du[3] = {P.cam_du.x, P.cam_du.y, P.cam_du.z};
+    const float dv[3] = {P.cam_dv.x, P.cam_dv.y, P.cam_dv.z};
+    T.c[0] = P.cam_center.x;
+    T.c[1] = P.cam_center.y;
+    T.c[2] = P.cam_center.z;
+    const float pxl = (float)x0 - 1.0f, pxh = (float)x1 + 1.0f, pyl = (float)y0 - 1.0f, pyh = (float)y1 + 1.0f;
+    const float pxm = fmaxf(fabsf(pxl), fabsf(pxh)), pym = fmaxf(fabsf(pyl), fabsf(pyh));
+    T.scale = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float base = p0[a] - T.c[a];
+        const float u0 = pxl * du[a], u1 = pxh * du[a], v0 = pyl * dv[a], v1 = pyh * dv[a];
+        const float ulp = 16.0f * 1.1920928955078125e-7f * (fabsf(T.c[a]) + fabsf(p0[a]) + pxm * fabsf(du[a]) + pym * fabsf(dv[a]));
+        T.Dl[a] = base + fminf(u0, u1) + fminf(v0, v1) - ulp;
+        T.Dh[a] = base + fmaxf(u0, u1) + fmaxf(v0, v1) + ulp;
+        T.scale = fmaxf(T.scale, fmaxf(fabsf(T.Dl[a]), fabsf(T.Dh[a])));
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        T.Dl[a] -= 1.1e-5f * T.scale;
+        T.Dh[a] += 1.1e-5f * T.scale;
+        T.iDl[a] = 1.0f / T.Dl[a];
+        T.iDh[a] = 1.0f / T.Dh[a];
+    }
+    T.usable = T.scale > 0.0f && T.scale < 1e30f;
+    return T;
+}
+
+__device__ __forceinline__ bool tile_misses_box_f(const TileDirsF& T, const float* bx) {
+    const float mn[3] = {bx[0], bx[1], bx[2]}, mx[3] = {bx[3], bx[4], bx[5]};
+    bool inside = true;
+    float mag = 0.0f, imax = 0.0f;  // magnitude of the subtraction operands, largest |1/D|
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float tol = 1e-4f * (fabsf(mn[a]) + fabsf(mx[a]) + fabsf(T.c[a])) + 1e-30f;
+        inside = inside && T.c[a] >= mn[a] - tol && T.c[a] <= mx[a] + tol;
+        mag = fmaxf(mag, fabsf(mn[a]) + fabsf(mx[a]) + fabsf(T.c[a]));
+    }
+    if (inside || !T.usable || !(mn[0] <= mx[0] && mn[1] <= mx[1] && mn[2] <= mx[2]) || !(mag < 1e30f)) return false;
+    float entry_min = -INFINITY, exit_max = INFINITY;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (!(T.Dl[a] > 1e-6f * T.scale || T.Dh[a] < -1e-6f * T.scale)) continue;  // may be ~parallel
+        imax = fmaxf(imax, fmaxf(fabsf(T.iDl[a]), fabsf(T.iDh[a])));
+        const float nA = mn[a] - T.c[a], xA = mx[a] - T.c[a];
+        const float ne = T.Dl[a] > 0.0f ? nA : xA, nx = T.Dl[a] > 0.0f ? xA : nA;
+        const float e0 = ne * T.iDl[a], e1 = ne * T.iDh[a];
+        const float f0 = nx * T.iDl[a], f1 = nx * T.iDh[a];
+        entry_min = fmaxf(entry_min, fminf(e0, e1));
+        exit_max = fminf(exit_max, fmaxf(f0, f1));
+    }
+    if (!(exit_max == exit_max) || !(entry_min == entry_min)) return false;
+    const float abs_slack = 1e-4f * mag * imax + 1e-30f;
+    if (!(abs_slack < 1e30f)) return false;
+    if (exit_max < -1e-4f * fabsf(exit_max) - abs_slack) return true;
+    return entry_min - exit_max > 1e-4f * (fabsf(entry_min) + fabsf(exit_max)) + abs_slack;
+}
+
+__device__ __forceinline__ bool tile_misses_root(const RenderParams& P, int x0, int x1, int y0, int y1) {
+    return tile_misses_box(tile_dirs(P, x0, x1, y0, y1), P.sc.root_box);
 }
 
 // What a sample that misses the root returns: clamp(0 + (1,1,1) * missColor) (query.h:181-183),
@@ -773,34 +880,32 @@ __device__ __forceinline__ int queue_of_tile(const RenderParams& P, int tile) {
     return (tile / P.tiles_x) & 7;
 }
 
-__global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
-    const int tile = (int)(blockIdx.x * BLOCK + threadIdx.x);
-    bool live = false;
-    if (tile < P.tiles_total) {
-        const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-        const int xa = tx * P.tile_w, ra = ty * P.tile_h;
-        const int xb = min(xa + P.tile_w, P.W) - 1, rb = min(ra + P.tile_h, P.rows) - 1;
-        const bool culled = P.cull && tile_misses_root(P, xa, xb, global_row(P, ra), global_row(P, rb));
-        if (culled) {
-            for (int r = ra; r <= rb; ++r)
-                for (int x = xa; x <= xb; ++x) {
-                    float* o = P.rgb + ((size_t)r * P.W + x) * 3;
-                    o[0] = P.miss_pixel.x;
-                    o[1] = P.miss_pixel.y;
-                    o[2] = P.miss_pixel.z;
-                    if (P.hit_idx) {
-                        const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp;
-                        for (int s = 0; s < P.spp; ++s) {
-                            P.hit_idx[k + s] = -1;
-                            P.hit_t[k + s] = -1.0f;
-                        }
-                    }
-                }
-        } else {
-            live = true;
+// Miss pixels (and hit AOV -1) of a culled tile, written by the lanes of `lanes` threads
+// starting at `first` (one lane per tile in tile_cull_kernel, a whole wave in tile_cut_kernel).
+__device__ __forceinline__ void write_culled_tile(const RenderParams& P, int tile, int first, int lanes) {
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    const int xa = tx * P.tile_w, ra = ty * P.tile_h;
+    const int tw = min(xa + P.tile_w, P.W) - xa, th = min(ra + P.tile_h, P.rows) - ra;
+    const float mp[3] = {P.miss_pixel.x, P.miss_pixel.y, P.miss_pixel.z};
+    for (int i = first; i < tw * th * 3; i += lanes) {
+        const int px = i / 3, c = i - 3 * px;
+        const int r = ra + px / tw, x = xa + px % tw;
+        P.rgb[((size_t)r * P.W + x) * 3 + c] = mp[c];
+    }
+    if (P.hit_idx) {
+        for (int i = first; i < tw * th * P.spp; i += lanes) {
+            const int px = i / P.spp, smp = i - P.spp * px;
+            const int r = ra + px / tw, x = xa + px % tw;
+            const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp + smp;
+            P.hit_idx[k] = -1;
+            P.hit_t[k] = -1.0f;
         }
     }
-    // Wave-aggregated append: one atomic per (wave, list).
+}
+
+// Wave-aggregated append of the lanes with `live` to the live list of their tile: one atomic
+// per (wave, list).
+__device__ __forceinline__ void append_live(const RenderParams& P, bool live, int tile) {
     const int q = live ? queue_of_tile(P, tile) : 0;
     const uint32_t lane = lane_id();
     uint64_t pending = ballot(live);
@@ -817,6 +922,70 @@ __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
     }
 }
 
+// Pass 1, one lane per tile: the root test.  Without a cut (sc.ncut == 0) the survivors go
+// straight to the live lists; with one they go to the candidate list for pass 2.
+__global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
+    const int tile = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    bool live = false;
+    if (tile < P.tiles_total) {
+        const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        const int xa = tx * P.tile_w, ra = ty * P.tile_h;
+        const int xb = min(xa + P.tile_w, P.W) - 1, rb = min(ra + P.tile_h, P.rows) - 1;
+        const bool culled = P.cull && tile_misses_root(P, xa, xb, global_row(P, ra), global_row(P, rb));
+        if (culled) write_culled_tile(P, tile, 0, 1);
+        else live = true;
+    }
+    if (P.cull && P.sc.ncut > 0) {
+        const uint32_t lane = lane_id();
+        const uint64_t m = ballot(live);
+        if (m == 0) return;
+        uint32_t base = 0;
+        if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(&P.live_count[8 * COUNTER_STRIDE], (uint32_t)__popcll(m));
+        base = rdlane(base, (uint32_t)__builtin_ctzll(m));
+        if (live) P.cand_tiles[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = tile;
+        return;
+    }
+    append_live(P, live, tile);
+}
+
+// Pass 2, one wave per group of CUT_GROUP candidate tiles (in list order), one lane per box of the
+// cut (sc.cut, <= 64 boxes that hold every leaf exactly once): a tile is culled when every
+// lane proves its box missed by every ray of the tile (tile_misses_box_f), else it stays live.
+// The tile bounds are the same for every lane (a wave-uniform computation).  The group's live
+// tiles are appended together (lane j holds tile j): one atomic per (group, list).
+#ifndef RT_CUT_GROUP
+#define RT_CUT_GROUP 8
+#endif
+constexpr int CUT_GROUP = RT_CUT_GROUP;
+__global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
+    const uint32_t lane = lane_id();
+    const int waves = (int)(gridDim.x * (BLOCK / 64));
+    const int n = (int)ldc_u32(&P.live_count[8 * COUNTER_STRIDE]);
+    // When the root box already covers more than a quarter of the image the scene fills the
+    // view and the cut rarely removes a tile (c5's heightfield: none of 739,248), so the
+    // candidates pass through untested (a speed choice only: passing is always exact).
+    const bool test = P.cut_force || 4 * (int64_t)n <= (int64_t)P.tiles_total;
+    // One group per wave, in dispatch order (the grid covers every possible candidate; waves
+    // past the list leave): the live lists keep the candidates' near-raster order, which the
+    // render kernel's L2 reuse depends on (a grid-stride loop here scrambles it: c5 +5 %).
+    for (int g = (int)(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64); CUT_GROUP * g < n; g += waves) {
+        const int m = min(CUT_GROUP, n - CUT_GROUP * g);
+        const int my_tile = (int)lane < m ? P.cand_tiles[CUT_GROUP * g + (int)lane] : -1;
+        uint64_t live = test ? 0ull : (m >= 64 ? ~0ull : (1ull << m) - 1ull);  // lanes >= m hold no tile
+        for (int j = 0; test && j < m; ++j) {
+            const int tile = (int)rdlane((uint32_t)my_tile, (uint32_t)j);
+            const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+            const int xa = tx * P.tile_w, ra = ty * P.tile_h;
+            const int xb = min(xa + P.tile_w, P.W) - 1, rb = min(ra + P.tile_h, P.rows) - 1;
+            const TileDirsF T = tile_dirs_f(P, xa, xb, global_row(P, ra), global_row(P, rb));
+            const bool hit = (int)lane < P.sc.ncut && !tile_misses_box_f(T, P.sc.cut + 6 * (size_t)lane);
+            if (ballot(hit) == 0) write_culled_tile(P, tile, (int)lane, 64);
+            else live |= 1ull << j;
+        }
+        append_live(P, ((live >> lane) & 1ull) != 0, my_tile);
+    }
+}
+
 // Virtual block -> live tile, without atomics.  With 8 lists there are tiles_virtual =
 // 8 * tiles_x * ceil(tiles_y / 8) virtual blocks, at least 8 times the longest list (RT_TILES_ROWS
 // puts at most tiles_x * ceil(tiles_y / 8) tiles in a list, RT_TILES_XCD_CHUNK at most
@@ -826,13 +995,6 @@ __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
 // With one list (RT_TILES_LINEAR) virtual block j takes slot j.  The list lengths are read once
 // per block: the lists are immutable while the render kernel runs, so they and their entries
 // are read through the constant address space (scalar loads).
-__device__ __forceinline__ uint32_t ldc_u32(const uint32_t* p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return *(const __attribute__((address_space(4))) uint32_t*)p;
-#else
-    return *p;
-#endif
-}
 
 __device__ __forceinline__ int list_length(const RenderParams& P, int q) {
     return (int)ldc_u32(&P.live_count[q * COUNTER_STRIDE]);
@@ -1126,7 +1288,7 @@ __global__ __launch_bounds__(BLOCK) void hw1_rect_kernel(Hw1Params P, int4* __re
     w[1] = -(Ev + tiny);
     w[2] = -(4 * uu * dmax + Eu + Ev + Ed + tiny);
     w[3] = (double)FLT_EPSILON - Ed;
-    // D over the image, per axis, padded as in tile_misses_root
+    // D over the image, per axis, padded as in tile_dirs
     const double cc[3] = {P.center.x, P.center.y, P.center.z}, p0[3] = {P.p00.x, P.p00.y, P.p00.z},
                  du[3] = {P.du.x, P.du.y, P.du.z}, dv[3] = {P.dv.x, P.dv.y, P.dv.z};
     const double xm = fmax(fabs((double)X0), fabs((double)X1)), ym = fmax(fabs((double)Y0), fabs((double)Y1));
@@ -1401,6 +1563,8 @@ struct rt_scene {
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     float bmax[3] = {0, 0, 0};
     DevBuf inode, wnode, ibox, leaf, tnorm, objids, mats, lights, jitter;
+    DevBuf cut;  // tile culling: boxes of a cut of the tree (6 floats each)
+    int ncut = 0;
     bool wide = false;
     DevBuf work;  // live tile list counters + the lists
     int64_t last_tiles_total = 0;
@@ -1616,6 +1780,46 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
         s->root_box[0] = s->root_box[1] = s->root_box[2] = INFINITY;
         s->root_box[3] = s->root_box[4] = s->root_box[5] = -INFINITY;
     }
+    // Tile-culling cut (tile_misses_scene): from the root, repeatedly replace the internal node
+    // with the largest box (half surface area) by its children, up to kCut nodes.  Every leaf
+    // keeps exactly one ancestor-or-self in the set; a missing child (NO_REF) holds no leaf.
+    if (cid[0] != NO_REF && !(cid[0] & LEAF_BIT)) {
+        int kcut = 64;  // one box per lane of tile_cut_kernel
+        if (const char* e = std::getenv("RT_CULL_BOXES")) kcut = std::min(64, std::max(0, std::atoi(e)));
+        auto area = [&](uint32_t n) {
+            const rt_aabb& bb = aabbs[n];
+            const double dx = double(bb.max_corner.x) - bb.min_corner.x, dy = double(bb.max_corner.y) - bb.min_corner.y,
+                         dz = double(bb.max_corner.z) - bb.min_corner.z;
+            const double a = dx * dy + dy * dz + dz * dx;
+            return a == a ? a : INFINITY;
+        };
+        std::vector<uint32_t> cutn{0u};
+        while (int(cutn.size()) < kcut) {
+            int best = -1;
+            double ba = -1.0;
+            for (int i = 0; i < int(cutn.size()); ++i) {
+                if (cid[cutn[i]] & LEAF_BIT) continue;
+                const double a = area(cutn[i]);
+                if (a > ba) { ba = a; best = i; }
+            }
+            if (best < 0) break;
+            const rt_bvh_node& nd = nodes[cutn[best]];
+            cutn.erase(cutn.begin() + best);
+            if (nd.left_idx != NO_REF && cid[nd.left_idx] != NO_REF) cutn.push_back(nd.left_idx);
+            if (nd.right_idx != NO_REF && cid[nd.right_idx] != NO_REF) cutn.push_back(nd.right_idx);
+        }
+        if (kcut > 1) {
+            std::vector<float> hc(6 * cutn.size());
+            for (size_t i = 0; i < cutn.size(); ++i) {
+                const rt_aabb& bb = aabbs[cutn[i]];
+                const float v6[6] = {bb.min_corner.x, bb.min_corner.y, bb.min_corner.z,
+                                     bb.max_corner.x, bb.max_corner.y, bb.max_corner.z};
+                std::memcpy(&hc[6 * i], v6, sizeof(v6));
+            }
+            if ((rc = s->cut.upload(hc.data(), hc.size() * sizeof(float))) != RT_OK) return rc;
+            s->ncut = int(cutn.size());
+        }
+    }
     if ((rc = s->inode.upload(hin.data(), hin.size() * sizeof(float4))) != RT_OK) return rc;
     if (wide_ok && (rc = s->wnode.upload(hwn.data(), hwn.size() * sizeof(float4))) != RT_OK) return rc;
     s->wide = wide_ok && !(s->root_ref & LEAF_BIT);
@@ -1715,6 +1919,39 @@ f3 miss_pixel_value(const rt_render_opts* o) {
 
 }  // namespace
 
+namespace {
+// Fraction of the image covered by the bounding rectangle of the root box's projected corners
+// (1 when a corner is not in front of the camera).  The tree-cut culling pass (tile_cut_kernel)
+// is launched only when this is small: a scene that fills the view gains no culled tiles from
+// it and pays for the pass (a speed choice; culling or not gives the same image).
+double root_box_coverage(const float* rb, const rt_camera* cam) {
+    const double c[3] = {cam->center.x, cam->center.y, cam->center.z};
+    const double b0[3] = {cam->pixel00_loc.x - c[0], cam->pixel00_loc.y - c[1], cam->pixel00_loc.z - c[2]};
+    const double du[3] = {cam->pixel_delta_u.x, cam->pixel_delta_u.y, cam->pixel_delta_u.z};
+    const double dv[3] = {cam->pixel_delta_v.x, cam->pixel_delta_v.y, cam->pixel_delta_v.z};
+    // solve s*b0 + a*du + b*dv = corner - c (Cramer); pixel = (a/s, b/s)
+    auto det3 = [](const double* x, const double* y, const double* z) {
+        return x[0] * (y[1] * z[2] - y[2] * z[1]) - y[0] * (x[1] * z[2] - x[2] * z[1]) + z[0] * (x[1] * y[2] - x[2] * y[1]);
+    };
+    const double D = det3(b0, du, dv);
+    if (!(std::fabs(D) > 0.0) || !(rb[0] <= rb[3] && rb[1] <= rb[4] && rb[2] <= rb[5])) return 1.0;
+    double x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+    for (int k = 0; k < 8; ++k) {
+        const double p[3] = {double(rb[(k & 1) ? 3 : 0]) - c[0], double(rb[(k & 2) ? 4 : 1]) - c[1],
+                             double(rb[(k & 4) ? 5 : 2]) - c[2]};
+        const double sx = det3(p, du, dv) / D, a = det3(b0, p, dv) / D, b = det3(b0, du, p) / D;
+        if (!(sx > 0.0)) return 1.0;
+        x0 = std::min(x0, a / sx);
+        x1 = std::max(x1, a / sx);
+        y0 = std::min(y0, b / sx);
+        y1 = std::max(y1, b / sx);
+    }
+    const double W = cam->pixel_width, H = cam->pixel_height;
+    const double w = std::max(0.0, std::min(W, x1) - std::max(0.0, x0)), h = std::max(0.0, std::min(H, y1) - std::max(0.0, y0));
+    return w * h / (W * H);
+}
+}  // namespace
+
 extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, float* rgb,
                                 int32_t* hit_idx, float* hit_t, void* stream) {
     if (!s || !cam || !o || !rgb) return set_error(RT_ERR_ARG, "rt_render_device: null argument");
@@ -1745,6 +1982,11 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     P.sc.num_lights = s->nlights;
     P.sc.root_ref = s->root_ref;
     std::memcpy(P.sc.root_box, s->root_box, sizeof(P.sc.root_box));
+    P.sc.cut = static_cast<const float*>(s->cut.p);
+    double max_cov = 0.3;  // RT_CULL_COVERAGE: tests force the cut pass on (>= 1: always, untested candidates none)
+    if (const char* e = std::getenv("RT_CULL_COVERAGE")) max_cov = std::atof(e);
+    P.sc.ncut = s->ncut > 0 && root_box_coverage(s->root_box, cam) <= max_cov ? s->ncut : 0;
+    P.cut_force = max_cov >= 1.0 ? 1 : 0;
     std::memcpy(P.sc.bmax, s->bmax, sizeof(P.sc.bmax));
     P.cam_center = f3{cam->center.x, cam->center.y, cam->center.z};
     P.cam_p00 = f3{cam->pixel00_loc.x, cam->pixel00_loc.y, cam->pixel00_loc.z};
@@ -1785,12 +2027,14 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     P.tiles_virtual = P.nqueues == 1 ? P.tiles_total : 8 * P.tiles_x * ((tiles_y + 7) / 8);
     P.tiles_per_block = 2;
     if (const char* e = std::getenv("RT_TILES_PER_BLOCK")) P.tiles_per_block = std::max(1, std::atoi(e));
-    constexpr size_t kCounterBytes = 8 * COUNTER_STRIDE * sizeof(uint32_t);
-    const size_t work_bytes = kCounterBytes + size_t(P.nqueues) * size_t(P.queue_cap) * sizeof(int32_t);
+    constexpr size_t kCounterBytes = 9 * COUNTER_STRIDE * sizeof(uint32_t);  // 8 live lists + candidates
+    const size_t list_bytes = size_t(P.nqueues) * size_t(P.queue_cap) * sizeof(int32_t);
+    const size_t work_bytes = kCounterBytes + list_bytes + size_t(P.tiles_total) * sizeof(int32_t);
     if (s->work.n < work_bytes && (rc = s->work.alloc(work_bytes)) != RT_OK) return rc;
     P.live_count = static_cast<uint32_t*>(s->work.p);
     s->last_tiles_total = P.tiles_total;
     P.live_tiles = reinterpret_cast<int32_t*>(static_cast<char*>(s->work.p) + kCounterBytes);
+    P.cand_tiles = reinterpret_cast<int32_t*>(static_cast<char*>(s->work.p) + kCounterBytes + list_bytes);
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int slot = int(s->launches % rt_scene::kRing);
@@ -1798,6 +2042,11 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     HIP_TRY(hipMemsetAsync(s->work.p, 0, kCounterBytes, st));
     hipLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, P);
     HIP_TRY(hipGetLastError());
+    if (P.cull && P.sc.ncut > 0) {
+        const int cut_blocks = std::max(1, (P.tiles_total + 4 * CUT_GROUP - 1) / (4 * CUT_GROUP));
+        hipLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, st, P);
+        HIP_TRY(hipGetLastError());
+    }
     HIP_TRY(hipEventRecord(s->evm[slot], st));
     if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, st);
     else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, st);

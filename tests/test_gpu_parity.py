@@ -325,10 +325,14 @@ def test_full_size_properties_c5():
         _check_fb(rgb[y0:y0 + 2], ref[y0:y0 + 2])
 
 
+@pytest.mark.parametrize("force_cut", [False, True])
 @pytest.mark.parametrize("scene", ["frog.json", "cornell.json", "sphere_single.json"])
-def test_tile_culling_changes_nothing(scene):
-    """Tile culling against the root box is exact: random cameras (near, far, inside the box,
-    grazing, far from the origin) give bit-identical frames and hit AOVs with it on and off."""
+def test_tile_culling_changes_nothing(scene, force_cut, monkeypatch):
+    """Tile culling against the root box (and, forced on for every camera, against the 64-box
+    cut of the tree) is exact: random cameras (near, far, inside the box, grazing, far from
+    the origin) give bit-identical frames and hit AOVs with it on and off."""
+    if force_cut:
+        monkeypatch.setenv("RT_CULL_COVERAGE", "1.0")
     hs = host_scene(scene)
     ds = _device_scene(scene)
     box = np.concatenate([hs.aabbs[0, :3], hs.aabbs[0, 3:]])

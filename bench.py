@@ -6,9 +6,12 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N ...
 
-A step = one full frame: every rank renders its image bands (rows cut into 8-row bands,
-band b -> rank b % N) with the HIP kernel into device memory, then the strips are gathered
-to rank 0 over RCCL (torch.distributed, backend "nccl"); with two strip buffers the gather of
+A step = one full frame delivered on rank 0: every rank renders its image bands (rows cut
+into 8-row bands, band b -> rank b % N) with the HIP kernels into device memory, which also
+write the strip's P6 samples (write_p6 semantics, fused into the render and cull kernels); the
+byte strips are gathered to
+rank 0 over RCCL (torch.distributed, backend "nccl") and un-permuted there on the GPU
+(--gather f32 gathers the float strips instead).  With two strip buffers the gather of
 frame k overlaps the render of frame k+1, and all K gathers finish inside the timed region.
 Scene upload and BVH build are
 outside the timed region (as G/src/main.cu:362-378 times only render()).  Inputs are
@@ -52,6 +55,10 @@ def parse():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: CPU-staged gather (lets N ranks share one GPU to exercise the N>1 path)")
+    ap.add_argument("--gather", default="p6", choices=["p6", "f32"],
+                    help="what a step delivers on rank 0: p6 = the frame's P6 samples (each rank quantises "
+                         "its strip on its GPU, the bytes are gathered and un-permuted; SURVEY.md §8(f) #3), "
+                         "f32 = the float framebuffer strips")
     ap.add_argument("--traffic-file", default=str(REPO / "profiles" / "traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (see DESIGN.md)")
     return ap.parse_args()
@@ -128,29 +135,44 @@ def main():
     # runs on its own stream; before a buffer is rendered into again, the current stream waits
     # for that buffer's previous gather — a stream dependency, the host does not block).
     strips = [torch.zeros((max_rows, W, 3), dtype=torch.float32, device=dev) for _ in range(2)]
+    p6 = a.gather == "p6"
+    rb = W * 3  # P6 bytes per row (maxval 255)
+    qstrips = [torch.zeros((max_rows, rb), dtype=torch.uint8, device=dev) for _ in range(2)] if p6 else None
     gdev = dev if a.backend == "nccl" else torch.device("cpu")
-    gathers = [[torch.empty(strips[0].shape, dtype=torch.float32, device=gdev) for _ in range(world)]
+    payload = qstrips if p6 else strips
+    gathers = [torch.empty((world,) + tuple(payload[0].shape), dtype=payload[0].dtype, device=gdev)
                if (world > 1 and rank == 0) else None for _ in range(2)]
+    p6_frame = torch.empty((H, rb), dtype=torch.uint8, device=dev) if (p6 and rank == 0 and world > 1) else None
     pending = [None, None]
     stream = torch.cuda.current_stream(dev).cuda_stream
     frames = [0]
 
+    def finish(b):
+        """Frame in buffer b is complete on rank 0 once its gather is: un-permute the P6 bands."""
+        if pending[b] is None:
+            return
+        pending[b].wait()
+        pending[b] = None
+        if p6 and rank == 0:
+            g = gathers[b] if a.backend == "nccl" else gathers[b].to(dev)
+            rt.unpermute_strips_device(g.data_ptr(), max_rows, rb, H, BAND_ROWS, world, p6_frame.data_ptr(),
+                                       False, stream)
+
     def step():
         b = frames[0] & 1
         frames[0] += 1
-        if pending[b] is not None:
-            pending[b].wait()
-            pending[b] = None
-        ds.render_device(cam, opts, strips[b].data_ptr(), stream=stream)
+        finish(b)  # frame k-2 used these buffers
+        # p6: the render and cull kernels write the strip's P6 samples themselves (fused epilogue)
+        ds.render_device(cam, opts, strips[b].data_ptr(), stream=stream,
+                         p6_dev_ptr=qstrips[b].data_ptr() if p6 else None)
         if world > 1:
-            src = strips[b] if a.backend == "nccl" else strips[b].cpu()
-            pending[b] = dist.gather(src, gather_list=gathers[b], dst=0, async_op=True)
+            src = payload[b] if a.backend == "nccl" else payload[b].cpu()
+            glist = list(gathers[b].unbind(0)) if rank == 0 else None
+            pending[b] = dist.gather(src, gather_list=glist, dst=0, async_op=True)
 
     def drain():
-        for b in range(2):
-            if pending[b] is not None:
-                pending[b].wait()
-                pending[b] = None
+        for b in ((frames[0]) & 1, (frames[0] + 1) & 1):  # oldest frame first
+            finish(b)
 
     for _ in range(a.warmup):
         step()
@@ -181,21 +203,34 @@ def main():
     # gather the bytes, un-permute on rank 0's GPU; timed once, outside the render metric
     from raytracinginonesemester_amd import dist as rdist
     last = (frames[0] - 1) & 1  # the buffers of the last frame
-    strip, gather = strips[last], gathers[last]
+    strip = strips[last]
     rdist.gather_p6(strip, H, BAND_ROWS, world, rank, stream=stream)  # warm (allocations)
     torch.cuda.synchronize(dev)
     te0 = time.perf_counter()
-    p6 = rdist.gather_p6(strip, H, BAND_ROWS, world, rank, stream=stream)
+    p6_bytes = rdist.gather_p6(strip, H, BAND_ROWS, world, rank, stream=stream)
     te1 = time.perf_counter()
 
-    # assemble the float frame on rank 0 (band un-permute) for the parity check
+    # the float frame on rank 0 (one more gather of the last frame's float strips, outside the
+    # timed region) and the last timed frame's P6 samples, for the parity check
     frame = None
+    fparts = None
+    if world > 1:
+        fl = [torch.empty_like(strip) for _ in range(world)] if rank == 0 else None
+        src = strip if a.backend == "nccl" else strip.cpu()
+        if a.backend == "gloo" and rank == 0:
+            fl = [torch.empty(strip.shape, dtype=strip.dtype) for _ in range(world)]
+        dist.gather(src, gather_list=fl, dst=0)
+        fparts = fl
     if rank == 0:
-        parts = gather if world > 1 else [strip]
+        parts = fparts if world > 1 else [strip]
         frame = np.zeros((H, W, 3), np.float32)
         for r in range(world):
             ys = [y for y in range(H) if (y // BAND_ROWS) % world == r] if world > 1 else list(range(H))
             frame[ys] = parts[r][:len(ys)].cpu().numpy()
+    step_p6 = None
+    if p6 and rank == 0:
+        body = (p6_frame if world > 1 else qstrips[last][:H]).cpu().numpy().tobytes()
+        step_p6 = rt.p6_header(W, H) + body
 
     if world > 1:
         dist.barrier()
@@ -235,6 +270,9 @@ def main():
                    "triangles": hs.num_triangles, "bands": f"{BAND_ROWS}-row bands round-robin over {world} GPU(s)",
                    "gather": (f"{'RCCL' if a.backend == 'nccl' else 'gloo (CPU-staged)'} gather to rank 0"
                               if world > 1 else None),
+                   "step_delivers": ("P6 samples of the frame on rank 0 (render kernels write them"
+                                     + (" + gather of the byte strips + un-permute)" if world > 1 else ")")
+                                     if a.gather == "p6" else "float framebuffer strips on rank 0"),
                    "kernel": a.kernel},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
@@ -246,12 +284,14 @@ def main():
         ref = np.frombuffer(gzip.open(REPO / "tests" / "golden" / "scenes" / "c3_full" / "fb.f32.gz").read(),
                             np.float32).reshape(H, W, 3)
         ppm_ref = gzip.open(REPO / "tests" / "golden" / "scenes" / "c3_full" / "image.ppm.gz").read()
-        pd = np.abs(np.frombuffer(p6[17:], np.uint8).astype(int) - np.frombuffer(ppm_ref[17:], np.uint8).astype(int))
+        pd = np.abs(np.frombuffer(p6_bytes[17:], np.uint8).astype(int) - np.frombuffer(ppm_ref[17:], np.uint8).astype(int))
         line["parity"] = {"vs": "reference CPU render() output (tests/golden/scenes/c3_full)",
                           "rgb_maxabs": float(np.abs(frame - ref).max()),
                           "rgb_bitexact_frac": float((frame.view(np.uint32) == ref.view(np.uint32)).mean()),
-                          "ppm_maxabs": int(pd.max()), "ppm_identical": p6 == ppm_ref,
+                          "ppm_maxabs": int(pd.max()), "ppm_identical": p6_bytes == ppm_ref,
                           "ppm_from": "device P6 epilogue (rt_ppm_quantize_device + gather + un-permute)"}
+        if step_p6 is not None:
+            line["parity"]["timed_step_ppm_identical"] = step_p6 == ppm_ref
     if world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(hs, cam, cfg)
         line["speedup_vs_cpu_baseline"] = round(value / line["cpu_baseline"]["value"], 2)

@@ -223,6 +223,14 @@ int rt_shard_rows(int height, int band_rows, int band_index, int band_count);
 int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt,
                      float* rgb_dev, int32_t* hit_idx_dev, float* hit_t_dev, void* hip_stream);
 
+/* rt_render_device that also writes the pixels' P6 samples (write_p6 defaults: maxval 255,
+ * clamp, sqrt gamma; ppm_p6.cpp:137-155) to p6_dev (rows*W*3 bytes, same row order as
+ * rgb_dev) from the render and cull kernels themselves: the frame epilogue fused into the
+ * kernels that produce the pixels (p6_dev may be NULL). */
+int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt,
+                        float* rgb_dev, int32_t* hit_idx_dev, float* hit_t_dev, uint8_t* p6_dev,
+                        void* hip_stream);
+
 /* Synchronous convenience: render into host memory (rows*W*3 floats, + optional AOVs). */
 int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt,
               float* rgb_host, int32_t* hit_idx_host, float* hit_t_host);

@@ -130,6 +130,7 @@ SIGNATURES = {
     "rt_render_opts_default": (None, [P]),
     "rt_shard_rows": (I, [I, I, I, I]),
     "rt_render_device": (I, [P, P, P, P, P, P, P]),
+    "rt_render_device_p6": (I, [P, P, P, P, P, P, P, P]),
     "rt_render": (I, [P, P, P, P, P, P]),
     "rt_render_reference": (I, [SZ, I, I, P, Vec3, I, I, P, P, P, P, P, I, P, I, I, P]),
     "rt_render_hw1": (I, [I, P, P, P, SZ, P, Vec3, Vec3, I, P, P, P, P]),

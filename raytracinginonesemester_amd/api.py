@@ -253,9 +253,11 @@ class DeviceScene:
         return (rgb, hi, ht) if aov else rgb
 
     def render_device(self, camera: Camera, opts, rgb_dev_ptr: int, hit_idx_ptr=None, hit_t_ptr=None,
-                      stream: Optional[int] = None) -> None:
-        check(lib().rt_render_device(self._h, C.byref(camera.c), C.byref(opts), rgb_dev_ptr, hit_idx_ptr,
-                                     hit_t_ptr, stream))
+                      stream: Optional[int] = None, p6_dev_ptr=None) -> None:
+        """Render into device memory (rt_render_device); with ``p6_dev_ptr`` the render and cull
+        kernels also write the pixels' P6 samples (write_p6 defaults), rt_render_device_p6."""
+        check(lib().rt_render_device_p6(self._h, C.byref(camera.c), C.byref(opts), rgb_dev_ptr, hit_idx_ptr,
+                                        hit_t_ptr, p6_dev_ptr, stream))
 
     def kernel_times(self, max_launches: int = 256) -> np.ndarray:
         """ms of the render kernel for the most recent launches (HIP events on its stream)."""

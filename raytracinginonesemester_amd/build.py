@@ -44,7 +44,7 @@ def _stale(target: Path, deps) -> bool:
 def build(force: bool = False) -> Path:
     OUT.mkdir(parents=True, exist_ok=True)
     OBJ.mkdir(parents=True, exist_ok=True)
-    hdrs = [REPO / "include" / "rt_mi355x.h", CSRC / "rt_common.hpp", CSRC / "rt_math.hpp",
+    hdrs = [REPO / "include" / "rt_mi355x.h", CSRC / "rt_common.hpp", CSRC / "rt_math.hpp", CSRC / "rt_ppm.hpp",
             CSRC / "rt_hip_host.hpp"]
     host_o = OBJ / "rt_host.o"
     dev_objs = []

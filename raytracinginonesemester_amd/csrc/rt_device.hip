@@ -42,6 +42,7 @@
 #include "rt_common.hpp"
 #include "rt_hip_host.hpp"
 #include "rt_math.hpp"
+#include "rt_ppm.hpp"
 
 using namespace rtd;
 
@@ -110,6 +111,8 @@ struct RenderParams {
     float* __restrict__ rgb;
     int32_t* __restrict__ hit_idx;
     float* __restrict__ hit_t;
+    uint8_t* __restrict__ p6;  // optional: write_p6-default samples of the pixels (rows*W*3 bytes)
+    uint8_t miss_p6[4];        // the culled pixels' samples
 };
 
 // ---- wave primitives ------------------------------------------------------------------
@@ -887,10 +890,34 @@ __device__ __forceinline__ void write_culled_tile(const RenderParams& P, int til
     const int xa = tx * P.tile_w, ra = ty * P.tile_h;
     const int tw = min(xa + P.tile_w, P.W) - xa, th = min(ra + P.tile_h, P.rows) - ra;
     const float mp[3] = {P.miss_pixel.x, P.miss_pixel.y, P.miss_pixel.z};
-    for (int i = first; i < tw * th * 3; i += lanes) {
-        const int px = i / 3, c = i - 3 * px;
-        const int r = ra + px / tw, x = xa + px % tw;
-        P.rgb[((size_t)r * P.W + x) * 3 + c] = mp[c];
+    if (lanes == 1 && tw == 4 && (xa & 3) == 0 && (P.W & 3) == 0 && ((uintptr_t)P.rgb & 15) == 0 &&
+        ((uintptr_t)P.p6 & 3) == 0) {
+        // 4-pixel rows (the common tile width): 48 B of floats as three 16-byte stores and 12 B
+        // of samples as three 4-byte stores per row (W and x multiples of 4: aligned)
+        const float4 f0 = make_float4(mp[0], mp[1], mp[2], mp[0]), f1 = make_float4(mp[1], mp[2], mp[0], mp[1]),
+                     f2 = make_float4(mp[2], mp[0], mp[1], mp[2]);
+        const uint32_t b0 = P.miss_p6[0], b1 = P.miss_p6[1], b2 = P.miss_p6[2];
+        const uint32_t w0 = b0 | b1 << 8 | b2 << 16 | b0 << 24, w1 = b1 | b2 << 8 | b0 << 16 | b1 << 24,
+                       w2 = b2 | b0 << 8 | b1 << 16 | b2 << 24;
+        for (int r = ra; r < ra + th; ++r) {
+            float4* o = reinterpret_cast<float4*>(P.rgb + ((size_t)r * P.W + xa) * 3);
+            o[0] = f0;
+            o[1] = f1;
+            o[2] = f2;
+            if (P.p6) {
+                uint32_t* q = reinterpret_cast<uint32_t*>(P.p6 + ((size_t)r * P.W + xa) * 3);
+                q[0] = w0;
+                q[1] = w1;
+                q[2] = w2;
+            }
+        }
+    } else {
+        for (int i = first; i < tw * th * 3; i += lanes) {
+            const int px = i / 3, c = i - 3 * px;
+            const int r = ra + px / tw, x = xa + px % tw;
+            P.rgb[((size_t)r * P.W + x) * 3 + c] = mp[c];
+            if (P.p6) P.p6[((size_t)r * P.W + x) * 3 + c] = P.miss_p6[c];
+        }
     }
     if (P.hit_idx) {
         for (int i = first; i < tw * th * P.spp; i += lanes) {
@@ -1036,10 +1063,16 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
         // x / 2^k and x * 2^-k are the same correctly rounded value (the exact quotients are
         // equal), so the power-of-two divide is a multiply here.
         const float rs = 1.0f / (float)P.spp;
-        float* o = P.rgb + ((size_t)r * P.W + x) * 3;
-        o[0] = acc.x * rs;
-        o[1] = acc.y * rs;
-        o[2] = acc.z * rs;
+        const size_t k = ((size_t)r * P.W + x) * 3;
+        const f3 px = mk(acc.x * rs, acc.y * rs, acc.z * rs);
+        P.rgb[k] = px.x;
+        P.rgb[k + 1] = px.y;
+        P.rgb[k + 2] = px.z;
+        if (P.p6) {  // the frame epilogue fused in (write_p6 defaults)
+            P.p6[k] = rtp::p6_default_sample(px.x);
+            P.p6[k + 1] = rtp::p6_default_sample(px.y);
+            P.p6[k + 2] = rtp::p6_default_sample(px.z);
+        }
     }
 }
 
@@ -1066,10 +1099,16 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
     }
     if (valid) {
         const float fs = (float)P.spp;
-        float* o = P.rgb + ((size_t)r * P.W + x) * 3;
-        o[0] = acc.x / fs;
-        o[1] = acc.y / fs;
-        o[2] = acc.z / fs;
+        const size_t k = ((size_t)r * P.W + x) * 3;
+        const f3 px = mk(acc.x / fs, acc.y / fs, acc.z / fs);
+        P.rgb[k] = px.x;
+        P.rgb[k + 1] = px.y;
+        P.rgb[k + 2] = px.z;
+        if (P.p6) {
+            P.p6[k] = rtp::p6_default_sample(px.x);
+            P.p6[k + 1] = rtp::p6_default_sample(px.y);
+            P.p6[k + 2] = rtp::p6_default_sample(px.z);
+        }
     }
 }
 
@@ -1954,6 +1993,11 @@ double root_box_coverage(const float* rb, const rt_camera* cam) {
 
 extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, float* rgb,
                                 int32_t* hit_idx, float* hit_t, void* stream) {
+    return rt_render_device_p6(s, cam, o, rgb, hit_idx, hit_t, nullptr, stream);
+}
+
+extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, float* rgb,
+                                   int32_t* hit_idx, float* hit_t, uint8_t* p6, void* stream) {
     if (!s || !cam || !o || !rgb) return set_error(RT_ERR_ARG, "rt_render_device: null argument");
     if (o->spp < 1) return set_error(RT_ERR_ARG, "spp must be >= 1");
     if ((hit_idx == nullptr) != (hit_t == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
@@ -2006,6 +2050,14 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     P.rgb = rgb;
     P.hit_idx = hit_idx;
     P.hit_t = hit_t;
+    P.p6 = p6;
+    {
+        const f3 mp = miss_pixel_value(o);
+        P.miss_p6[0] = rtp::p6_default_sample(mp.x);
+        P.miss_p6[1] = rtp::p6_default_sample(mp.y);
+        P.miss_p6[2] = rtp::p6_default_sample(mp.z);
+        P.miss_p6[3] = 0;
+    }
     const bool samples = o->kernel != RT_KERNEL_WAVE_PIXELS && o->spp <= BLOCK && (o->spp & (o->spp - 1)) == 0;
     int ppb = samples ? BLOCK / o->spp : BLOCK;  // pixels per block
     int tw = 1;

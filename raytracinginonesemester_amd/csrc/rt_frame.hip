@@ -20,6 +20,7 @@
 
 #include "rt_common.hpp"
 #include "rt_hip_host.hpp"
+#include "rt_ppm.hpp"
 
 using rt::set_error;
 using rt::hip_msg;
@@ -30,26 +31,7 @@ constexpr int BLOCK = 256;
 typedef float __attribute__((ext_vector_type(4))) vf4;
 typedef uint32_t __attribute__((ext_vector_type(4))) vu4;
 
-// std::lround as glibc computes it on x86-64: nearest integer, halves away from zero; a NaN or
-// a value outside long's range converts to LONG_MIN (the x86 "integer indefinite"), which the
-// caller's `rounded < 0` check turns into 0.
-__device__ __forceinline__ uint32_t float_to_sample(float f, int maxval, bool clamp, bool gamma2) {
-    double x = (double)f;
-    if (gamma2) {
-        if (x < 0.0) x = 0.0;
-        x = sqrt(x);
-    }
-    if (clamp) {
-        if (x < 0.0) x = 0.0;
-        if (x > 1.0) x = 1.0;
-    }
-    const double s = x * (double)maxval;
-    if (!(fabs(s) < 9223372036854775808.0)) return 0u;
-    const double r = round(s);
-    if (r < 0.0) return 0u;
-    if (r > (double)maxval) return (uint32_t)maxval;
-    return (uint32_t)r;
-}
+using rtp::float_to_sample;
 
 struct QuantParams {
     const float* rgb;

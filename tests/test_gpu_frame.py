@@ -124,3 +124,30 @@ def test_gather_p6_single_rank_matches_host_encode():
     for flip in (False, True):
         got = rd.gather_p6(t, 45, 8, 1, 0, flip_y=flip)
         assert got == rt.encode_p6(rgb, flip_y=flip)
+
+
+@pytest.mark.parametrize("spp,miss,kernel,bands", [
+    (16, (0.0, 0.0, 0.0), rt.RT_KERNEL_AUTO, (8, 0, 1)),        # c3's shape: samples kernel, culled tiles
+    (3, (0.5, 0.7, 1.0), rt.RT_KERNEL_AUTO, (8, 0, 1)),         # pixels kernel, non-black miss pixels
+    (4, (0.2, 0.1, 0.05), rt.RT_KERNEL_LANE, (8, 1, 3)),        # lane kernel, a band shard
+])
+def test_render_device_fused_p6_matches_write_p6(spp, miss, kernel, bands):
+    """rt_render_device_p6: the P6 samples the render and cull kernels write alongside the float
+    pixels are write_p6's quantisation of those pixels, byte for byte (live and culled tiles)."""
+    from conftest import host_scene
+
+    hs = host_scene("frog.json")
+    cam = hs.camera(160, 90)
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    band_rows, band_index, band_count = bands
+    opts, _keep = ds.make_opts(spp=spp, max_depth=1, miss_color=miss, band_rows=band_rows,
+                               band_index=band_index, band_count=band_count, kernel=kernel)
+    rows = rt._lib.lib().rt_shard_rows(90, band_rows, band_index, band_count)
+    rgb = torch.zeros((rows, 160, 3), dtype=torch.float32, device=DEV)
+    p6 = torch.full((rows, 160 * 3), 7, dtype=torch.uint8, device=DEV)
+    stream = torch.cuda.current_stream(DEV).cuda_stream
+    ds.render_device(cam, opts, rgb.data_ptr(), stream=stream, p6_dev_ptr=p6.data_ptr())
+    torch.cuda.synchronize(DEV)
+    want = rt.encode_p6(rgb.cpu().numpy())
+    assert want[-p6.numel():] == p6.cpu().numpy().tobytes()
+    ds.close()

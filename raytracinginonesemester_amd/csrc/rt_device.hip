@@ -1114,11 +1114,15 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
 
 // Each block runs tiles_per_block virtual blocks (planned_tile): fewer, longer blocks, so
 // the dispatcher does not spend the frame launching blocks that find no live tile.
-template <int MODE, bool SAMPLES, bool D1>
+// WAVES: waves per SIMD the kernel is compiled for.  6 (80 VGPRs) is fastest for scenes whose
+// nodes stay in L2 (c3: 6 > 5, 7 > 4 waves); scenes far larger than the L2s (c5, 345 MB) gain
+// from one more wave of latency hiding despite more spills (7: -4 % on c5), so the depth-1
+// sample kernels are also built for 7 (launch picks by scene size, big_scene_waves).
 #ifndef RT_RENDER_WAVES
-#define RT_RENDER_WAVES 6  // waves per SIMD the render kernel is compiled for (80 VGPRs)
+#define RT_RENDER_WAVES 6
 #endif
-__global__ __launch_bounds__(BLOCK, RT_RENDER_WAVES) void render_tiles_kernel(RenderParams P) {
+template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES>
+__global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
     const int b = (int)blockIdx.x, g = (int)gridDim.x;
     const int q = P.nqueues == 1 ? 0 : (b & 7);
@@ -1930,17 +1934,32 @@ int prepare_jitter(rt_scene* s, const rt_render_opts* o) {
 // tiles_virtual / tiles_per_block blocks (rounded up to a multiple of 8) over the planned
 // virtual blocks (planned_tile).
 template <int MODE, bool SAMPLES>
-void launch_mode(const RenderParams& P, hipStream_t st) {
+void launch_mode(const RenderParams& P, bool big, hipStream_t st) {
     const int g = (P.tiles_virtual + P.tiles_per_block - 1) / P.tiles_per_block;
     const dim3 grid((g + 7) / 8 * 8);
-    if (P.max_depth == 1) hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES, true>), grid, dim3(BLOCK), 0, st, P);
-    else hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES, false>), grid, dim3(BLOCK), 0, st, P);
+    if (P.max_depth == 1) {
+        if constexpr (SAMPLES && MODE != RT_KERNEL_LANE) {
+            if (big) {
+                hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES, true, 7>), grid, dim3(BLOCK), 0, st, P);
+                return;
+            }
+        }
+        hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES, true>), grid, dim3(BLOCK), 0, st, P);
+    } else {
+        hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES, false>), grid, dim3(BLOCK), 0, st, P);
+    }
 }
 
 template <int MODE>
-void launch(const RenderParams& P, bool samples, hipStream_t st) {
-    if (samples) launch_mode<MODE, true>(P, st);
-    else launch_mode<MODE, false>(P, st);
+void launch(const RenderParams& P, bool samples, bool big, hipStream_t st) {
+    if (samples) launch_mode<MODE, true>(P, big, st);
+    else launch_mode<MODE, false>(P, big, st);
+}
+
+// Scene data well beyond the eight 4 MB L2s (c5: 345 MB; frog: 6.6 MB): the 7-wave build.
+bool big_scene_waves(const rt_scene* s) {
+    if (const char* e = std::getenv("RT_RENDER_WAVES_BIG")) return std::atoi(e) != 0;
+    return s->bytes > (size_t(64) << 20);
 }
 
 // Host restatement of a pixel whose spp samples all miss the root: each sample is
@@ -2100,9 +2119,10 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(s->evm[slot], st));
-    if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, st);
-    else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, st);
-    else launch<RT_KERNEL_WAVE>(P, samples, st);
+    const bool big = big_scene_waves(s);
+    if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, big, st);
+    else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, big, st);
+    else launch<RT_KERNEL_WAVE>(P, samples, big, st);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(s->ev1[slot], st));
     s->launches++;

@@ -70,6 +70,26 @@ def test_golden_scene_parity(name, kernel, flags):
     _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
 
 
+@pytest.mark.parametrize("name", ["c3_small", "c5_small", "frog_bounce"])
+def test_big_scene_kernel_build_parity(name, monkeypatch):
+    """The 7-wave build of the depth-1 sample kernels (picked for scenes far beyond the L2s)
+    forced on small scenes: the reference's outputs bit for bit."""
+    monkeypatch.setenv("RT_RENDER_WAVES_BIG", "1")
+    meta = golden_meta(name)
+    scene = G_SCENES[name]
+    hs = host_scene(scene)
+    cam = hs.camera(meta["width"], meta["height"])
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    rgb, hi, ht = ds.render(cam, spp=meta["spp"], max_depth=meta["max_depth"],
+                            diffuse_bounce=bool(meta["diffuse_bounce"]), miss_color=hexv(meta["miss_color"]),
+                            aov=True)
+    assert np.array_equal(hi.reshape(-1), golden_array(name, "hits.i32.gz", np.int32))
+    assert np.array_equal(ht.reshape(-1).view(np.uint32),
+                          golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
+    _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
+    ds.close()
+
+
 @pytest.mark.parametrize("flags,tiles,tpb", LAUNCHES)
 def test_c3_full_frame_matches_reference(flags, tiles, tpb, monkeypatch):
     """1920x1080x16 frog (config c3) against the reference's own full-size outputs, for every

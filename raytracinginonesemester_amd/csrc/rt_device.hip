@@ -992,6 +992,13 @@ __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
     // view and the cut rarely removes a tile (c5's heightfield: none of 739,248), so the
     // candidates pass through untested (a speed choice only: passing is always exact).
     const bool test = P.cut_force || 4 * (int64_t)n <= (int64_t)P.tiles_total;
+    // this lane's box of the cut, loaded once (the culled-tile stores below would otherwise make
+    // the compiler reload it for every tile)
+    float box[6] = {0.f, 0.f, 0.f, -1.f, -1.f, -1.f};
+    if ((int)lane < P.sc.ncut) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) box[i] = P.sc.cut[6 * (size_t)lane + i];
+    }
     // One group per wave, in dispatch order (the grid covers every possible candidate; waves
     // past the list leave): the live lists keep the candidates' near-raster order, which the
     // render kernel's L2 reuse depends on (a grid-stride loop here scrambles it: c5 +5 %).
@@ -1005,7 +1012,7 @@ __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
             const int xa = tx * P.tile_w, ra = ty * P.tile_h;
             const int xb = min(xa + P.tile_w, P.W) - 1, rb = min(ra + P.tile_h, P.rows) - 1;
             const TileDirsF T = tile_dirs_f(P, xa, xb, global_row(P, ra), global_row(P, rb));
-            const bool hit = (int)lane < P.sc.ncut && !tile_misses_box_f(T, P.sc.cut + 6 * (size_t)lane);
+            const bool hit = (int)lane < P.sc.ncut && !tile_misses_box_f(T, box);
             if (ballot(hit) == 0) write_culled_tile(P, tile, (int)lane, 64);
             else live |= 1ull << j;
         }

@@ -106,7 +106,6 @@ struct RenderParams {
     int32_t cut_force;    // test every candidate in tile_cut_kernel (no pass-through)
     int32_t nqueues;
     int32_t queue_cap;
-    int32_t tiles_per_block;                          // virtual blocks per render block
     int32_t tiles_virtual;                            // virtual blocks (planned_tile)
     float* __restrict__ rgb;
     int32_t* __restrict__ hit_idx;
@@ -1119,8 +1118,10 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
     }
 }
 
-// Each block runs tiles_per_block virtual blocks (planned_tile): fewer, longer blocks, so
-// the dispatcher does not spend the frame launching blocks that find no live tile.
+// One virtual block (planned_tile) per workgroup; a block whose slot holds no live tile leaves
+// at once.  (Looping a block over several slots measured no faster on c3 and, by keeping the
+// per-sample invariants live across the loop, spilled 224 B instead of 144 B per lane: c5 -6 %
+// without the loop.)
 // WAVES: waves per SIMD the kernel is compiled for.  6 (80 VGPRs) is fastest for scenes whose
 // nodes stay in L2 (c3: 6 > 5, 7 > 4 waves); scenes far larger than the L2s (c5, 345 MB) gain
 // from one more wave of latency hiding despite more spills (7: -4 % on c5), so the depth-1
@@ -1131,33 +1132,13 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
 template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES>
 __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
-    const int b = (int)blockIdx.x, g = (int)gridDim.x;
+    const int b = (int)blockIdx.x;
+    if (b >= P.tiles_virtual) return;
     const int q = P.nqueues == 1 ? 0 : (b & 7);
-    const int len = list_length(P, q);
-    // Next live virtual block of this block from m on (m = tiles_per_block: none).  The block
-    // leaves before the tile loop when it has none, so blocks without work skip the loop's
-    // set-up (the compiler hoists per-sample invariants, and their spills, in front of it).
-    auto next_tile = [&](int& m) {
-        for (; m < P.tiles_per_block; ++m) {
-            const int j = b + m * g;
-            if (j >= P.tiles_virtual) break;
-            const int tile = planned_tile(P, len, q, P.nqueues == 1 ? j : (j >> 3));
-            if (tile >= 0) return tile;
-        }
-        m = P.tiles_per_block;
-        return -1;
-    };
-    int m = 0;
-    int tile = next_tile(m);
+    const int tile = planned_tile(P, list_length(P, q), q, P.nqueues == 1 ? b : (b >> 3));
     if (tile < 0) return;
-    for (;;) {
-        if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col);
-        else pixels_tile<MODE, D1>(P, tile);
-        ++m;
-        tile = next_tile(m);
-        if (tile < 0) break;
-        if constexpr (SAMPLES) __syncthreads();  // col is rewritten by the next tile
-    }
+    if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col);
+    else pixels_tile<MODE, D1>(P, tile);
 }
 
 // ---- HW1 brute force (HW1/src/render.cpp:72-116) ----------------------------------------
@@ -1938,12 +1919,10 @@ int prepare_jitter(rt_scene* s, const rt_render_opts* o) {
     return RT_OK;
 }
 
-// tiles_virtual / tiles_per_block blocks (rounded up to a multiple of 8) over the planned
-// virtual blocks (planned_tile).
+// tiles_virtual blocks (rounded up to a multiple of 8), one per planned virtual block.
 template <int MODE, bool SAMPLES>
 void launch_mode(const RenderParams& P, bool big, hipStream_t st) {
-    const int g = (P.tiles_virtual + P.tiles_per_block - 1) / P.tiles_per_block;
-    const dim3 grid((g + 7) / 8 * 8);
+    const dim3 grid((P.tiles_virtual + 7) / 8 * 8);
     if (P.max_depth == 1) {
         if constexpr (SAMPLES && MODE != RT_KERNEL_LANE) {
             if (big) {
@@ -2103,8 +2082,6 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.nqueues = P.tile_order == RT_TILES_LINEAR ? 1 : 8;
     P.queue_cap = P.tiles_total;
     P.tiles_virtual = P.nqueues == 1 ? P.tiles_total : 8 * P.tiles_x * ((tiles_y + 7) / 8);
-    P.tiles_per_block = 2;
-    if (const char* e = std::getenv("RT_TILES_PER_BLOCK")) P.tiles_per_block = std::max(1, std::atoi(e));
     constexpr size_t kCounterBytes = 9 * COUNTER_STRIDE * sizeof(uint32_t);  // 8 live lists + candidates
     const size_t list_bytes = size_t(P.nqueues) * size_t(P.queue_cap) * sizeof(int32_t);
     const size_t work_bytes = kCounterBytes + list_bytes + size_t(P.tiles_total) * sizeof(int32_t);

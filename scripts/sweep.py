@@ -8,7 +8,7 @@ every variant's frame is bit-identical to the first variant's.
 import argparse
 import itertools
 import json
-import os
+import os  # noqa: F401
 import sys
 from pathlib import Path
 
@@ -28,8 +28,7 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--kernels", default="wave,lane")
 ap.add_argument("--tiles", default="linear,xcd_chunk,rows")
 ap.add_argument("--flags", default="0", help="RT_FLAG_* values to compare, e.g. 0,2,4 "
-                "(1 no cull, 2 megakernel, 4 binary nodes)")
-ap.add_argument("--tpb", default="2", help="tiles per render block (RT_TILES_PER_BLOCK), e.g. 1,2,4,8")
+                "(1 no cull, 4 binary nodes)")
 a = ap.parse_args()
 
 cfg = configs.G_CONFIGS[a.config]
@@ -39,13 +38,11 @@ cam = hs.camera(cfg["width"], cfg["height"])
 ds = rt.DeviceScene.from_host(hs)
 K = {"wave": rt.RT_KERNEL_WAVE, "lane": rt.RT_KERNEL_LANE, "wavepix": rt._lib.RT_KERNEL_WAVE_PIXELS}
 T = {"linear": rt.RT_TILES_LINEAR, "xcd_chunk": rt.RT_TILES_XCD_CHUNK, "rows": rt.RT_TILES_ROWS}
-variants = list(itertools.product(a.kernels.split(","), a.tiles.split(","), a.flags.split(","),
-                                  a.tpb.split(",")))
+variants = list(itertools.product(a.kernels.split(","), a.tiles.split(","), a.flags.split(",")))
 times = {v: [] for v in variants}
 ref = None
 for r in range(a.rounds):
     for v in variants:
-        os.environ["RT_TILES_PER_BLOCK"] = v[3]
         for _ in range(a.reps):
             img = ds.render(cam, spp=cfg["spp"], max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
                             kernel=K[v[0]], tile_order=T[v[1]],
@@ -57,7 +54,7 @@ for r in range(a.rounds):
 samples = cfg["width"] * cfg["height"] * cfg["spp"]
 for v in variants:
     t = np.array(times[v])
-    print(json.dumps({"config": a.config, "kernel": v[0], "tiles": v[1], "flags": int(v[2]), "tpb": v[3],
+    print(json.dumps({"config": a.config, "kernel": v[0], "tiles": v[1], "flags": int(v[2]),
                       "median_ms": round(float(np.median(t)), 4),
                       "min_ms": round(float(t.min()), 4), "Gsamples_s": round(float(samples / np.median(t) / 1e6), 3)}),
           flush=True)

@@ -30,9 +30,9 @@ RGB_TOL = 2e-6
 KERNELS = [rt.RT_KERNEL_WAVE, rt.RT_KERNEL_LANE]
 # (flags, tile order, tiles per render block): launch shapes, all of which must give the same frame
 BIN = rt._lib.RT_FLAG_BINARY
-LAUNCHES = [(0, rt.RT_TILES_AUTO, None), (BIN, rt.RT_TILES_AUTO, None), (0, rt.RT_TILES_LINEAR, "1"),
-            (BIN, rt.RT_TILES_ROWS, "5"), (0, rt.RT_TILES_XCD_CHUNK, "3"),
-            (rt._lib.RT_FLAG_NO_CULL, rt.RT_TILES_XCD_CHUNK, "2"), (BIN | rt._lib.RT_FLAG_NO_CULL, rt.RT_TILES_LINEAR, "2")]
+LAUNCHES = [(0, rt.RT_TILES_AUTO), (BIN, rt.RT_TILES_AUTO), (0, rt.RT_TILES_LINEAR),
+            (BIN, rt.RT_TILES_ROWS), (0, rt.RT_TILES_XCD_CHUNK),
+            (rt._lib.RT_FLAG_NO_CULL, rt.RT_TILES_XCD_CHUNK), (BIN | rt._lib.RT_FLAG_NO_CULL, rt.RT_TILES_LINEAR)]
 
 
 def _device_scene(scene):
@@ -90,12 +90,10 @@ def test_big_scene_kernel_build_parity(name, monkeypatch):
     ds.close()
 
 
-@pytest.mark.parametrize("flags,tiles,tpb", LAUNCHES)
-def test_c3_full_frame_matches_reference(flags, tiles, tpb, monkeypatch):
+@pytest.mark.parametrize("flags,tiles", LAUNCHES)
+def test_c3_full_frame_matches_reference(flags, tiles):
     """1920x1080x16 frog (config c3) against the reference's own full-size outputs, for every
-    launch shape (tile orders, tiles per render block, culling on/off)."""
-    if tpb is not None:
-        monkeypatch.setenv("RT_TILES_PER_BLOCK", tpb)
+    launch shape (tile orders, binary/4-ary records, culling on/off)."""
     meta = golden_meta("c3_full")
     hs = host_scene("frog.json")
     cam = hs.camera(1920, 1080)
@@ -374,19 +372,13 @@ def test_tile_culling_changes_nothing(scene, force_cut, monkeypatch):
 
 
 @pytest.mark.parametrize("spp", [3, 16])
-def test_many_tiles_per_render_block(spp, monkeypatch):
-    """Render blocks looping over several planned tiles (RT_TILES_PER_BLOCK), for the
-    sample-per-lane and pixel-per-lane kernels: identical to one tile per block, and rows of
-    it against the oracle."""
+def test_720p_frame_rows_against_oracle(spp):
+    """A 1280x720 frame for the sample-per-lane (16 spp) and pixel-per-lane (3 spp) kernels:
+    rows through the frog against the oracle."""
     hs = host_scene("frog.json")
     cam = hs.camera(1280, 720)
     ds = _device_scene("frog.json")
-    monkeypatch.setenv("RT_TILES_PER_BLOCK", "1")
-    a = ds.render(cam, spp=spp, max_depth=1, aov=True)
-    monkeypatch.setenv("RT_TILES_PER_BLOCK", "7")
     b = ds.render(cam, spp=spp, max_depth=1, aov=True)
-    for x, y in zip(a, b):
-        assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32))
     ref = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,
                        hs.tri_object_ids, hs.materials, hs.lights, spp=spp, max_depth=1, rows=(352, 368))
     _check_fb(b[0][352:368], ref[352:368])

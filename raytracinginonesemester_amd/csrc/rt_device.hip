@@ -576,8 +576,9 @@ __device__ __forceinline__ int32_t leaf_tri(const SceneView& sc, int32_t slot) {
 // All lanes of a wave call it; `valid` marks lanes owning a sample.  D1: max_depth == 1 (no
 // bounce; the configuration the benchmarks run).
 template <int MODE, bool D1>
-__device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int32_t* prim_idx,
-                           float* prim_t) {
+// The primary-hit AOV (P.hit_idx / P.hit_t at element aov, when aov >= 0) is written as soon as
+// the camera ray's traversal ends, so nothing of it stays live across the shading.
+__device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int64_t aov) {
     const SceneView& sc = P.sc;
     RayPre ray = camera_ray(P, valid, x, y, s);
     if constexpr (D1) {
@@ -592,8 +593,10 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
         }
 #endif
         if (valid) {
-            *prim_idx = hs.slot >= 0 ? leaf_tri(sc, hs.slot) : -1;
-            *prim_t = hs.slot >= 0 ? hs.bestT : -1.0f;
+            if (aov >= 0) {
+                P.hit_idx[aov] = hs.slot >= 0 ? leaf_tri(sc, hs.slot) : -1;
+                P.hit_t[aov] = hs.slot >= 0 ? hs.bestT : -1.0f;
+            }
         }
 #ifdef RT_EXP_NO_SHADE  // timing experiments only (wrong output): primary traversal only
         return mk(hs.bestT, 0.f, 0.f);
@@ -615,8 +618,10 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
         sh.tri = -1;
         if (hit) sh = resolve_hit(sc, ray, hs.slot);
         if (depth == 0 && valid) {
-            *prim_idx = hit ? sh.tri : -1;
-            *prim_t = hit ? hs.bestT : -1.0f;
+            if (aov >= 0) {
+                P.hit_idx[aov] = hit ? sh.tri : -1;
+                P.hit_t[aov] = hit ? hs.bestT : -1.0f;
+            }
         }
         if (alive && !hit) {
             radiance = add(radiance, mul(thr, P.miss));
@@ -1040,44 +1045,47 @@ __device__ __forceinline__ int planned_tile(const RenderParams& P, int len, int 
 // One sample per lane: a block covers a tile_w x tile_h pixel tile x spp samples (spp a power
 // of two <= 256, tile_w*tile_h*spp == BLOCK); per-pixel sums run in sample order from LDS.
 template <int MODE, bool D1>
-__device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, float* col) {
+__device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, float* col, int* kpix) {
     const int t = (int)threadIdx.x;
-    const int s = t & (P.spp - 1);            // spp and tile_w are powers of two here
-    const int pit = t >> P.spp_log2;
-    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-    const int x = tx * P.tile_w + (pit & (P.tile_w - 1));
-    const int r = ty * P.tile_h + (pit >> P.tile_w_log2);
-    const bool valid = x < P.W && r < P.rows;
-    const int y = valid ? global_row(P, r) : 0;
-    int32_t pidx = -1;
-    float pt = -1.f;
-    const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, &pidx, &pt);
-    if (valid && P.hit_idx) {
-        const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp + (size_t)s;
-        P.hit_idx[k] = pidx;
-        P.hit_t[k] = pt;
+    {
+        const int s = t & (P.spp - 1);  // spp and tile_w are powers of two here
+        const int pit = t >> P.spp_log2;
+        const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        const int x = tx * P.tile_w + (pit & (P.tile_w - 1));
+        const int r = ty * P.tile_h + (pit >> P.tile_w_log2);
+        const bool valid = x < P.W && r < P.rows;
+        const int y = valid ? global_row(P, r) : 0;
+        const int pix = valid ? r * P.W + x : -1;
+        // The pixel's index goes through LDS (read back below), so the compiler does not keep
+        // it, or addresses made from it, live (and spilled) across the shading.
+        if (s == 0) kpix[t >> P.spp_log2] = pix;
+        const int64_t aov = valid && P.hit_idx ? (int64_t)pix * P.spp + s : -1;
+        const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, aov);
+        col[3 * t] = c.x;
+        col[3 * t + 1] = c.y;
+        col[3 * t + 2] = c.z;
     }
-    col[3 * t] = c.x;
-    col[3 * t + 1] = c.y;
-    col[3 * t + 2] = c.z;
     __syncthreads();
-    if (valid && s == 0) {
-        // col = col + TraceRayIterative(...) in sample order, then col / float(spp)
-        f3 acc = mk(0.f, 0.f, 0.f);
-        for (int k = 0; k < P.spp; ++k)
-            acc = add(acc, mk(col[3 * (t + k)], col[3 * (t + k) + 1], col[3 * (t + k) + 2]));
-        // x / 2^k and x * 2^-k are the same correctly rounded value (the exact quotients are
-        // equal), so the power-of-two divide is a multiply here.
-        const float rs = 1.0f / (float)P.spp;
-        const size_t k = ((size_t)r * P.W + x) * 3;
-        const f3 px = mk(acc.x * rs, acc.y * rs, acc.z * rs);
-        P.rgb[k] = px.x;
-        P.rgb[k + 1] = px.y;
-        P.rgb[k + 2] = px.z;
-        if (P.p6) {  // the frame epilogue fused in (write_p6 defaults)
-            P.p6[k] = rtp::p6_default_sample(px.x);
-            P.p6[k + 1] = rtp::p6_default_sample(px.y);
-            P.p6[k + 2] = rtp::p6_default_sample(px.z);
+    if ((t & (P.spp - 1)) == 0) {
+        const int pix = kpix[t >> P.spp_log2];
+        if (pix >= 0) {
+            // col = col + TraceRayIterative(...) in sample order, then col / float(spp)
+            f3 acc = mk(0.f, 0.f, 0.f);
+            for (int k = 0; k < P.spp; ++k)
+                acc = add(acc, mk(col[3 * (t + k)], col[3 * (t + k) + 1], col[3 * (t + k) + 2]));
+            // x / 2^k and x * 2^-k are the same correctly rounded value (the exact quotients
+            // are equal), so the power-of-two divide is a multiply here.
+            const float rs = 1.0f / (float)P.spp;
+            const size_t k = (size_t)pix * 3;
+            const f3 px = mk(acc.x * rs, acc.y * rs, acc.z * rs);
+            P.rgb[k] = px.x;
+            P.rgb[k + 1] = px.y;
+            P.rgb[k + 2] = px.z;
+            if (P.p6) {  // the frame epilogue fused in (write_p6 defaults)
+                P.p6[k] = rtp::p6_default_sample(px.x);
+                P.p6[k + 1] = rtp::p6_default_sample(px.y);
+                P.p6[k + 2] = rtp::p6_default_sample(px.z);
+            }
         }
     }
 }
@@ -1093,15 +1101,8 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
     const int y = valid ? global_row(P, r) : 0;
     f3 acc = mk(0.f, 0.f, 0.f);
     for (int s = 0; s < P.spp; ++s) {
-        int32_t pidx = -1;
-        float pt = -1.f;
-        const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, &pidx, &pt);
-        if (valid && P.hit_idx) {
-            const size_t k = ((size_t)r * P.W + x) * (size_t)P.spp + (size_t)s;
-            P.hit_idx[k] = pidx;
-            P.hit_t[k] = pt;
-        }
-        acc = add(acc, c);
+        const int64_t aov = valid && P.hit_idx ? ((int64_t)r * P.W + x) * P.spp + s : -1;
+        acc = add(acc, trace_sample<MODE, D1>(P, valid, x, y, s, aov));
     }
     if (valid) {
         const float fs = (float)P.spp;
@@ -1132,12 +1133,13 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
 template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES>
 __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
+    __shared__ int kpix[SAMPLES ? BLOCK : 1];
     const int b = (int)blockIdx.x;
     if (b >= P.tiles_virtual) return;
     const int q = P.nqueues == 1 ? 0 : (b & 7);
     const int tile = planned_tile(P, list_length(P, q), q, P.nqueues == 1 ? b : (b >> 3));
     if (tile < 0) return;
-    if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col);
+    if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col, kpix);
     else pixels_tile<MODE, D1>(P, tile);
 }
 

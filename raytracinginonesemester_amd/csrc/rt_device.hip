@@ -56,6 +56,7 @@ constexpr int BLOCK = 256;
 // Kernel instantiation flag on top of RT_KERNEL_WAVE: traverse the 4-ary records (SceneView::wide).
 // A compile-time choice, so each kernel holds one traversal loop per ray kind.
 constexpr int MODE_WIDE = 16;
+constexpr int MODE_PACKED = 32;  // box tests with packed FMAs (box_ends_pk): the big-scene kernels
 constexpr float kRayTMin = 1e-4f;             // query.h:233
 constexpr float RT_EPS = 1e-3f;               // shader.h:22
 
@@ -225,8 +226,11 @@ __device__ __forceinline__ BoxP leaf_box(const NodeRec& r) {
 // box_hit for the lanes in `act` (a wave mask; all lanes call it), as the mask of lanes that
 // pass: the float pre-classification for everyone, the exact double test only behind a
 // wave-uniform branch taken when some lane is ambiguous.
+template <bool PK = false>
 __device__ __forceinline__ uint64_t box_hit_mask(const RayPre& r, const BoxP& b, float tmax, uint64_t act) {
-    const AxisEnds e = box_ends(r, b);
+    AxisEnds e;
+    if constexpr (PK) e = box_ends_pk(r, b);
+    else e = box_ends(r, b);
     const BoxEnds c = box_lc_hc(e, kRayTMin, tmax);
     uint64_t hit = ballot(box_sure_hit1(r, c)) & act;
     uint64_t amb = act & ~(hit | ballot(box_miss(c)));
@@ -253,7 +257,7 @@ struct HitState {
 // lanes that own a ray.  any_hit_dist > 0: shadow query — a lane stops as soon as its
 // bestT < dist (bestT only decreases, so the reference's final `hit && t < dist` is then
 // already true); the traversal order up to that point is the reference's.
-template <bool WIDE>
+template <bool WIDE, bool PK>
 __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const RayPre& r, bool active,
                                                    bool any_hit, float any_hit_dist, HitState& hs) {
     const uint32_t lane = lane_id();
@@ -270,7 +274,7 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
     RT_STAT(13 + so, __popcll(alive));
     // The root's pop-time test (SearchBVH tests every popped node, query.h:252-254) is made
     // here with the initial bestT, before the loop, so the loop never needs the root box.
-    const uint64_t root_mask = box_hit_mask(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
+    const uint64_t root_mask = box_hit_mask<PK>(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
     if (root_mask == 0) {
         if (!any_hit) RT_STAT(17, 1);
         return;
@@ -310,7 +314,7 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
             } else {
                 ob = own_box(sc, ref, false);
             }
-            mask = box_hit_mask(r, ob, hs.bestT, mask);
+            mask = box_hit_mask<PK>(r, ob, hs.bestT, mask);
             if (mask == 0) continue;
             act = (mask & lane_bit) != 0;
         }
@@ -353,7 +357,7 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
                 if (refs[k] == NO_REF) continue;
                 const float4 p = wv[(3 * k) / 2], q = wv[(3 * k) / 2 + 1];
                 const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
-                const uint64_t mk_ = box_hit_mask(r, bk, hs.bestT, mask);
+                const uint64_t mk_ = box_hit_mask<PK>(r, bk, hs.bestT, mask);
                 if (mk_ != 0) {
                     st_ref = wrlane(refs[k], sp, st_ref);
                     st_mlo = wrlane((uint32_t)mk_, sp, st_mlo);
@@ -369,7 +373,7 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
         const uint4 q3 = ldc_u(N + 3);
         const uint32_t lref = q3.x, rref = q3.y;
         if (lref != NO_REF) {
-            const uint64_t ml = box_hit_mask(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
+            const uint64_t ml = box_hit_mask<PK>(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
             if (ml != 0) {
                 st_ref = wrlane(lref, sp, st_ref);
                 st_mlo = wrlane((uint32_t)ml, sp, st_mlo);
@@ -379,7 +383,7 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
             }
         }
         if (rref != NO_REF) {
-            const uint64_t mr = box_hit_mask(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
+            const uint64_t mr = box_hit_mask<PK>(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
             if (mr != 0) {
                 st_ref = wrlane(rref, sp, st_ref);
                 st_mlo = wrlane((uint32_t)mr, sp, st_mlo);
@@ -446,7 +450,7 @@ template <int MODE>
 __device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, bool active, bool any_hit,
                                          float any_hit_dist, HitState& hs) {
     if constexpr (MODE == RT_KERNEL_LANE) traverse_lane(sc, r, active, any_hit, any_hit_dist, hs);
-    else traverse_wave_impl<(MODE & MODE_WIDE) != 0>(sc, r, active, any_hit, any_hit_dist, hs);
+    else traverse_wave_impl<(MODE & MODE_WIDE) != 0, (MODE & MODE_PACKED) != 0>(sc, r, active, any_hit, any_hit_dist, hs);
 }
 
 // Full hit record of the winning leaf (intersectTriangle's tail, query.h:110-130).
@@ -1927,8 +1931,9 @@ void launch_mode(const RenderParams& P, bool big, hipStream_t st) {
     const dim3 grid((P.tiles_virtual + 7) / 8 * 8);
     if (P.max_depth == 1) {
         if constexpr (SAMPLES && MODE != RT_KERNEL_LANE) {
-            if (big) {
-                hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES, true, 7>), grid, dim3(BLOCK), 0, st, P);
+            if (big) {  // 7 waves and packed box tests (c5: -4 % each; both slower on c3)
+                hipLaunchKernelGGL((render_tiles_kernel<MODE | MODE_PACKED, SAMPLES, true, 7>), grid, dim3(BLOCK), 0,
+                                   st, P);
                 return;
             }
         }

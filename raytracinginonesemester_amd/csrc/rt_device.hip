@@ -104,6 +104,7 @@ struct RenderParams {
     uint32_t* live_count;                             // [k * COUNTER_STRIDE], tile_cull_kernel
     int32_t* live_tiles;                              // nqueues lists of queue_cap entries
     int32_t* cand_tiles;  // tiles the root test keeps, for tile_cut_kernel (counter: live_count[8 * stride])
+    uint32_t* next_count; // the other counter set, zeroed by tile_cull_kernel for the next frame
     int32_t cut_force;    // test every candidate in tile_cut_kernel (no pass-through)
     int32_t nqueues;
     int32_t queue_cap;
@@ -855,8 +856,10 @@ __device__ __forceinline__ bool tile_misses_box_f(const TileDirsF& T, const floa
     return entry_min - exit_max > 1e-4f * (fabsf(entry_min) + fabsf(exit_max)) + abs_slack;
 }
 
+// The root test of tile_cull_kernel, one lane per tile: the float form (its bounds carry their
+// own rounding, see tile_dirs_f; 2x cheaper than the double form on the 129,600 c3 tiles).
 __device__ __forceinline__ bool tile_misses_root(const RenderParams& P, int x0, int x1, int y0, int y1) {
-    return tile_misses_box(tile_dirs(P, x0, x1, y0, y1), P.sc.root_box);
+    return tile_misses_box_f(tile_dirs_f(P, x0, x1, y0, y1), P.sc.root_box);
 }
 
 // What a sample that misses the root returns: clamp(0 + (1,1,1) * missColor) (query.h:181-183),
@@ -961,6 +964,10 @@ __device__ __forceinline__ void append_live(const RenderParams& P, bool live, in
 // straight to the live lists; with one they go to the candidate list for pass 2.
 __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
     const int tile = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    // Counters are double-buffered across frames (no reset launch): this frame's set was zeroed
+    // by the previous frame's pass; zero the other one for the next frame (the previous frame,
+    // its last user, finished before this kernel started: same stream).
+    if (blockIdx.x == 0 && threadIdx.x < 9) P.next_count[threadIdx.x * COUNTER_STRIDE] = 0u;
     bool live = false;
     if (tile < P.tiles_total) {
         const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
@@ -1610,7 +1617,7 @@ struct rt_scene {
     std::vector<float> jitter_host;
     // Ring of HIP event pairs around each render kernel, recorded on the launch stream.
     static constexpr int kRing = 256;
-    // ev0 | counter reset + tile_cull_kernel | evm | render kernel | ev1
+    // ev0 | tile_cull_kernel (+ tile_cut_kernel) | evm | render kernel | ev1
     hipEvent_t ev0[kRing] = {}, evm[kRing] = {}, ev1[kRing] = {};
     uint64_t launches = 0;
     size_t bytes = 0;
@@ -2089,19 +2096,24 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.nqueues = P.tile_order == RT_TILES_LINEAR ? 1 : 8;
     P.queue_cap = P.tiles_total;
     P.tiles_virtual = P.nqueues == 1 ? P.tiles_total : 8 * P.tiles_x * ((tiles_y + 7) / 8);
-    constexpr size_t kCounterBytes = 9 * COUNTER_STRIDE * sizeof(uint32_t);  // 8 live lists + candidates
+    // two counter sets (8 live lists + candidates each), alternating by frame
+    constexpr size_t kCounterBytes = 9 * COUNTER_STRIDE * sizeof(uint32_t);
     const size_t list_bytes = size_t(P.nqueues) * size_t(P.queue_cap) * sizeof(int32_t);
-    const size_t work_bytes = kCounterBytes + list_bytes + size_t(P.tiles_total) * sizeof(int32_t);
-    if (s->work.n < work_bytes && (rc = s->work.alloc(work_bytes)) != RT_OK) return rc;
-    P.live_count = static_cast<uint32_t*>(s->work.p);
-    s->last_tiles_total = P.tiles_total;
-    P.live_tiles = reinterpret_cast<int32_t*>(static_cast<char*>(s->work.p) + kCounterBytes);
-    P.cand_tiles = reinterpret_cast<int32_t*>(static_cast<char*>(s->work.p) + kCounterBytes + list_bytes);
-    const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
+    const size_t work_bytes = 2 * kCounterBytes + list_bytes + size_t(P.tiles_total) * sizeof(int32_t);
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (s->work.n < work_bytes) {
+        if ((rc = s->work.alloc(work_bytes)) != RT_OK) return rc;
+        HIP_TRY(hipMemsetAsync(s->work.p, 0, 2 * kCounterBytes, st));
+    }
+    const int set = int(s->launches & 1);
+    P.live_count = reinterpret_cast<uint32_t*>(static_cast<char*>(s->work.p) + set * kCounterBytes);
+    P.next_count = reinterpret_cast<uint32_t*>(static_cast<char*>(s->work.p) + (1 - set) * kCounterBytes);
+    s->last_tiles_total = P.tiles_total;
+    P.live_tiles = reinterpret_cast<int32_t*>(static_cast<char*>(s->work.p) + 2 * kCounterBytes);
+    P.cand_tiles = reinterpret_cast<int32_t*>(static_cast<char*>(s->work.p) + 2 * kCounterBytes + list_bytes);
+    const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
     const int slot = int(s->launches % rt_scene::kRing);
     HIP_TRY(hipEventRecord(s->ev0[slot], st));
-    HIP_TRY(hipMemsetAsync(s->work.p, 0, kCounterBytes, st));
     hipLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, P);
     HIP_TRY(hipGetLastError());
     if (P.cull && P.sc.ncut > 0) {
@@ -2145,7 +2157,9 @@ extern "C" int rt_live_tiles(const rt_scene* s, int64_t* live, int64_t* total) {
     const int slot = int((s->launches - 1) % rt_scene::kRing);
     HIP_TRY(hipEventSynchronize(s->ev1[slot]));
     uint32_t c[8 * COUNTER_STRIDE];
-    HIP_TRY(hipMemcpy(c, s->work.p, sizeof(c), hipMemcpyDeviceToHost));
+    const size_t set_bytes = 9 * COUNTER_STRIDE * sizeof(uint32_t);  // the last frame's counter set
+    HIP_TRY(hipMemcpy(c, static_cast<const char*>(s->work.p) + ((s->launches - 1) & 1) * set_bytes, sizeof(c),
+                      hipMemcpyDeviceToHost));
     for (int k = 0; k < 8; ++k) *live += c[k * COUNTER_STRIDE];
     return RT_OK;
 }

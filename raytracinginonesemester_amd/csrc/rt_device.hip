@@ -103,7 +103,7 @@ struct RenderParams {
     f3 miss_pixel;                                    // pixel value when all spp samples miss
     uint32_t* live_count;                             // [k * COUNTER_STRIDE], tile_cull_kernel
     int32_t* live_tiles;                              // nqueues lists of queue_cap entries
-    int32_t* cand_tiles;  // tiles the root test keeps, for tile_cut_kernel (counter: live_count[8 * stride])
+    uint8_t* cut_flag;    // per list slot: 1 = tile_cut_kernel culled the tile (read when sc.ncut > 0)
     uint32_t* next_count; // the other counter set, zeroed by tile_cull_kernel for the next frame
     int32_t cut_force;    // test every candidate in tile_cut_kernel (no pass-through)
     int32_t nqueues;
@@ -960,8 +960,7 @@ __device__ __forceinline__ void append_live(const RenderParams& P, bool live, in
     }
 }
 
-// Pass 1, one lane per tile: the root test.  Without a cut (sc.ncut == 0) the survivors go
-// straight to the live lists; with one they go to the candidate list for pass 2.
+// Pass 1, one lane per tile: the root test; the survivors go to the live lists.
 __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
     const int tile = (int)(blockIdx.x * BLOCK + threadIdx.x);
     // Counters are double-buffered across frames (no reset launch): this frame's set was zeroed
@@ -977,24 +976,16 @@ __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
         if (culled) write_culled_tile(P, tile, 0, 1);
         else live = true;
     }
-    if (P.cull && P.sc.ncut > 0) {
-        const uint32_t lane = lane_id();
-        const uint64_t m = ballot(live);
-        if (m == 0) return;
-        uint32_t base = 0;
-        if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(&P.live_count[8 * COUNTER_STRIDE], (uint32_t)__popcll(m));
-        base = rdlane(base, (uint32_t)__builtin_ctzll(m));
-        if (live) P.cand_tiles[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = tile;
-        return;
-    }
     append_live(P, live, tile);
 }
 
-// Pass 2, one wave per group of CUT_GROUP candidate tiles (in list order), one lane per box of the
-// cut (sc.cut, <= 64 boxes that hold every leaf exactly once): a tile is culled when every
-// lane proves its box missed by every ray of the tile (tile_misses_box_f), else it stays live.
-// The tile bounds are the same for every lane (a wave-uniform computation).  The group's live
-// tiles are appended together (lane j holds tile j): one atomic per (group, list).
+// Pass 2 (sc.ncut > 0), one wave per CUT_GROUP consecutive slots of a live list, one lane
+// per box of the cut (sc.cut, <= 64 boxes that hold every leaf exactly once): a tile is culled
+// when every lane proves its box missed by every ray of the tile (tile_misses_box_f; the tile
+// bounds are wave-uniform).  A culled tile gets its miss pixels here and the flag of its slot,
+// which the render block of that slot reads before anything else; the lists are not
+// compacted, so there are no atomics (appending the survivors to fresh lists cost c3 ~15 us of
+// counter contention).
 #ifndef RT_CUT_GROUP
 #define RT_CUT_GROUP 8
 #endif
@@ -1002,25 +993,32 @@ constexpr int CUT_GROUP = RT_CUT_GROUP;
 __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
     const uint32_t lane = lane_id();
     const int waves = (int)(gridDim.x * (BLOCK / 64));
-    const int n = (int)ldc_u32(&P.live_count[8 * COUNTER_STRIDE]);
-    // When the root box already covers more than a quarter of the image the scene fills the
-    // view and the cut rarely removes a tile (c5's heightfield: none of 739,248), so the
-    // candidates pass through untested (a speed choice only: passing is always exact).
+    int n = 0, max_len = 0;
+    for (int k = 0; k < P.nqueues; ++k) {
+        const int l = (int)ldc_u32(&P.live_count[k * COUNTER_STRIDE]);
+        n += l;
+        max_len = max(max_len, l);
+    }
+    // When the root test already keeps more than a quarter of the tiles the scene fills the
+    // view and the cut rarely removes one (c5's heightfield: none of 739,248): flags 0, no
+    // tests (a speed choice only: keeping a tile is always exact).
     const bool test = P.cut_force || 4 * (int64_t)n <= (int64_t)P.tiles_total;
-    // this lane's box of the cut, loaded once (the culled-tile stores below would otherwise make
-    // the compiler reload it for every tile)
+    // this lane's box of the cut, loaded once
     float box[6] = {0.f, 0.f, 0.f, -1.f, -1.f, -1.f};
-    if ((int)lane < P.sc.ncut) {
+    if (test && (int)lane < P.sc.ncut) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) box[i] = P.sc.cut[6 * (size_t)lane + i];
     }
-    // One group per wave, in dispatch order (the grid covers every possible candidate; waves
-    // past the list leave): the live lists keep the candidates' near-raster order, which the
-    // render kernel's L2 reuse depends on (a grid-stride loop here scrambles it: c5 +5 %).
-    for (int g = (int)(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64); CUT_GROUP * g < n; g += waves) {
-        const int m = min(CUT_GROUP, n - CUT_GROUP * g);
-        const int my_tile = (int)lane < m ? P.cand_tiles[CUT_GROUP * g + (int)lane] : -1;
-        uint64_t live = test ? 0ull : (m >= 64 ? ~0ull : (1ull << m) - 1ull);  // lanes >= m hold no tile
+    // (list q, group g) pairs, lists interleaved, each wave from its own index on
+    for (int p = (int)(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64);; p += waves) {
+        const int q = p % P.nqueues, g = p / P.nqueues;
+        if (CUT_GROUP * g >= max_len) break;
+        const int len = (int)ldc_u32(&P.live_count[q * COUNTER_STRIDE]);
+        if (CUT_GROUP * g >= len) continue;
+        const int m = min(CUT_GROUP, len - CUT_GROUP * g);
+        const size_t slot0 = (size_t)q * P.queue_cap + (size_t)(CUT_GROUP * g);
+        const int my_tile = (int)lane < m ? P.live_tiles[slot0 + lane] : -1;
+        uint64_t culled = 0;
         for (int j = 0; test && j < m; ++j) {
             const int tile = (int)rdlane((uint32_t)my_tile, (uint32_t)j);
             const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
@@ -1028,10 +1026,12 @@ __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
             const int xb = min(xa + P.tile_w, P.W) - 1, rb = min(ra + P.tile_h, P.rows) - 1;
             const TileDirsF T = tile_dirs_f(P, xa, xb, global_row(P, ra), global_row(P, rb));
             const bool hit = (int)lane < P.sc.ncut && !tile_misses_box_f(T, box);
-            if (ballot(hit) == 0) write_culled_tile(P, tile, (int)lane, 64);
-            else live |= 1ull << j;
+            if (ballot(hit) == 0) {
+                write_culled_tile(P, tile, (int)lane, 64);
+                culled |= 1ull << j;
+            }
         }
-        append_live(P, ((live >> lane) & 1ull) != 0, my_tile);
+        if ((int)lane < m) P.cut_flag[slot0 + lane] = (uint8_t)((culled >> lane) & 1ull);
     }
 }
 
@@ -1148,8 +1148,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
     const int b = (int)blockIdx.x;
     if (b >= P.tiles_virtual) return;
     const int q = P.nqueues == 1 ? 0 : (b & 7);
-    const int tile = planned_tile(P, list_length(P, q), q, P.nqueues == 1 ? b : (b >> 3));
+    const int i = P.nqueues == 1 ? b : (b >> 3);
+    const int tile = planned_tile(P, list_length(P, q), q, i);
     if (tile < 0) return;
+    if (P.sc.ncut > 0 && P.cut_flag[(size_t)q * P.queue_cap + i]) return;  // culled by tile_cut_kernel
     if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col, kpix);
     else pixels_tile<MODE, D1>(P, tile);
 }
@@ -2092,6 +2094,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.lane_samples = samples ? 1 : 0;
     P.tile_order = o->tile_order == RT_TILES_AUTO ? RT_TILES_ROWS : o->tile_order;
     P.cull = (o->flags & RT_FLAG_NO_CULL) ? 0 : 1;
+    if (!P.cull) P.sc.ncut = 0;  // the render kernel reads the cut flags only when the cut pass ran
     P.miss_pixel = miss_pixel_value(o);
     P.nqueues = P.tile_order == RT_TILES_LINEAR ? 1 : 8;
     P.queue_cap = P.tiles_total;
@@ -2099,7 +2102,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // two counter sets (8 live lists + candidates each), alternating by frame
     constexpr size_t kCounterBytes = 9 * COUNTER_STRIDE * sizeof(uint32_t);
     const size_t list_bytes = size_t(P.nqueues) * size_t(P.queue_cap) * sizeof(int32_t);
-    const size_t work_bytes = 2 * kCounterBytes + list_bytes + size_t(P.tiles_total) * sizeof(int32_t);
+    const size_t work_bytes = 2 * kCounterBytes + list_bytes + size_t(P.nqueues) * size_t(P.queue_cap);
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (s->work.n < work_bytes) {
         if ((rc = s->work.alloc(work_bytes)) != RT_OK) return rc;
@@ -2110,14 +2113,15 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.next_count = reinterpret_cast<uint32_t*>(static_cast<char*>(s->work.p) + (1 - set) * kCounterBytes);
     s->last_tiles_total = P.tiles_total;
     P.live_tiles = reinterpret_cast<int32_t*>(static_cast<char*>(s->work.p) + 2 * kCounterBytes);
-    P.cand_tiles = reinterpret_cast<int32_t*>(static_cast<char*>(s->work.p) + 2 * kCounterBytes + list_bytes);
+    P.cut_flag = reinterpret_cast<uint8_t*>(static_cast<char*>(s->work.p) + 2 * kCounterBytes + list_bytes);
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
     const int slot = int(s->launches % rt_scene::kRing);
     HIP_TRY(hipEventRecord(s->ev0[slot], st));
     hipLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, P);
     HIP_TRY(hipGetLastError());
     if (P.cull && P.sc.ncut > 0) {
-        const int cut_blocks = std::max(1, (P.tiles_total + 4 * CUT_GROUP - 1) / (4 * CUT_GROUP));
+        // 16 waves per CU; each takes (list, group) pairs grid-stride (c3: about one each)
+        const int cut_blocks = 4 * s->cus;
         hipLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, st, P);
         HIP_TRY(hipGetLastError());
     }

@@ -1136,10 +1136,14 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
 // without the loop.)
 // WAVES: waves per SIMD the kernel is compiled for.  6 (80 VGPRs) is fastest for scenes whose
 // nodes stay in L2 (c3: 6 > 5, 7 > 4 waves); scenes far larger than the L2s (c5, 345 MB) gain
-// from one more wave of latency hiding despite more spills (7: -4 % on c5), so the depth-1
-// sample kernels are also built for 7 (launch picks by scene size, big_scene_waves).
+// from more waves of latency hiding despite more spills, so the depth-1 sample kernels are
+// also built for RT_BIG_WAVES with packed box tests (c5: 8 waves 94.5 ms < 7 waves 96.4 <
+// 6 waves 99.9; launch picks by scene size, big_scene_waves).
 #ifndef RT_RENDER_WAVES
 #define RT_RENDER_WAVES 6
+#endif
+#ifndef RT_BIG_WAVES
+#define RT_BIG_WAVES 8
 #endif
 template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES>
 __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
@@ -1940,9 +1944,9 @@ void launch_mode(const RenderParams& P, bool big, hipStream_t st) {
     const dim3 grid((P.tiles_virtual + 7) / 8 * 8);
     if (P.max_depth == 1) {
         if constexpr (SAMPLES && MODE != RT_KERNEL_LANE) {
-            if (big) {  // 7 waves and packed box tests (c5: -4 % each; both slower on c3)
-                hipLaunchKernelGGL((render_tiles_kernel<MODE | MODE_PACKED, SAMPLES, true, 7>), grid, dim3(BLOCK), 0,
-                                   st, P);
+            if (big) {  // more waves and packed box tests (c5 faster with each; both slower on c3)
+                hipLaunchKernelGGL((render_tiles_kernel<MODE | MODE_PACKED, SAMPLES, true, RT_BIG_WAVES>), grid,
+                                   dim3(BLOCK), 0, st, P);
                 return;
             }
         }

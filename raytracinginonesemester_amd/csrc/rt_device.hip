@@ -1062,8 +1062,23 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
         const int s = t & (P.spp - 1);  // spp and tile_w are powers of two here
         const int pit = t >> P.spp_log2;
         const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-        const int x = tx * P.tile_w + (pit & (P.tile_w - 1));
-        const int r = ty * P.tile_h + (pit >> P.tile_w_log2);
+#ifndef RT_ROW_PIXELS
+        // Pixels in Z order inside a square tile (a wave's pixels form a square: 2x2 at 16 spp,
+        // more coherent rays than a row of 4); row-major otherwise.  Any order gives the same
+        // image: each sample is independent and each pixel's samples stay consecutive lanes.
+        int px, py;
+        if (P.tile_w == P.tile_h) {
+            px = (pit & 1) | ((pit >> 1) & 2) | ((pit >> 2) & 4) | ((pit >> 3) & 8);
+            py = ((pit >> 1) & 1) | ((pit >> 2) & 2) | ((pit >> 3) & 4) | ((pit >> 4) & 8);
+        } else {
+            px = pit & (P.tile_w - 1);
+            py = pit >> P.tile_w_log2;
+        }
+#else
+        const int px = pit & (P.tile_w - 1), py = pit >> P.tile_w_log2;
+#endif
+        const int x = tx * P.tile_w + px;
+        const int r = ty * P.tile_h + py;
         const bool valid = x < P.W && r < P.rows;
         const int y = valid ? global_row(P, r) : 0;
         const int pix = valid ? r * P.W + x : -1;

@@ -36,7 +36,7 @@ cam = hs.camera(cfg["width"], cfg["height"])
 builds = []
 for spec in a.libs:
     name, path = spec.split("=", 1) if "=" in spec else (spec, spec)
-    _lib.LIB_PATH = _lib.PKG / "lib" / "librt_mi355x.so" if name == "default" and path == "default" else Path(path)
+    _lib.LIB_PATH = _lib.PKG / "lib" / "librt_mi355x.so" if path == "default" else Path(path)
     _lib._lib = None
     h = _lib.lib()
     builds.append((name, h, rt.DeviceScene.from_host(hs)))

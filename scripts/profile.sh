@@ -5,7 +5,7 @@
 # usage: scripts/profile.sh <tag> [bench args...]
 set -u
 TAG=${1:-r01}; shift || true
-ARGS=${*:-"--steps 5 --warmup 1"}
+ARGS=${*:-"--steps 20 --warmup 3"}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"

@@ -819,8 +819,10 @@ __device__ __forceinline__ TileDirsF tile_dirs_f(const RenderParams& P, int x0, 
     for (int a = 0; a < 3; ++a) {
         T.Dl[a] -= 1.1e-5f * T.scale;
         T.Dh[a] += 1.1e-5f * T.scale;
-        T.iDl[a] = 1.0f / T.Dl[a];
-        T.iDh[a] = 1.0f / T.Dh[a];
+        // v_rcp_f32 (1 ulp): far inside the 1e-4 decision slack, and ~10x cheaper than the
+        // correctly rounded division
+        T.iDl[a] = rcp_approx(T.Dl[a]);
+        T.iDh[a] = rcp_approx(T.Dh[a]);
     }
     T.usable = T.scale > 0.0f && T.scale < 1e30f;
     return T;

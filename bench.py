@@ -276,6 +276,11 @@ def main():
                    "kernel": a.kernel},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     # measured HBM-side bytes per launch over the kernel time: the scene is
+                     # L2-resident and nodes are fetched once per wave, so this sits far below
+                     # the algorithmic rate (the kernel is VALU- / latency-bound)
+                     "traffic_gbs": (round(traffic / (kernel_ms / 1e3) / 1e9, 2) if traffic else None),
+                     "traffic_frac": (round(traffic / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5) if traffic else None),
                      "kernel": "render_tiles_kernel", "kernel_ms": round(kernel_ms, 4),
                      "frame_ms": round(frame_ms, 4), "algorithmic_bytes_per_sample": round(B, 3)},
         "p6_epilogue_ms": round((te1 - te0) * 1e3, 3),

@@ -245,7 +245,7 @@ def main():
     achieved = B * per_gpu_samples / (kernel_ms / 1e3) / 1e9  # GB/s of the dominant kernel
     traffic = None
     tf = Path(a.traffic_file)
-    if tf.exists():
+    if tf.exists() and world == 1:  # measured for the 1-GPU launch of this config
         try:
             traffic = json.loads(tf.read_text()).get(a.config, {}).get("bytes_per_launch")
         except Exception:

@@ -382,3 +382,30 @@ def test_720p_frame_rows_against_oracle(spp):
     ref = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,
                        hs.tri_object_ids, hs.materials, hs.lights, spp=spp, max_depth=1, rows=(352, 368))
     _check_fb(b[0][352:368], ref[352:368])
+
+
+@pytest.mark.parametrize("scene", ["frog.json", "cornell.json", "sphere_single.json"])
+def test_cut_culling_fuzz_grazing_cameras(scene, monkeypatch):
+    """The float tile bounds of both culling passes (root box and 64-box cut) against many
+    cameras aimed at box faces, edges and corners from near and far, with tiny and wide fields
+    of view: culled frames are bit-identical to unculled ones."""
+    monkeypatch.setenv("RT_CULL_COVERAGE", "1.0")
+    hs = host_scene(scene)
+    ds = _device_scene(scene)
+    box = np.concatenate([hs.aabbs[0, :3], hs.aabbs[0, 3:]]).astype(np.float64)
+    lo, hi = box[:3], box[3:]
+    ext = float(np.linalg.norm(hi - lo))
+    rng = np.random.default_rng(2024)
+    for k in range(40):
+        # a point on a face / edge / corner of the root box or of a random sub-box
+        t = rng.choice([0.0, 1.0, 0.5, rng.uniform()], size=3)
+        target = lo + t * (hi - lo)
+        dirn = rng.normal(size=3)
+        dirn /= np.linalg.norm(dirn)
+        pos = target + dirn * ext * rng.choice([0.05, 0.6, 3.0, 50.0])
+        up = (0.0, 0.0, 1.0) if abs(dirn[2]) < 0.9 else (0.0, 1.0, 0.0)
+        cam = rt.Camera(tuple(pos), tuple(target), up, float(rng.choice([8.0, 35.0, 600.0])), 24.0, 80, 48)
+        a = ds.render(cam, spp=4, max_depth=1, aov=True)
+        b = ds.render(cam, spp=4, max_depth=1, aov=True, flags=rt._lib.RT_FLAG_NO_CULL)
+        for x, y in zip(a, b):
+            assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), k

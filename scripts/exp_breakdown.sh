@@ -4,4 +4,4 @@ set -e
 A="default=default noshade=build/variants/noshade/librt_mi355x.so noshadow=build/variants/noshadow/librt_mi355x.so rootonly=build/variants/rootonly/librt_mi355x.so"
 echo "== c3"; timeout -k 10 200 python scripts/ab_libs.py --no-check --config c3 --rounds 7 --reps 5 $A
 echo "== c5"; timeout -k 10 300 python scripts/ab_libs.py --no-check --config c5 --rounds 2 --reps 2 $A
-echo "== tpb"; timeout -k 10 200 python scripts/sweep.py --kernels wave --tiles rows --tpb 1,2,4,8,16 --rounds 3 --reps 5
+

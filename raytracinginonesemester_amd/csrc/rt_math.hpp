@@ -48,7 +48,7 @@ struct BoxP {
 };
 
 // Relative slack of the float pre-classification (see box_classify).
-constexpr float kBoxRel = 4e-6f;
+constexpr float kBoxRel = 1e-6f;
 
 // A ray as the slab test needs it.  `par` bit a: |dir[a]| < 1e-8f, where intersectAABB
 // degenerates to an exact inside test on that axis (bvh.h:90-91).  iv is a float reciprocal
@@ -166,7 +166,9 @@ __host__ __device__ inline bool box_hit_exact(const RayPre& r, const BoxP& b, do
 // 1.8e-7 |t| + 2.4e-7 |oiv| + 1.2e-7 E (+ 6e-8 (|t| + 3E) for the +-2E steps); the reference's
 // double tNear/tFar are within
 // 3.4e-16 |t| of t.  E = kBoxRel (2 |oiv| + bmax |iv|) + 1e-30 >= kBoxRel (|t| + |oiv|)
-// (|t| <= |b| |iv| + |oiv|) with kBoxRel = 4e-6 covers both with > 10x slack; the 1e-30 term
+// (|t| <= |b| |iv| + |oiv|) with kBoxRel = 1e-6 covers both with > 4x slack (the error is
+// <= 2.4e-7 (|t| + |oiv|) + 3e-7 E <= 0.25 E; 4e-6 had 16x, but 4x more of the box tests fell
+// to the double path: c3 -2 %, c5 -4 % at 1e-6); the 1e-30 term
 // covers subnormal absolute error.  So lowLo <= exact lo <= lowHi and highLo <= exact hi <=
 // highHi per axis, and with Lmax / Hmin the reference's max of lows / min of highs (tmin and
 // tmax exact in both precisions):

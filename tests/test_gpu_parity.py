@@ -409,3 +409,15 @@ def test_cut_culling_fuzz_grazing_cameras(scene, monkeypatch):
         b = ds.render(cam, spp=4, max_depth=1, aov=True, flags=rt._lib.RT_FLAG_NO_CULL)
         for x, y in zip(a, b):
             assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), k
+
+
+def test_hw1_timing_entry_point():
+    """rt_render_hw1_ex with kernel timing: a positive device time and the same image."""
+    c = configs.HW1_CONFIGS["c1"]
+    mesh = rt.MeshHW1(configs.MESHES / c["mesh"])
+    cam = rt.Camera(c["position"], c["look_at"], c["up"], c["focal_mm"], c["sensor_mm"], 64, 64, hw1=True)
+    args = (mesh.positions, mesh.normals, mesh.indices, cam, c["light_pos"], c["light_color"])
+    rgb, ms = rt.render_hw1(*args, timing=True)
+    rgb_b, ms_b = rt.render_hw1(*args, timing=True, brute=True)
+    assert ms > 0 and ms_b > 0
+    assert np.array_equal(rgb.view(np.uint32), rgb_b.view(np.uint32))

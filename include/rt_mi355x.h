@@ -288,10 +288,12 @@ int rt_box_test_host(const float* rays, const float* boxes, const float* tminmax
  * rt_render_device calls on this scene, oldest first, measured with HIP events recorded
  * on the launch stream around the kernel.  Waits for those launches to finish. */
 int rt_kernel_times(const rt_scene* s, float* ms_out, int max, int* n_out);
-/* The same for the whole device frame: list reset, tile cull pre-pass and render kernel. */
+/* The same for the whole device frame: the root-box cull pass, the tree-cut cull pass (when it
+ * runs) and the render kernel. */
 int rt_frame_times(const rt_scene* s, float* ms_out, int max, int* n_out);
-/* Pixel tiles of the most recent rt_render_device call that survived the root-box cull
- * (traced), and all tiles.  Waits for that call to finish. */
+/* Pixel tiles of the most recent rt_render_device call that survived the root-box cull, and
+ * all tiles (the tree-cut pass may still cull some of the survivors; those are flagged, not
+ * removed from the lists).  Waits for that call to finish. */
 int rt_live_tiles(const rt_scene* s, int64_t* live, int64_t* total);
 
 int rt_device_count(int* n);

@@ -47,8 +47,8 @@ BAND_ROWS = 8
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)  # ~35 ms of frames: a steadier average
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(configs.G_CONFIGS))
     ap.add_argument("--kernel", default="auto", choices=["auto", "wave", "lane"])
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -1,21 +1,25 @@
 #!/usr/bin/env python3
 """Headline benchmark: Mrays/s (camera samples/s) of the per-pixel ray path at
-1920x1080x16 spp on the frog scene (BASELINE.json configs[2]; c4 when N > 1).
+1920x1080x16 spp on the frog scene (BASELINE.json configs[2]; c4 when N > 1), counting frames
+that reached host memory.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c5] [--kernel wave|lane]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c5] [--deliver p6|f32]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N ...
 
-A step = one full frame delivered on rank 0: every rank renders its image bands (rows cut
-into 8-row bands, band b -> rank b % N) with the HIP kernels into device memory, which also
-write the strip's P6 samples (write_p6 semantics, fused into the render and cull kernels); the
-byte strips are gathered to
-rank 0 over RCCL (torch.distributed, backend "nccl") and un-permuted there on the GPU
-(--gather f32 gathers the float strips instead).  With two strip buffers the gather of
-frame k overlaps the render of frame k+1, and all K gathers finish inside the timed region.
-Scene upload and BVH build are
-outside the timed region (as G/src/main.cu:362-378 times only render()).  Inputs are
-resident in HBM when timing starts.  Rank 0 prints one JSON line.
+A step = one full frame delivered to rank 0's host memory, as the reference's timed region
+is render() plus the device-to-host copy of the frame (G/src/main.cu:369-376).  The native
+frame renderer (rt_renderer, include/rt_mi355x.h) does it: every rank renders its 8-row bands
+(band b -> rank b % N) with the HIP kernels, which write the strip's P6 samples themselves
+(write_p6, fused epilogue); the strips reach rank 0 over RCCL (grouped ncclSend/ncclRecv,
+xGMI) and rank 0 copies them into a pinned host frame with 2-D copies that place each band at
+its rows.  Frames are pipelined 3 deep: frame k+1 renders while frame k is gathered and
+copied.  Every timed frame is waited for in host memory before the clock stops.
+--deliver f32 delivers the float framebuffer (the reference's own payload, 4x the bytes).
+--comm torch keeps the older torch.distributed gather (nccl or gloo) as an alternate launcher.
+
+Scene upload and BVH build are outside the timed region (as G/src/main.cu:362-378 times only
+render() + copy).  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -42,6 +46,7 @@ from raytracinginonesemester_amd import configs  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 BAND_ROWS = 8
+METRIC = "Mrays/s at 1920x1080x16spp (1/2/4/8 GPU) + PPM max-abs pixel diff"
 
 
 def parse():
@@ -51,35 +56,60 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(configs.G_CONFIGS))
     ap.add_argument("--kernel", default="auto", choices=["auto", "wave", "lane"])
+    ap.add_argument("--deliver", default="p6", choices=["p6", "f32"])
+    ap.add_argument("--gather", default="auto", choices=["auto", "rccl", "direct"])
+    ap.add_argument("--depth", type=int, default=3)
+    ap.add_argument("--comm", default="native", choices=["native", "torch"],
+                    help="native: rt_renderer (RCCL inside librt_mi355x); torch: torch.distributed gather")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="--comm torch only. gloo: CPU-staged gather (lets N ranks share one GPU)")
+    ap.add_argument("--gather-payload", default="p6", choices=["p6", "f32"], help="--comm torch only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="gloo: CPU-staged gather (lets N ranks share one GPU to exercise the N>1 path)")
-    ap.add_argument("--gather", default="p6", choices=["p6", "f32"],
-                    help="what a step delivers on rank 0: p6 = the frame's P6 samples (each rank quantises "
-                         "its strip on its GPU, the bytes are gathered and un-permuted; SURVEY.md §8(f) #3), "
-                         "f32 = the float framebuffer strips")
+    ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
     ap.add_argument("--traffic-file", default=str(REPO / "profiles" / "traffic.json"),
-                    help="per-launch HBM bytes measured by rocprofv3 --pmc (see DESIGN.md)")
+                    help="per-launch HBM bytes and issue counters measured by rocprofv3 --pmc (DESIGN.md §5)")
     return ap.parse_args()
+
+
+# ---- CPU baseline -----------------------------------------------------------------------
+def usable_cores() -> dict:
+    """Cores this process may run on: the affinity mask, capped by a cgroup CPU quota."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(per))))
+    except Exception:
+        pass
+    model = platform.processor() or platform.machine()
+    try:
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    usable = min(aff, quota) if quota else aff
+    return {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota, "usable": usable, "model": model}
 
 
 def cpu_baseline(hs, cam, cfg) -> dict:
     """The oracle restatement (bit-exact to the reference build, tests/test_oracle.py) timed on
-    this host's cores over the full frame, plus the reference's own CPU render() built from its
-    sources (oracle/_ref/ref_g, 1 thread, as shipped) when present."""
+    every usable core of this host on a bounded sample of the frame, plus the HW1 C1 CPU path
+    and, when present, the reference's own CPU render() built from its sources (1 thread)."""
     from oracle import pyoracle as orc
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    cores = usable_cores()
+    threads = cores["usable"]
     b = cam.basis()
     oc = orc.camera_from_basis(b["center"], b["pixel00_loc"], b["pixel_delta_u"], b["pixel_delta_v"],
                                cam.pixel_width, cam.pixel_height)
-    # bounded sample: a band of rows through the frame centre (the frog), then all rows for c3
     H, W, spp = cam.pixel_height, cam.pixel_width, cfg["spp"]
     rows = (0, H) if cfg is configs.G_CONFIGS["c3"] else (H // 2 - 32, H // 2 + 32)
-    # repeat the sample until ~10 s of CPU work (at least once), so the rate is not a blip
     reps, t0 = 0, time.perf_counter()
-    while True:
+    while True:  # repeat the sample until ~10 s of CPU work (at least once)
         orc.render_g(hs.num_triangles, oc, hs.nodes, hs.aabbs, hs.triangles, hs.tri_object_ids, hs.materials,
                      hs.lights, spp=spp, max_depth=cfg["max_depth"], miss=hs.settings["miss_color"], rows=rows,
                      threads=threads)
@@ -89,8 +119,31 @@ def cpu_baseline(hs, cam, cfg) -> dict:
     dt = time.perf_counter() - t0
     n = (rows[1] - rows[0]) * W * spp * reps
     out = {"value": n / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-           "sample": f"oracle/rt_oracle.c (bit-exact restatement) rows {rows[0]}..{rows[1]} of "
-                     f"{W}x{H}x{spp}, {reps} pass(es), {n} samples, {dt:.2f} s, OpenMP {threads} threads"}
+           "sample": f"oracle/rt_oracle.c (bit-exact restatement of G/ render()) rows {rows[0]}..{rows[1]} of "
+                     f"{W}x{H}x{spp}, {reps} pass(es), {n} samples, {dt:.2f} s, OpenMP {threads} threads",
+           "host": cores}
+    # HW1 CPU path (north_star: "the HW1 CPU path timed on the same box's host cores"): C1
+    try:
+        c1 = configs.HW1_CONFIGS["c1"]
+        mesh = rt.MeshHW1(configs.MESHES / c1["mesh"])
+        hcam = orc.camera(c1["position"], c1["look_at"], c1["up"], c1["focal_mm"], c1["sensor_mm"], c1["width"],
+                          c1["height"], hw1=True)
+        hw1 = {}
+        for th in (1, threads):
+            reps1, t1 = 0, time.perf_counter()
+            while True:
+                orc.render_hw1(mesh.positions, mesh.normals, mesh.indices, hcam, c1["light_pos"], c1["light_color"],
+                               spp=c1["spp"], threads=th)
+                reps1 += 1
+                if time.perf_counter() - t1 >= 2.0:
+                    break
+            d1 = time.perf_counter() - t1
+            hw1[f"{th}_threads"] = round(c1["width"] * c1["height"] * c1["spp"] * reps1 / d1 / 1e6, 4)
+        out["hw1_c1"] = {"unit": "Mrays/s", **hw1,
+                         "sample": "C1: HW1 brute force (HW1/src/render.cpp:72-116), sphere 960 tris, 256x256x1spp, "
+                                   "oracle restatement"}
+    except Exception as e:  # pragma: no cover - reported, not fatal
+        out["hw1_c1"] = {"error": repr(e)}
     ref = REPO / "oracle" / "_ref" / "ref_g"
     if ref.exists() and cfg is configs.G_CONFIGS["c3"]:
         with tempfile.TemporaryDirectory() as td:
@@ -103,8 +156,205 @@ def cpu_baseline(hs, cam, cfg) -> dict:
                     "value": W * H * spp / (ms / 1e3) / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "reference",
                     "sample": "G/ render() CPU branch built from /root/reference sources (oracle/_ref/ref_g), "
                               f"full frame, per-pixel jitter rebuild as shipped, {ms / 1e3:.2f} s"}
-    out["host_cpu"] = platform.processor() or platform.machine()
     return out
+
+
+# ---- timing helpers ----------------------------------------------------------------------
+def sync_all(dev, world):
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+
+def max_over_ranks(vals, world):
+    t = torch.tensor(vals, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
+
+
+def run_frames(r, cam, opts, n, depth):
+    """Submit n frames, waiting for every one of them (host memory on rank 0)."""
+    pend = []
+    last = None
+    for _ in range(n):
+        pend.append(r.submit(cam, opts))
+        if len(pend) >= depth:
+            last = r.wait(pend.pop(0))
+    for t in pend:
+        last = r.wait(t)
+    return last
+
+
+def timed_native(r, cam, opts, steps, warmup, depth, dev, world):
+    run_frames(r, cam, opts, warmup, depth)
+    sync_all(dev, world)
+    t0 = time.perf_counter()
+    last = run_frames(r, cam, opts, steps, depth)
+    sync_all(dev, world)
+    t1 = time.perf_counter()
+    return t1 - t0, last
+
+
+def native(a, hs, cam, cfg, world, rank, local, dev):
+    spp = cfg["spp"]
+    kernel = {"auto": rt.RT_KERNEL_AUTO, "wave": rt.RT_KERNEL_WAVE, "lane": rt.RT_KERNEL_LANE}[a.kernel]
+    opts, _jit = rt.DeviceScene.make_opts(spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
+                                          kernel=kernel)
+    gather = {"auto": rt.RT_GATHER_AUTO, "rccl": rt.RT_GATHER_RCCL, "direct": rt.RT_GATHER_DIRECT}[a.gather]
+
+    def make(deliver, depth=a.depth):
+        uid = None
+        if world > 1:
+            obj = [rt.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            uid = obj[0]
+        return rt.Renderer.from_host(hs, devices=(local,), world_size=world, rank0=rank, unique_id=uid,
+                                     band_rows=BAND_ROWS, deliver=deliver, gather=gather, depth=depth)
+
+    deliver = rt.RT_DELIVER_F32 if a.deliver == "f32" else rt.RT_DELIVER_P6
+    r = make(deliver)
+    elapsed, last = timed_native(r, cam, opts, a.steps, a.warmup, a.depth, dev, world)
+    sc = r.scene(0)
+    kt, ft = sc.kernel_times(a.steps), sc.frame_times(a.steps)
+    res = {"elapsed": elapsed,
+           "kernel_ms": float(kt.mean()) if len(kt) else float("nan"),
+           "frame_ms": float(ft.mean()) if len(ft) else float("nan"),
+           "live_tiles": list(sc.live_tiles())}
+    if rank == 0:
+        g, d, f = (r.times(k, a.steps) for k in (rt.RT_TIME_GATHER, rt.RT_TIME_DELIVER, rt.RT_TIME_FRAME))
+        res.update(gather_ms=float(g.mean()), deliver_ms=float(d.mean()), frame_latency_ms=float(f.mean()))
+        addr, n = last
+        res["frame_bytes"] = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_uint8 * n).from_address(addr)).tobytes()
+    res["gather_path"] = "rccl" if (world > 1 and a.gather != "direct") else "direct (own strip to host)"
+    r.close()
+    if a.no_extras:
+        return res
+    # secondary: render only (strips stay in HBM), the rate the round-1 bench reported
+    rn = make(rt.RT_DELIVER_NONE)
+    el, _ = timed_native(rn, cam, opts, a.steps, a.warmup, a.depth, dev, world)
+    res["render_only_s"] = el
+    rn.close()
+    # secondary: the other payload (f32 = the reference's Vec3 framebuffer), also the float parity
+    other = rt.RT_DELIVER_P6 if deliver == rt.RT_DELIVER_F32 else rt.RT_DELIVER_F32
+    ro = make(other)
+    el, last_o = timed_native(ro, cam, opts, max(10, a.steps // 4), 2, a.depth, dev, world)
+    res["other_payload"] = {"deliver": "p6" if other == rt.RT_DELIVER_P6 else "f32", "s": el,
+                            "steps": max(10, a.steps // 4)}
+    if rank == 0:
+        addr, n = last_o
+        res["other_bytes"] = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_uint8 * n).from_address(addr)).tobytes()
+    ro.close()
+    return res
+
+
+def band_shards(hs, cam, cfg, local, steps=20):
+    """Each rank's share of a frame at N = 2/4/8, rendered alone on this GPU (the per-rank
+    compute a multi-GPU run will show): frame_ms (cull + cut + render) and kernel_ms."""
+    ds = rt.DeviceScene.from_host(hs, device=local)
+    H, W = cam.pixel_height, cam.pixel_width
+    p6 = torch.zeros((H * W * 3,), dtype=torch.uint8, device=torch.device("cuda", local))
+    out = {}
+    for n in (2, 4, 8):
+        per = []
+        for r in range(n):
+            o, _j = ds.make_opts(spp=cfg["spp"], max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
+                                 band_rows=BAND_ROWS, band_index=r, band_count=n)
+            for _ in range(3 + steps):
+                ds.render_device(cam, o, 0, stream=None, p6_dev_ptr=p6.data_ptr())
+            torch.cuda.synchronize()
+            per.append((float(ds.frame_times(steps).mean()), float(ds.kernel_times(steps).mean())))
+        fr = [p[0] for p in per]
+        out[str(n)] = {"frame_ms": [round(x, 4) for x in fr], "kernel_ms": [round(p[1], 4) for p in per],
+                       "max_over_mean": round(max(fr) / (sum(fr) / len(fr)), 4)}
+    ds.close()
+    return out
+
+
+# ---- the torch.distributed launcher (alternate path, round 1) ----------------------------
+def torch_path(a, hs, cam, cfg, world, rank, local, dev):
+    """Per step: render (fused P6) into a device strip; world > 1: torch.distributed.gather of
+    the strips to rank 0 (async, two buffers), un-permute on rank 0's GPU, then the frame's
+    bytes copied to host memory on rank 0."""
+    W, H, spp = cam.pixel_width, cam.pixel_height, cfg["spp"]
+    kernel = {"auto": rt.RT_KERNEL_AUTO, "wave": rt.RT_KERNEL_WAVE, "lane": rt.RT_KERNEL_LANE}[a.kernel]
+    ds = rt.DeviceScene.from_host(hs, device=local)
+    opts, _jit = ds.make_opts(spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
+                              band_rows=BAND_ROWS, band_index=rank, band_count=world, kernel=kernel)
+    lib = rt._lib.lib()
+    max_rows = max(lib.rt_shard_rows(H, BAND_ROWS, r, world) for r in range(world))
+    p6 = a.gather_payload == "p6"
+    rb = W * 3 * (1 if p6 else 4)
+    strips = [torch.zeros((max_rows, rb), dtype=torch.uint8, device=dev) for _ in range(2)]
+    gdev = dev if a.backend == "nccl" else torch.device("cpu")
+    gathers = [torch.empty((world, max_rows, rb), dtype=torch.uint8, device=gdev)
+               if (world > 1 and rank == 0) else None for _ in range(2)]
+    frame_dev = torch.empty((H, rb), dtype=torch.uint8, device=dev) if rank == 0 else None
+    host = [torch.empty((H, rb), dtype=torch.uint8).pin_memory() for _ in range(2)] if rank == 0 else None
+    pending = [None, None]
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    frames = [0]
+
+    def finish(b):
+        if pending[b] is None:
+            return
+        if world > 1:
+            pending[b].wait()
+        pending[b] = None
+        if rank == 0:
+            if world > 1:
+                g = gathers[b] if a.backend == "nccl" else gathers[b].to(dev)
+                rt.unpermute_strips_device(g.data_ptr(), max_rows, rb, H, BAND_ROWS, world, frame_dev.data_ptr(),
+                                           False, stream)
+                host[b].copy_(frame_dev)
+            else:
+                host[b].copy_(strips[b][:H])
+
+    def step():
+        b = frames[0] & 1
+        frames[0] += 1
+        finish(b)
+        s = strips[b]
+        if p6:
+            ds.render_device(cam, opts, 0, stream=stream, p6_dev_ptr=s.data_ptr())
+        else:
+            ds.render_device(cam, opts, s.data_ptr(), stream=stream)
+        if world > 1:
+            src = s if a.backend == "nccl" else s.cpu()
+            pending[b] = dist.gather(src, gather_list=list(gathers[b].unbind(0)) if rank == 0 else None, dst=0,
+                                     async_op=True)
+        else:
+            pending[b] = True
+
+    def drain():
+        for b in ((frames[0]) & 1, (frames[0] + 1) & 1):
+            finish(b)
+
+    for _ in range(a.warmup):
+        step()
+    drain()
+    sync_all(dev, world)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    drain()
+    sync_all(dev, world)
+    t1 = time.perf_counter()
+    kt, ft = ds.kernel_times(a.steps), ds.frame_times(a.steps)
+    res = {"elapsed": t1 - t0, "kernel_ms": float(kt.mean()), "frame_ms": float(ft.mean()),
+           "live_tiles": list(ds.live_tiles()), "gather_path": f"torch.distributed.gather ({a.backend})"}
+    if rank == 0:
+        res["frame_bytes"] = host[(frames[0] - 1) & 1].numpy().tobytes()
+    ds.close()
+    return res
+
+
+def load_traffic(path: Path, config: str):
+    try:
+        return json.loads(path.read_text()).get(config)
+    except Exception:
+        return None
 
 
 def main():
@@ -119,7 +369,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        if a.backend == "nccl":
+        # control plane (barriers, max over ranks, the RCCL id) over gloo; the frame data moves
+        # over the renderer's own RCCL communicator (or torch's nccl group with --comm torch)
+        if a.comm == "torch" and a.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
@@ -129,114 +381,32 @@ def main():
     hs = rt.HostScene.load_json(sp, REPO if sp.parent == configs.SCENES else sp.parent)
     cam = hs.camera(cfg["width"], cfg["height"])
     W, H, spp = cam.pixel_width, cam.pixel_height, cfg["spp"]
-    kernel = {"auto": rt.RT_KERNEL_AUTO, "wave": rt.RT_KERNEL_WAVE, "lane": rt.RT_KERNEL_LANE}[a.kernel]
-    ds = rt.DeviceScene.from_host(hs, device=local)
-    opts, _jit = ds.make_opts(spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
-                              band_rows=BAND_ROWS, band_index=rank, band_count=world, kernel=kernel)
-    lib = rt._lib.lib()
-    rows_of = [lib.rt_shard_rows(H, BAND_ROWS, r, world) for r in range(world)]
-    max_rows = max(rows_of)
-    # Two strip buffers: frame k+1 renders while frame k's strips are gathered (the collective
-    # runs on its own stream; before a buffer is rendered into again, the current stream waits
-    # for that buffer's previous gather — a stream dependency, the host does not block).
-    strips = [torch.zeros((max_rows, W, 3), dtype=torch.float32, device=dev) for _ in range(2)]
-    p6 = a.gather == "p6"
-    rb = W * 3  # P6 bytes per row (maxval 255)
-    qstrips = [torch.zeros((max_rows, rb), dtype=torch.uint8, device=dev) for _ in range(2)] if p6 else None
-    gdev = dev if a.backend == "nccl" else torch.device("cpu")
-    payload = qstrips if p6 else strips
-    gathers = [torch.empty((world,) + tuple(payload[0].shape), dtype=payload[0].dtype, device=gdev)
-               if (world > 1 and rank == 0) else None for _ in range(2)]
-    p6_frame = torch.empty((H, rb), dtype=torch.uint8, device=dev) if (p6 and rank == 0 and world > 1) else None
-    pending = [None, None]
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    frames = [0]
 
-    def finish(b):
-        """Frame in buffer b is complete on rank 0 once its gather is: un-permute the P6 bands."""
-        if pending[b] is None:
-            return
-        pending[b].wait()
-        pending[b] = None
-        if p6 and rank == 0:
-            g = gathers[b] if a.backend == "nccl" else gathers[b].to(dev)
-            rt.unpermute_strips_device(g.data_ptr(), max_rows, rb, H, BAND_ROWS, world, p6_frame.data_ptr(),
-                                       False, stream)
+    comm = a.comm
+    fallback = None
+    if comm == "native":
+        try:
+            res = native(a, hs, cam, cfg, world, rank, local, dev)
+        except rt.RTError as e:
+            if world == 1 or e.code != -8:
+                raise
+            fallback = f"native RCCL failed ({e}); torch.distributed gather used"
+            print(f"bench: {fallback}", file=sys.stderr, flush=True)
+            comm = "torch"
+    if comm == "torch":
+        a.deliver = a.gather_payload
+        res = torch_path(a, hs, cam, cfg, world, rank, local, dev)
 
-    def step():
-        b = frames[0] & 1
-        frames[0] += 1
-        finish(b)  # frame k-2 used these buffers
-        # p6: the render and cull kernels write the strip's P6 samples themselves (fused epilogue)
-        ds.render_device(cam, opts, strips[b].data_ptr(), stream=stream,
-                         p6_dev_ptr=qstrips[b].data_ptr() if p6 else None)
-        if world > 1:
-            src = payload[b] if a.backend == "nccl" else payload[b].cpu()
-            glist = list(gathers[b].unbind(0)) if rank == 0 else None
-            pending[b] = dist.gather(src, gather_list=glist, dst=0, async_op=True)
-
-    def drain():
-        for b in ((frames[0]) & 1, (frames[0] + 1) & 1):  # oldest frame first
-            finish(b)
-
-    for _ in range(a.warmup):
-        step()
-    drain()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    drain()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=gdev)
-    kt, ft = ds.kernel_times(a.steps), ds.frame_times(a.steps)
-    kmean = torch.tensor([float(kt.mean()) if len(kt) else float("nan"),
-                          float(ft.mean()) if len(ft) else float("nan")], dtype=torch.float64, device=gdev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        dist.all_reduce(kmean, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
-    kernel_ms, frame_ms = float(kmean[0].item()), float(kmean[1].item())
-
-    # the frame epilogue on the devices (SURVEY.md §8(f) #3): quantise every strip to P6 samples,
-    # gather the bytes, un-permute on rank 0's GPU; timed once, outside the render metric
-    from raytracinginonesemester_amd import dist as rdist
-    last = (frames[0] - 1) & 1  # the buffers of the last frame
-    strip = strips[last]
-    rdist.gather_p6(strip, H, BAND_ROWS, world, rank, stream=stream)  # warm (allocations)
-    torch.cuda.synchronize(dev)
-    te0 = time.perf_counter()
-    p6_bytes = rdist.gather_p6(strip, H, BAND_ROWS, world, rank, stream=stream)
-    te1 = time.perf_counter()
-
-    # the float frame on rank 0 (one more gather of the last frame's float strips, outside the
-    # timed region) and the last timed frame's P6 samples, for the parity check
-    frame = None
-    fparts = None
-    if world > 1:
-        fl = [torch.empty_like(strip) for _ in range(world)] if rank == 0 else None
-        src = strip if a.backend == "nccl" else strip.cpu()
-        if a.backend == "gloo" and rank == 0:
-            fl = [torch.empty(strip.shape, dtype=strip.dtype) for _ in range(world)]
-        dist.gather(src, gather_list=fl, dst=0)
-        fparts = fl
-    if rank == 0:
-        parts = fparts if world > 1 else [strip]
-        frame = np.zeros((H, W, 3), np.float32)
-        for r in range(world):
-            ys = [y for y in range(H) if (y // BAND_ROWS) % world == r] if world > 1 else list(range(H))
-            frame[ys] = parts[r][:len(ys)].cpu().numpy()
-    step_p6 = None
-    if p6 and rank == 0:
-        body = (p6_frame if world > 1 else qstrips[last][:H]).cpu().numpy().tobytes()
-        step_p6 = rt.p6_header(W, H) + body
-
+    elapsed = res["elapsed"]
+    vals = [elapsed, res["kernel_ms"], res["frame_ms"]]
+    if "render_only_s" in res:
+        vals.append(res["render_only_s"])
+        vals.append(res["other_payload"]["s"])
+    m = max_over_ranks(vals, world)
+    elapsed, kernel_ms, frame_ms = m[0], m[1], m[2]
+    shards = None
+    if world == 1 and not a.no_extras and comm == "native":
+        shards = band_shards(hs, cam, cfg, local)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -245,18 +415,8 @@ def main():
 
     samples = W * H * spp
     value = samples * a.steps / elapsed / 1e6
-    B = configs.BYTES_PER_SAMPLE[a.config]
-    per_gpu_samples = samples / world
-    achieved = B * per_gpu_samples / (kernel_ms / 1e3) / 1e9  # GB/s of the dominant kernel
-    traffic = None
-    tf = Path(a.traffic_file)
-    if tf.exists() and world == 1:  # measured for the 1-GPU launch of this config
-        try:
-            traffic = json.loads(tf.read_text()).get(a.config, {}).get("bytes_per_launch")
-        except Exception:
-            traffic = None
     line = {
-        "metric": "Mrays/s at 1920x1080x16spp (1/2/4/8 GPU) + PPM max-abs pixel diff",
+        "metric": METRIC,
         "value": round(value, 3),
         "unit": "Mrays/s",
         "n_gpus": world,
@@ -270,38 +430,81 @@ def main():
         "data": "synthetic=false: frog.obj scene (reference asset), camera/light from frog.json"
                 if a.config == "c3" else "synthetic seeded 1,048,576-triangle heightfield",
         "config": {"workload": f"{a.config if world == 1 else 'c4'}: {cfg['scene']} {W}x{H}x{spp}spp "
-                               f"max_bounces={cfg['max_depth']}, "
-                               f"Lambert/Blinn-Phong + 1 hard shadow ray per light",
+                               f"max_bounces={cfg['max_depth']}, Lambert/Blinn-Phong + 1 hard shadow ray per light",
                    "triangles": hs.num_triangles, "bands": f"{BAND_ROWS}-row bands round-robin over {world} GPU(s)",
-                   "gather": (f"{'RCCL' if a.backend == 'nccl' else 'gloo (CPU-staged)'} gather to rank 0"
-                              if world > 1 else None),
-                   "step_delivers": ("P6 samples of the frame on rank 0 (render kernels write them"
-                                     + (" + gather of the byte strips + un-permute)" if world > 1 else ")")
-                                     if a.gather == "p6" else "float framebuffer strips on rank 0"),
-                   "kernel": a.kernel},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     # measured HBM-side bytes per launch over the kernel time: the scene is
-                     # L2-resident and nodes are fetched once per wave, so this sits far below
-                     # the algorithmic rate (the kernel is VALU- / latency-bound)
-                     "traffic_gbs": (round(traffic / (kernel_ms / 1e3) / 1e9, 2) if traffic else None),
-                     "traffic_frac": (round(traffic / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5) if traffic else None),
-                     "kernel": "render_tiles_kernel", "kernel_ms": round(kernel_ms, 4),
-                     "frame_ms": round(frame_ms, 4), "algorithmic_bytes_per_sample": round(B, 3)},
-        "p6_epilogue_ms": round((te1 - te0) * 1e3, 3),
+                   "step_delivers": (f"the frame's {'P6 samples (PPM body)' if a.deliver == 'p6' else 'float framebuffer'}"
+                                     " in rank 0's host memory (pinned), every timed frame waited for"),
+                   "comm": ("native rt_renderer: " + res["gather_path"]) if comm == "native" else res["gather_path"],
+                   "pipeline_depth": a.depth if comm == "native" else 2, "kernel": a.kernel},
     }
+    if fallback:
+        line["config"]["fallback"] = fallback
+    per_gpu_samples = samples / world
+    ref_eq = configs.BYTES_PER_SAMPLE[a.config] * per_gpu_samples / (kernel_ms / 1e3) / 1e9
+    tr = load_traffic(Path(a.traffic_file), a.config) if world == 1 else None
+    traffic = tr.get("bytes_per_launch") if tr else None
+    compulsory = None
+    if tr and tr.get("compulsory_bytes_per_launch"):
+        compulsory = tr["compulsory_bytes_per_launch"]
+    roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": traffic,
+            "kernel": "render_tiles_kernel", "kernel_ms": round(kernel_ms, 4), "frame_ms": round(frame_ms, 4)}
+    if traffic:
+        ach = traffic / (kernel_ms / 1e3) / 1e9
+        roof.update(achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
+                    achieved_from="measured HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+                                  f"{tr.get('source', '?')}) / live kernel_ms")
+    else:
+        roof.update(achieved=None, frac=None, achieved_from="no PMC traffic for this launch shape")
+    if compulsory:
+        roof["compulsory_bytes_per_launch"] = compulsory
+        roof["compulsory_GBps"] = round(compulsory / (kernel_ms / 1e3) / 1e9, 2)
+    roof["reference_equivalent_GBps"] = round(ref_eq, 2)
+    roof["reference_equivalent_note"] = ("SURVEY.md §8(d) reference-layout model, "
+                                         f"{configs.BYTES_PER_SAMPLE[a.config]:.2f} B/sample: the bytes the "
+                                         "reference's per-ray traversal would fetch, not this kernel's traffic")
+    if tr and tr.get("issue"):
+        roof["issue"] = tr["issue"]
+        roof["binding"] = tr.get("binding")
+    line["roofline"] = roof
+    extra = {"kernel_ms": round(kernel_ms, 4), "frame_ms": round(frame_ms, 4)}
+    for k in ("gather_ms", "deliver_ms", "frame_latency_ms"):
+        if k in res:
+            extra[k] = round(res[k], 4)
+    if "render_only_s" in res:
+        extra["render_only_value"] = round(samples * a.steps / m[3] / 1e6, 3)
+        op = res["other_payload"]
+        extra[f"{op['deliver']}_host_value"] = round(samples * op["steps"] / m[4] / 1e6, 3)
+    extra["live_tiles"] = res.get("live_tiles")
+    if shards:
+        extra["band_shards_one_gpu"] = shards
+    line["timing"] = extra
+
     if not a.no_parity and a.config == "c3":
         ref = np.frombuffer(gzip.open(REPO / "tests" / "golden" / "scenes" / "c3_full" / "fb.f32.gz").read(),
                             np.float32).reshape(H, W, 3)
         ppm_ref = gzip.open(REPO / "tests" / "golden" / "scenes" / "c3_full" / "image.ppm.gz").read()
-        pd = np.abs(np.frombuffer(p6_bytes[17:], np.uint8).astype(int) - np.frombuffer(ppm_ref[17:], np.uint8).astype(int))
-        line["parity"] = {"vs": "reference CPU render() output (tests/golden/scenes/c3_full)",
-                          "rgb_maxabs": float(np.abs(frame - ref).max()),
-                          "rgb_bitexact_frac": float((frame.view(np.uint32) == ref.view(np.uint32)).mean()),
-                          "ppm_maxabs": int(pd.max()), "ppm_identical": p6_bytes == ppm_ref,
-                          "ppm_from": "device P6 epilogue (rt_ppm_quantize_device + gather + un-permute)"}
-        if step_p6 is not None:
-            line["parity"]["timed_step_ppm_identical"] = step_p6 == ppm_ref
+        par = {"vs": "reference CPU render() output (tests/golden/scenes/c3_full)"}
+
+        def p6_check(body: bytes, tag: str):
+            got = np.frombuffer(body, np.uint8).astype(int)
+            want = np.frombuffer(ppm_ref[17:], np.uint8).astype(int)
+            par[f"{tag}ppm_maxabs"] = int(np.abs(got - want).max())
+            par[f"{tag}ppm_identical"] = rt.p6_header(W, H) + body == ppm_ref
+
+        def f32_check(body: bytes, tag: str):
+            fr = np.frombuffer(body, np.float32).reshape(H, W, 3)
+            par[f"{tag}rgb_maxabs"] = float(np.abs(fr - ref).max())
+            par[f"{tag}rgb_bitexact_frac"] = float((fr.view(np.uint32) == ref.view(np.uint32)).mean())
+
+        if a.deliver == "p6":
+            p6_check(res["frame_bytes"], "timed_step_")
+            if "other_bytes" in res:
+                f32_check(res["other_bytes"], "")
+        else:
+            f32_check(res["frame_bytes"], "timed_step_")
+            if "other_bytes" in res:
+                p6_check(res["other_bytes"], "")
+        line["parity"] = par
     if world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(hs, cam, cfg)
         line["speedup_vs_cpu_baseline"] = round(value / line["cpu_baseline"]["value"], 2)

@@ -35,7 +35,8 @@ enum {
     RT_ERR_HIP = -4,          /* HIP runtime error (message in rt_last_error) */
     RT_ERR_NOMEM = -5,
     RT_ERR_NODEVICE = -6,     /* no gfx950 device / code object not loadable */
-    RT_ERR_UNSUPPORTED = -7   /* input outside what the kernels handle (see rt_last_error) */
+    RT_ERR_UNSUPPORTED = -7,  /* input outside what the kernels handle (see rt_last_error) */
+    RT_ERR_COMM = -8          /* RCCL could not be loaded or a collective failed */
 };
 
 /* ---- reference POD types ------------------------------------------------------------ */
@@ -176,6 +177,9 @@ int rt_scene_create(int device, size_t num_triangles, const rt_bvh_node* nodes, 
                     const rt_material* materials, int num_materials, const rt_light* lights,
                     int num_lights, rt_scene** out);
 void rt_scene_destroy(rt_scene* s);
+/* The same scene on another device: device-to-device copies of the packed arrays (no host
+ * repacking).  Frames of a scene run in launch order (see rt_render_device). */
+int rt_scene_clone(const rt_scene* src, int device, rt_scene** out);
 int rt_scene_device(const rt_scene* s);
 size_t rt_scene_device_bytes(const rt_scene* s);
 
@@ -219,14 +223,17 @@ int rt_shard_rows(int height, int band_rows, int band_index, int band_count);
 
 /* Render into device memory on `hip_stream` (hipStream_t; NULL = the null stream), no
  * host sync.  rgb_dev: rows*W*3 floats.  hit_idx_dev / hit_t_dev (optional, rows*W*spp):
- * primary-ray triangle index (-1 = miss) and t per (pixel, sample). */
+ * primary-ray triangle index (-1 = miss) and t per (pixel, sample).
+ * Frames of one scene are ordered: a call on another stream than the scene's previous frame
+ * makes its stream wait for that frame first (the scene's tile lists are reused per frame). */
 int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt,
                      float* rgb_dev, int32_t* hit_idx_dev, float* hit_t_dev, void* hip_stream);
 
 /* rt_render_device that also writes the pixels' P6 samples (write_p6 defaults: maxval 255,
  * clamp, sqrt gamma; ppm_p6.cpp:137-155) to p6_dev (rows*W*3 bytes, same row order as
  * rgb_dev) from the render and cull kernels themselves: the frame epilogue fused into the
- * kernels that produce the pixels (p6_dev may be NULL). */
+ * kernels that produce the pixels (p6_dev may be NULL).  rgb_dev may be NULL when p6_dev is
+ * not: the frame is then produced as P6 samples only. */
 int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt,
                         float* rgb_dev, int32_t* hit_idx_dev, float* hit_t_dev, uint8_t* p6_dev,
                         void* hip_stream);
@@ -242,6 +249,92 @@ int rt_render_reference(size_t num_triangles, int W, int H, const rt_camera* cam
                         const rt_triangle* triangles, const int32_t* tri_object_ids,
                         const rt_material* materials, int num_materials, const rt_light* lights,
                         int num_lights, int diffuse_bounce, rt_vec3* output);
+
+/* rt_render_reference over n_gpus devices (0..n_gpus-1) of this process: the image's 8-row
+ * bands dealt round-robin over the GPUs, the float strips gathered to device 0 with RCCL and
+ * copied into `output` (host).  The frame equals rt_render_reference's bit for bit.
+ * (SURVEY.md §8(b) n_gpus / §8(e); G/include/query.h:13-29 has no multi-GPU form.) */
+int rt_render_reference_gpus(size_t num_triangles, int W, int H, const rt_camera* cam, rt_vec3 miss_color,
+                             int max_depth, int spp, const rt_bvh_node* nodes, const rt_aabb* aabbs,
+                             const rt_triangle* triangles, const int32_t* tri_object_ids,
+                             const rt_material* materials, int num_materials, const rt_light* lights,
+                             int num_lights, int diffuse_bounce, int n_gpus, rt_vec3* output);
+
+/* ---- frame renderer: render(scene, camera) -> frame in host memory on 1..N GPUs ----------
+ * The loop around render() in G/src/main.cu:362-378 (render, then the frame copied to host
+ * memory), pipelined and sharded.  Per frame, every rank renders the bands b with
+ * b % world_size == rank (band_rows-row bands, rt_render_opts sharding) into a device strip on
+ * its compute stream; the strips reach rank 0 over RCCL (one grouped ncclSend/ncclRecv per
+ * rank on a comm stream, xGMI between GPUs); rank 0 copies them into a pinned host frame on a
+ * copy stream, placing every band at its image rows (2-D copies: no un-permute pass).  Frames
+ * are double/triple-buffered: frame k+1 renders while frame k is gathered and copied.
+ *
+ * Ranks: the process drives n_devices GPUs as global ranks rank0 .. rank0+n_devices-1 of
+ * world_size.  world_size == n_devices (or 0): one process, the communicator made with
+ * ncclCommInitAll.  world_size > n_devices: one rank group of a multi-process job (e.g. one
+ * process per GPU under torchrun); every process passes the same 128-byte unique_id, made by
+ * rt_comm_unique_id on the process holding rank 0 and shared by the caller.
+ * A device id may repeat (several band shards on one GPU, for tests): then gather must be
+ * RT_GATHER_DIRECT, each rank copying its bands straight into the host frame. */
+typedef struct rt_renderer rt_renderer;
+
+enum {
+    RT_DELIVER_P6 = 0,     /* the P6 body (write_p6 defaults), W*H*3 bytes, rows top to bottom */
+    RT_DELIVER_F32 = 1,    /* the float framebuffer, W*H*3 floats (the reference's output) */
+    RT_DELIVER_DEVICE = 2, /* P6 body assembled in rank 0's device memory; no host copy */
+    RT_DELIVER_NONE = 3    /* render only (strips stay on each rank): measurement */
+};
+enum {
+    RT_GATHER_AUTO = 0,    /* RCCL when world_size > 1 and the devices differ, else DIRECT */
+    RT_GATHER_RCCL = 1,    /* strips -> rank 0's GPU over RCCL, then one host copy stream */
+    RT_GATHER_DIRECT = 2   /* each local rank copies its own bands into the host frame (its own
+                              PCIe link); single process only */
+};
+enum { RT_RENDERER_SELF_SEND = 1 /* rank 0's own strip also goes through RCCL (tests at world 1) */ };
+
+typedef struct {
+    int32_t n_devices;        /* GPUs this process drives (1..64) */
+    const int32_t* devices;   /* their device ids; NULL = 0 .. n_devices-1 */
+    int32_t world_size;       /* ranks over all processes; 0 = n_devices */
+    int32_t rank0;            /* global rank of devices[0]; the others follow */
+    const void* unique_id;    /* 128 bytes (world_size > n_devices) */
+    int32_t band_rows;        /* default 8 */
+    int32_t deliver;          /* RT_DELIVER_* */
+    int32_t gather;           /* RT_GATHER_* */
+    int32_t depth;            /* frames in flight, 1..8 (default 3) */
+    int32_t flags;            /* RT_RENDERER_* */
+} rt_renderer_opts;
+void rt_renderer_opts_default(rt_renderer_opts* o);
+
+/* 128-byte RCCL unique id for a multi-process renderer (call on rank 0's process). */
+int rt_comm_unique_id(void* id128);
+
+/* Scene upload (rt_scene_create's arguments) to every local device (one upload, then
+ * device-to-device clones), stream/event/communicator setup. */
+int rt_renderer_create(size_t num_triangles, const rt_bvh_node* nodes, const rt_aabb* aabbs,
+                       const rt_triangle* triangles, const int32_t* tri_object_ids,
+                       const rt_material* materials, int num_materials, const rt_light* lights,
+                       int num_lights, const rt_renderer_opts* opts, rt_renderer** out);
+void rt_renderer_destroy(rt_renderer* r);
+
+/* Enqueue one frame (opts: its band fields are the renderer's).  Blocks only to reuse the
+ * buffers of frame ticket-depth, which must then be complete.  *ticket numbers the frames. */
+int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt_render_opts* opts, uint64_t* ticket);
+/* Wait for frame `ticket` (one of the last `depth` submitted).  On the process holding rank 0,
+ * *frame / *bytes give the delivered frame: pinned host memory (RT_DELIVER_P6/F32) or rank 0's
+ * device memory (RT_DELIVER_DEVICE), valid until the submit of frame ticket+depth; elsewhere
+ * NULL / 0.  Either pointer may be NULL. */
+int rt_renderer_wait(rt_renderer* r, uint64_t ticket, const void** frame, size_t* bytes);
+/* submit + wait + copy of the frame into out (cap bytes; rank 0 only). */
+int rt_renderer_render(rt_renderer* r, const rt_camera* cam, const rt_render_opts* opts, void* out, size_t cap);
+/* Local rank i's scene (for rt_frame_times / rt_kernel_times / rt_live_tiles). */
+rt_scene* rt_renderer_scene(rt_renderer* r, int i);
+int rt_renderer_local_ranks(const rt_renderer* r);
+/* Durations (ms) of the gather (RT_TIME_GATHER: rank 0's receives, or its copy wait in DIRECT
+ * mode) or of the host copy (RT_TIME_DELIVER) of the last min(max, frames) frames, oldest
+ * first, from HIP events on those streams (rank 0's process; n_out = 0 elsewhere). */
+enum { RT_TIME_GATHER = 0, RT_TIME_DELIVER = 1, RT_TIME_FRAME = 2 /* first render launch -> frame delivered */ };
+int rt_renderer_times(rt_renderer* r, int kind, float* ms_out, int max, int* n_out);
 
 /* HW1 brute-force path on the GPU (HW1/src/render.cpp:72-116 semantics: every triangle,
  * closest t >= 0 with the first index winning ties, HW1 shade).  Synchronous; host I/O. */

@@ -15,12 +15,16 @@ LIB_PATH = Path(os.environ.get("RT_MI355X_LIB", PKG / "lib" / "librt_mi355x.so")
 RT_OK = 0
 RT_ERR = {
     -1: "RT_ERR_ARG", -2: "RT_ERR_IO", -3: "RT_ERR_PARSE", -4: "RT_ERR_HIP",
-    -5: "RT_ERR_NOMEM", -6: "RT_ERR_NODEVICE", -7: "RT_ERR_UNSUPPORTED",
+    -5: "RT_ERR_NOMEM", -6: "RT_ERR_NODEVICE", -7: "RT_ERR_UNSUPPORTED", -8: "RT_ERR_COMM",
 }
 RT_KERNEL_AUTO, RT_KERNEL_WAVE, RT_KERNEL_LANE, RT_KERNEL_WAVE_PIXELS = 0, 1, 2, 3
 RT_TILES_AUTO, RT_TILES_LINEAR, RT_TILES_XCD_CHUNK, RT_TILES_ROWS = 0, 1, 2, 3
 RT_FLAG_NO_CULL = 1
 RT_FLAG_BINARY = 4
+RT_DELIVER_P6, RT_DELIVER_F32, RT_DELIVER_DEVICE, RT_DELIVER_NONE = 0, 1, 2, 3
+RT_GATHER_AUTO, RT_GATHER_RCCL, RT_GATHER_DIRECT = 0, 1, 2
+RT_RENDERER_SELF_SEND = 1
+RT_TIME_GATHER, RT_TIME_DELIVER, RT_TIME_FRAME = 0, 1, 2
 
 
 class RTError(RuntimeError):
@@ -97,6 +101,12 @@ class RenderOpts(C.Structure):
                 ("tile_order", C.c_int32), ("flags", C.c_int32)]
 
 
+class RendererOpts(C.Structure):
+    _fields_ = [("n_devices", C.c_int32), ("devices", C.c_void_p), ("world_size", C.c_int32),
+                ("rank0", C.c_int32), ("unique_id", C.c_void_p), ("band_rows", C.c_int32),
+                ("deliver", C.c_int32), ("gather", C.c_int32), ("depth", C.c_int32), ("flags", C.c_int32)]
+
+
 P = C.c_void_p
 I = C.c_int
 SZ = C.c_size_t
@@ -125,6 +135,7 @@ SIGNATURES = {
     "rt_unpermute_strips_device": (I, [P, I, SZ, I, I, I, I, P, P]),
     "rt_scene_create": (I, [I, SZ, P, P, P, P, P, I, P, I, P]),
     "rt_scene_destroy": (None, [P]),
+    "rt_scene_clone": (I, [P, I, P]),
     "rt_scene_device": (I, [P]),
     "rt_scene_device_bytes": (SZ, [P]),
     "rt_render_opts_default": (None, [P]),
@@ -133,6 +144,17 @@ SIGNATURES = {
     "rt_render_device_p6": (I, [P, P, P, P, P, P, P, P]),
     "rt_render": (I, [P, P, P, P, P, P]),
     "rt_render_reference": (I, [SZ, I, I, P, Vec3, I, I, P, P, P, P, P, I, P, I, I, P]),
+    "rt_render_reference_gpus": (I, [SZ, I, I, P, Vec3, I, I, P, P, P, P, P, I, P, I, I, I, P]),
+    "rt_renderer_opts_default": (None, [P]),
+    "rt_comm_unique_id": (I, [P]),
+    "rt_renderer_create": (I, [SZ, P, P, P, P, P, I, P, I, P, P]),
+    "rt_renderer_destroy": (None, [P]),
+    "rt_renderer_submit": (I, [P, P, P, P]),
+    "rt_renderer_wait": (I, [P, C.c_uint64, P, P]),
+    "rt_renderer_render": (I, [P, P, P, P, SZ]),
+    "rt_renderer_scene": (P, [P, I]),
+    "rt_renderer_local_ranks": (I, [P]),
+    "rt_renderer_times": (I, [P, I, P, I, P]),
     "rt_render_hw1": (I, [I, P, P, P, SZ, P, Vec3, Vec3, I, P, P, P, P]),
     "rt_render_hw1_ex": (I, [I, P, P, P, SZ, P, Vec3, Vec3, I, P, I, P, P, P, P]),
     "rt_intersect_rays": (I, [I, P, P, P, I, I, C.c_float, C.c_float, P, P]),

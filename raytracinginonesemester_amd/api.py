@@ -200,8 +200,21 @@ class DeviceScene:
         check(lib().rt_scene_create(int(device), P, ptr(self._keep[0]), ptr(self._keep[1]), ptr(self._keep[2]),
                                     ptr(objs), ptr(mats), nmat, ptr(lts), nl, C.byref(h)))
         self._h = h
+        self._owned = True
         self.num_triangles = P
         self.device = device
+
+    @classmethod
+    def _borrow(cls, handle, num_triangles: int, owner) -> "DeviceScene":
+        """A scene owned by a Renderer (its timing queries; destroyed with the renderer)."""
+        self = cls.__new__(cls)
+        self._h = C.c_void_p(handle)
+        self._owned = False
+        self._owner = owner
+        self._keep = []
+        self.num_triangles = num_triangles
+        self.device = int(lib().rt_scene_device(self._h))
+        return self
 
     @classmethod
     def from_host(cls, hs: HostScene, device: int = 0) -> "DeviceScene":
@@ -280,8 +293,102 @@ class DeviceScene:
         return out[:n.value]
 
     def close(self) -> None:
-        if self._h:
+        if self._h and self._owned:
             lib().rt_scene_destroy(self._h)
+        self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Renderer:
+    """render(scene, camera) -> frame in host memory on 1..N GPUs (rt_renderer, include/rt_mi355x.h).
+
+    Every rank renders its 8-row bands (band b -> rank b % world) into a device strip with the
+    fused P6 epilogue; the strips reach rank 0 over RCCL and are copied band by band into a
+    pinned host frame, pipelined `depth` frames deep.  ``devices``: the GPUs this process
+    drives; ``world_size``/``rank0``/``unique_id`` join a multi-process job (one process per
+    GPU): rank 0's process makes the id with :func:`comm_unique_id` and shares it.
+    """
+
+    def __init__(self, num_triangles: int, nodes, aabbs, triangles, tri_object_ids=None, materials=None,
+                 lights=None, devices=(0,), world_size: int = 0, rank0: int = 0, unique_id: bytes = None,
+                 band_rows: int = 8, deliver: int = L.RT_DELIVER_P6, gather: int = L.RT_GATHER_AUTO,
+                 depth: int = 3, flags: int = 0):
+        P = int(num_triangles)
+        keep = [_c(nodes, np.uint32), _c(aabbs, np.float32), _c(triangles, np.float32)]
+        objs = None if tri_object_ids is None else _c(tri_object_ids, np.int32)
+        mats = None if materials is None else _c(materials, np.float32).reshape(-1, 13)
+        lts = None if lights is None else np.ascontiguousarray(lights, dtype=LIGHT_DTYPE)
+        devs = np.ascontiguousarray(list(devices), np.int32)
+        o = L.RendererOpts()
+        lib().rt_renderer_opts_default(C.byref(o))
+        o.n_devices, o.devices = len(devs), devs.ctypes.data
+        o.world_size, o.rank0 = int(world_size), int(rank0)
+        uid = None
+        if unique_id is not None:
+            uid = C.create_string_buffer(bytes(unique_id), 128)
+            o.unique_id = C.addressof(uid)
+        o.band_rows, o.deliver, o.gather, o.depth, o.flags = int(band_rows), int(deliver), int(gather), int(depth), int(flags)
+        h = C.c_void_p()
+        check(lib().rt_renderer_create(P, ptr(keep[0]), ptr(keep[1]), ptr(keep[2]), ptr(objs), ptr(mats),
+                                       0 if mats is None else mats.shape[0], ptr(lts),
+                                       0 if lts is None else lts.shape[0], C.byref(o), C.byref(h)))
+        self._h = h
+        self.num_triangles = P
+        self.deliver = int(deliver)
+        self.world = int(world_size) or len(devs)
+        self.rank0 = int(rank0)
+
+    @classmethod
+    def from_host(cls, hs: HostScene, **kw) -> "Renderer":
+        return cls(hs.num_triangles, hs.nodes, hs.aabbs, hs.triangles, hs.tri_object_ids, hs.materials,
+                   hs.lights, **kw)
+
+    @property
+    def local_ranks(self) -> int:
+        return int(lib().rt_renderer_local_ranks(self._h))
+
+    def scene(self, i: int = 0) -> DeviceScene:
+        """Local rank i's device scene (frame/kernel timing queries)."""
+        h = lib().rt_renderer_scene(self._h, int(i))
+        if not h:
+            raise L.RTError(-1, f"no local rank {i}")
+        return DeviceScene._borrow(h, self.num_triangles, self)
+
+    def submit(self, camera: Camera, opts) -> int:
+        t = C.c_uint64()
+        check(lib().rt_renderer_submit(self._h, C.byref(camera.c), C.byref(opts), C.byref(t)))
+        return t.value
+
+    def wait(self, ticket: int):
+        """(address, bytes) of the delivered frame on rank 0's process, else (None, 0)."""
+        f, n = C.c_void_p(), C.c_size_t()
+        check(lib().rt_renderer_wait(self._h, int(ticket), C.byref(f), C.byref(n)))
+        return f.value, n.value
+
+    def render(self, camera: Camera, spp: int = 1, max_depth: int = 1, diffuse_bounce: bool = True,
+               miss_color=(0, 0, 0), jitter=None, kernel: int = L.RT_KERNEL_AUTO, flags: int = 0):
+        """One synchronous frame: (H, W, 3) uint8 P6 samples or float32 (rank 0; None elsewhere)."""
+        o, _jit = DeviceScene.make_opts(spp, max_depth, diffuse_bounce, miss_color, jitter, kernel=kernel, flags=flags)
+        W, H = camera.pixel_width, camera.pixel_height
+        f32 = self.deliver == L.RT_DELIVER_F32
+        out = np.zeros((H, W, 3), np.float32 if f32 else np.uint8)
+        check(lib().rt_renderer_render(self._h, C.byref(camera.c), C.byref(o), ptr(out), out.nbytes))
+        return out if self.rank0 == 0 and self.deliver != L.RT_DELIVER_NONE else None
+
+    def times(self, kind: int, max_frames: int = 256) -> np.ndarray:
+        out = np.zeros(max_frames, np.float32)
+        n = C.c_int()
+        check(lib().rt_renderer_times(self._h, int(kind), ptr(out), int(max_frames), C.byref(n)))
+        return out[:n.value]
+
+    def close(self) -> None:
+        if self._h:
+            lib().rt_renderer_destroy(self._h)
             self._h = C.c_void_p()
 
     def __del__(self):
@@ -291,10 +398,19 @@ class DeviceScene:
             pass
 
 
+def comm_unique_id() -> bytes:
+    """128-byte RCCL unique id for a multi-process Renderer (made on rank 0's process)."""
+    b = C.create_string_buffer(128)
+    check(lib().rt_comm_unique_id(b))
+    return b.raw
+
+
 def render(numTriangles, W, H, cam: Camera, missColor, max_depth, spp, nodes, aabbs, triangles,
-           triObjectIds, objectMaterials, numObjectMaterials, lights, numLights, diffuse_bounce, output):
+           triObjectIds, objectMaterials, numObjectMaterials, lights, numLights, diffuse_bounce, output,
+           n_gpus: int = 1):
     """The reference entry point (G/include/query.h:13-29) with host arrays; fills ``output``
-    (H*W*3 float32, row-major, row 0 = top) like the CPU branch of query.cu:130-166."""
+    (H*W*3 float32, row-major, row 0 = top) like the CPU branch of query.cu:130-166.
+    n_gpus > 1 shards the bands over GPUs 0..n_gpus-1 (rt_render_reference_gpus)."""
     out = np.asarray(output)
     if out.dtype != np.float32 or not out.flags.c_contiguous or out.size != W * H * 3:
         raise ValueError("output must be a contiguous float32 array of W*H*3")
@@ -302,10 +418,13 @@ def render(numTriangles, W, H, cam: Camera, missColor, max_depth, spp, nodes, aa
     lts = np.ascontiguousarray(lights, dtype=LIGHT_DTYPE)[:numLights]
     nd, ab, tr = _c(nodes, np.uint32), _c(aabbs, np.float32), _c(triangles, np.float32)
     ob = None if triObjectIds is None else _c(triObjectIds, np.int32)
-    check(lib().rt_render_reference(int(numTriangles), int(W), int(H), C.byref(cam.c), _v3(missColor),
-                                    int(max_depth), int(spp), ptr(nd), ptr(ab), ptr(tr), ptr(ob), ptr(mats),
-                                    int(numObjectMaterials), ptr(lts), int(numLights),
-                                    1 if diffuse_bounce else 0, ptr(out)))
+    args = (int(numTriangles), int(W), int(H), C.byref(cam.c), _v3(missColor), int(max_depth), int(spp), ptr(nd),
+            ptr(ab), ptr(tr), ptr(ob), ptr(mats), int(numObjectMaterials), ptr(lts), int(numLights),
+            1 if diffuse_bounce else 0)
+    if n_gpus == 1:
+        check(lib().rt_render_reference(*args, ptr(out)))
+    else:
+        check(lib().rt_render_reference_gpus(*args, int(n_gpus), ptr(out)))
     return out
 
 

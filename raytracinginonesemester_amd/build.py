@@ -26,7 +26,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 FP = ["-ffp-contract=off", "-fno-fast-math"]
-DEVICE_UNITS = ["rt_device", "rt_frame", "rt_lbvh"]
+DEVICE_UNITS = ["rt_device", "rt_frame", "rt_lbvh", "rt_renderer"]
 
 
 def _run(cmd):
@@ -63,7 +63,7 @@ def build(force: bool = False) -> Path:
                   "-mcode-object-version=5",
                   "-Wno-unused-function", *inc, "-c", CSRC / f"{name}.hip", "-o", dev_o])
     if force or _stale(so, [host_o, *dev_objs]):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", host_o, *dev_objs, "-o", so])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", host_o, *dev_objs, "-o", so, "-ldl"])
     cli = OUT / "rt_render_cli"
     if force or _stale(cli, [CSRC / "rt_render_cli.cpp", REPO / "include" / "rt_mi355x.hpp", so]):
         _run([CXX, "-std=c++17", "-O2", *FP, "-Wall", *inc, CSRC / "rt_render_cli.cpp", "-o", cli,

@@ -913,10 +913,12 @@ __device__ __forceinline__ void write_culled_tile(const RenderParams& P, int til
         const uint32_t w0 = b0 | b1 << 8 | b2 << 16 | b0 << 24, w1 = b1 | b2 << 8 | b0 << 16 | b1 << 24,
                        w2 = b2 | b0 << 8 | b1 << 16 | b2 << 24;
         for (int r = ra; r < ra + th; ++r) {
-            float4* o = reinterpret_cast<float4*>(P.rgb + ((size_t)r * P.W + xa) * 3);
-            o[0] = f0;
-            o[1] = f1;
-            o[2] = f2;
+            if (P.rgb) {
+                float4* o = reinterpret_cast<float4*>(P.rgb + ((size_t)r * P.W + xa) * 3);
+                o[0] = f0;
+                o[1] = f1;
+                o[2] = f2;
+            }
             if (P.p6) {
                 uint32_t* q = reinterpret_cast<uint32_t*>(P.p6 + ((size_t)r * P.W + xa) * 3);
                 q[0] = w0;
@@ -928,7 +930,7 @@ __device__ __forceinline__ void write_culled_tile(const RenderParams& P, int til
         for (int i = first; i < tw * th * 3; i += lanes) {
             const int px = i / 3, c = i - 3 * px;
             const int r = ra + px / tw, x = xa + px % tw;
-            P.rgb[((size_t)r * P.W + x) * 3 + c] = mp[c];
+            if (P.rgb) P.rgb[((size_t)r * P.W + x) * 3 + c] = mp[c];
             if (P.p6) P.p6[((size_t)r * P.W + x) * 3 + c] = P.miss_p6[c];
         }
     }
@@ -1106,9 +1108,11 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
             const float rs = 1.0f / (float)P.spp;
             const size_t k = (size_t)pix * 3;
             const f3 px = mk(acc.x * rs, acc.y * rs, acc.z * rs);
-            P.rgb[k] = px.x;
-            P.rgb[k + 1] = px.y;
-            P.rgb[k + 2] = px.z;
+            if (P.rgb) {
+                P.rgb[k] = px.x;
+                P.rgb[k + 1] = px.y;
+                P.rgb[k + 2] = px.z;
+            }
             if (P.p6) {  // the frame epilogue fused in (write_p6 defaults)
                 P.p6[k] = rtp::p6_default_sample(px.x);
                 P.p6[k + 1] = rtp::p6_default_sample(px.y);
@@ -1136,9 +1140,11 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
         const float fs = (float)P.spp;
         const size_t k = ((size_t)r * P.W + x) * 3;
         const f3 px = mk(acc.x / fs, acc.y / fs, acc.z / fs);
-        P.rgb[k] = px.x;
-        P.rgb[k + 1] = px.y;
-        P.rgb[k + 2] = px.z;
+        if (P.rgb) {
+            P.rgb[k] = px.x;
+            P.rgb[k + 1] = px.y;
+            P.rgb[k + 2] = px.z;
+        }
         if (P.p6) {
             P.p6[k] = rtp::p6_default_sample(px.x);
             P.p6[k + 1] = rtp::p6_default_sample(px.y);
@@ -1644,6 +1650,12 @@ struct rt_scene {
     hipEvent_t ev0[kRing] = {}, evm[kRing] = {}, ev1[kRing] = {};
     uint64_t launches = 0;
     size_t bytes = 0;
+    // The work buffers (live lists, counters) are per scene, so frames of one scene must run in
+    // order: a frame launched on another stream than the previous one first waits for that
+    // frame's last event.  A frame whose launches failed part-way leaves the counter sets in an
+    // unknown state: the next frame zeroes both.
+    hipStream_t last_stream = nullptr;
+    bool counters_dirty = false;
     ~rt_scene() {
         for (int i = 0; i < kRing; ++i) {
             if (ev0[i]) (void)hipEventDestroy(ev0[i]);
@@ -1906,6 +1918,44 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     return RT_OK;
 }
 
+extern "C" int rt_scene_clone(const rt_scene* src, int device, rt_scene** out) {
+    if (!src || !out) return set_error(RT_ERR_ARG, "rt_scene_clone: null argument");
+    *out = nullptr;
+    int rc = check_device(device);
+    if (rc != RT_OK) return rc;
+    DeviceGuard g(device);
+    std::unique_ptr<rt_scene> s(new (std::nothrow) rt_scene());
+    if (!s) return set_error(RT_ERR_NOMEM, "out of memory");
+    s->device = device;
+    s->P = src->P;
+    s->nmat = src->nmat;
+    s->nlights = src->nlights;
+    s->root_ref = src->root_ref;
+    std::memcpy(s->root_box, src->root_box, sizeof(s->root_box));
+    std::memcpy(s->bmax, src->bmax, sizeof(s->bmax));
+    s->ncut = src->ncut;
+    s->wide = src->wide;
+    s->cus = src->cus;
+    s->bytes = src->bytes;
+    // device-to-device copies of the packed arrays (over xGMI when the devices differ)
+    const std::pair<DevBuf*, const DevBuf*> bufs[] = {{&s->inode, &src->inode}, {&s->wnode, &src->wnode},
+                                                      {&s->ibox, &src->ibox},   {&s->leaf, &src->leaf},
+                                                      {&s->tnorm, &src->tnorm}, {&s->objids, &src->objids},
+                                                      {&s->mats, &src->mats},   {&s->lights, &src->lights},
+                                                      {&s->cut, &src->cut}};
+    for (const auto& [d, q] : bufs) {
+        if ((rc = d->alloc(q->n)) != RT_OK) return rc;
+        if (q->n) HIP_TRY(hipMemcpyPeer(d->p, device, q->p, src->device, q->n));
+    }
+    for (int i = 0; i < rt_scene::kRing; ++i) {
+        HIP_TRY(hipEventCreate(&s->ev0[i]));
+        HIP_TRY(hipEventCreate(&s->evm[i]));
+        HIP_TRY(hipEventCreate(&s->ev1[i]));
+    }
+    *out = s.release();
+    return RT_OK;
+}
+
 extern "C" void rt_scene_destroy(rt_scene* s) {
     if (!s) return;
     DeviceGuard g(s->device);
@@ -2040,7 +2090,7 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
 
 extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, float* rgb,
                                    int32_t* hit_idx, float* hit_t, uint8_t* p6, void* stream) {
-    if (!s || !cam || !o || !rgb) return set_error(RT_ERR_ARG, "rt_render_device: null argument");
+    if (!s || !cam || !o || (!rgb && !p6)) return set_error(RT_ERR_ARG, "rt_render_device: null argument");
     if (o->spp < 1) return set_error(RT_ERR_ARG, "spp must be >= 1");
     if ((hit_idx == nullptr) != (hit_t == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
     const int W = cam->pixel_width, H = cam->pixel_height;
@@ -2125,9 +2175,17 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     const size_t list_bytes = size_t(P.nqueues) * size_t(P.queue_cap) * sizeof(int32_t);
     const size_t work_bytes = 2 * kCounterBytes + list_bytes + size_t(P.nqueues) * size_t(P.queue_cap);
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (s->launches > 0 && st != s->last_stream)  // the previous frame of this scene ran elsewhere
+        HIP_TRY(hipStreamWaitEvent(st, s->ev1[(s->launches - 1) % rt_scene::kRing], 0));
+    s->last_stream = st;
     if (s->work.n < work_bytes) {
+        if (s->launches > 0) HIP_TRY(hipStreamSynchronize(st));  // the old buffer may still be read
         if ((rc = s->work.alloc(work_bytes)) != RT_OK) return rc;
+        s->counters_dirty = true;
+    }
+    if (s->counters_dirty) {
         HIP_TRY(hipMemsetAsync(s->work.p, 0, 2 * kCounterBytes, st));
+        s->counters_dirty = false;
     }
     const int set = int(s->launches & 1);
     P.live_count = reinterpret_cast<uint32_t*>(static_cast<char*>(s->work.p) + set * kCounterBytes);
@@ -2137,24 +2195,30 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.cut_flag = reinterpret_cast<uint8_t*>(static_cast<char*>(s->work.p) + 2 * kCounterBytes + list_bytes);
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
     const int slot = int(s->launches % rt_scene::kRing);
-    HIP_TRY(hipEventRecord(s->ev0[slot], st));
-    hipLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, P);
-    HIP_TRY(hipGetLastError());
-    if (P.cull && P.sc.ncut > 0) {
-        // 16 waves per CU; each takes (list, group) pairs grid-stride (c3: about one each)
-        const int cut_blocks = 4 * s->cus;
-        hipLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, st, P);
+    // From the cull launch on, a failure leaves the counter sets unknown (counters_dirty).
+    auto frame = [&]() -> int {
+        HIP_TRY(hipEventRecord(s->ev0[slot], st));
+        hipLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, P);
         HIP_TRY(hipGetLastError());
-    }
-    HIP_TRY(hipEventRecord(s->evm[slot], st));
-    const bool big = big_scene_waves(s);
-    if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, big, st);
-    else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, big, st);
-    else launch<RT_KERNEL_WAVE>(P, samples, big, st);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(s->ev1[slot], st));
-    s->launches++;
-    return RT_OK;
+        if (P.cull && P.sc.ncut > 0) {
+            // 16 waves per CU; each takes (list, group) pairs grid-stride (c3: about one each)
+            const int cut_blocks = 4 * s->cus;
+            hipLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, st, P);
+            HIP_TRY(hipGetLastError());
+        }
+        HIP_TRY(hipEventRecord(s->evm[slot], st));
+        const bool big = big_scene_waves(s);
+        if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, big, st);
+        else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, big, st);
+        else launch<RT_KERNEL_WAVE>(P, samples, big, st);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(s->ev1[slot], st));
+        return RT_OK;
+    };
+    rc = frame();
+    s->launches++;  // the events of this slot belong to this frame even when it failed
+    if (rc != RT_OK) s->counters_dirty = true;
+    return rc;
 }
 
 namespace {

@@ -1,0 +1,637 @@
+// rt_renderer.hip — render(scene, camera) -> frame in host memory on 1..N GPUs (host code).
+//
+// The reference renders one frame on one GPU and copies the float framebuffer to the host
+// inside its timed region (G/src/main.cu:362-378; render() is G/include/query.h:13-29).  Here
+// a frame is sharded over ranks as 8-row bands dealt round-robin (rank r renders bands
+// b % world == r); each rank renders its bands into a contiguous device strip
+// with the fused P6 epilogue (rt_render_device_p6), the strips reach rank 0's GPU with one
+// grouped ncclSend/ncclRecv per rank (RCCL over xGMI), and rank 0 copies every strip into a
+// pinned host frame with 2-D copies that put each band at its image rows, so no un-permute
+// pass runs.  Per rank three streams (compute, comm, copy) and per frame slot a strip buffer:
+// frame k+1 renders while frame k is gathered and copied to the host.
+//
+// RCCL is loaded at run time (dlopen "librccl.so.1"): in a process that has imported torch
+// this is torch's own RCCL (same soname, already loaded), otherwise the image's.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <set>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "rt_common.hpp"
+#include "rt_hip_host.hpp"
+
+using rt::check_device;
+using rt::DevBuf;
+using rt::DeviceGuard;
+using rt::hip_msg;
+using rt::set_error;
+
+namespace {
+
+// ---- RCCL, resolved at run time --------------------------------------------------------
+struct Rccl {
+    bool ok = false;
+    std::string err;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+const Rccl& rccl() {
+    static Rccl R;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            const char* e = dlerror();
+            R.err = std::string("dlopen librccl.so.1: ") + (e ? e : "?");
+            return;
+        }
+        bool all = true;
+        auto sym = [&](auto& fp, const char* name) {
+            fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+            if (!fp) {
+                all = false;
+                R.err += std::string(" missing ") + name;
+            }
+        };
+        sym(R.GetUniqueId, "ncclGetUniqueId");
+        sym(R.CommInitRank, "ncclCommInitRank");
+        sym(R.CommInitAll, "ncclCommInitAll");
+        sym(R.CommDestroy, "ncclCommDestroy");
+        sym(R.GroupStart, "ncclGroupStart");
+        sym(R.GroupEnd, "ncclGroupEnd");
+        sym(R.Send, "ncclSend");
+        sym(R.Recv, "ncclRecv");
+        sym(R.GetErrorString, "ncclGetErrorString");
+        R.ok = all;
+    });
+    return R;
+}
+
+int nccl_error(ncclResult_t e, const char* what) {
+    const Rccl& R = rccl();
+    return set_error(RT_ERR_COMM, std::string("RCCL ") + what + ": " +
+                                      (R.GetErrorString ? R.GetErrorString(e) : std::to_string(int(e))));
+}
+#define NCCL_TRY(expr)                                    \
+    do {                                                  \
+        ncclResult_t e_ = (expr);                         \
+        if (e_ != ncclSuccess) return nccl_error(e_, #expr); \
+    } while (0)
+
+constexpr int kTimeRing = 256;
+
+// Bands of rank r (b % world == r) in its strip, in band order, go to image rows b*band_rows.
+// The full bands are one strided 2-D copy; a partial last band (H % band_rows) a plain one.
+hipError_t scatter_strip(char* dst, const char* strip, int r, int world, int H, int band_rows, size_t rb,
+                         hipMemcpyKind kind, hipStream_t st) {
+    if (world <= 1) return hipMemcpyAsync(dst, strip, size_t(H) * rb, kind, st);
+    const int full = H / band_rows;  // bands 0 .. full-1 have band_rows rows
+    const int nfull = full > r ? (full - 1 - r) / world + 1 : 0;
+    const size_t band = size_t(band_rows) * rb;
+    if (nfull > 0) {
+        const hipError_t e = hipMemcpy2DAsync(dst + size_t(r) * band, size_t(world) * band, strip, band, band,
+                                              size_t(nfull), kind, st);
+        if (e != hipSuccess) return e;
+    }
+    if (H % band_rows != 0 && full % world == r) {  // band `full` is partial and ours
+        const size_t rows = size_t(H - full * band_rows);
+        return hipMemcpyAsync(dst + size_t(full) * band, strip + size_t(nfull) * band, rows * rb, kind, st);
+    }
+    return hipSuccess;
+}
+
+struct LocalRank {
+    int device = 0;
+    int rank = 0;  // global rank
+    rt_scene* scene = nullptr;
+    hipStream_t compute = nullptr, comm = nullptr, copy = nullptr;
+    ncclComm_t nccl = nullptr;
+    int rows = 0;                      // rows of this rank's strip for the current geometry
+    std::vector<DevBuf> strip;         // per slot: rows*W*3 bytes (P6) or floats (F32)
+    std::vector<hipEvent_t> rendered;  // per slot, on compute
+    std::vector<hipEvent_t> released;  // per slot: the last reader of the strip finished
+    std::vector<bool> release_recorded;
+};
+
+}  // namespace
+
+struct rt_renderer {
+    std::vector<LocalRank> ranks;
+    int world = 1;
+    int band_rows = 8;
+    int deliver = RT_DELIVER_P6;
+    int gather = RT_GATHER_DIRECT;
+    int depth = 3;
+    int flags = 0;
+    bool rank0_local = false;  // ranks[0] is global rank 0
+    // geometry the buffers are sized for
+    int W = 0, H = 0, max_rows = 0;
+    size_t row_bytes = 0, frame_bytes = 0, strip_cap = 0;
+    // rank 0's side, per slot
+    std::vector<DevBuf> gathered;       // RCCL: world strips of strip_cap bytes
+    std::vector<DevBuf> dev_frame;      // RT_DELIVER_DEVICE
+    std::vector<void*> host;            // pinned host frames
+    std::vector<hipEvent_t> delivered;  // on ranks[0].copy
+    std::vector<uint64_t> slot_ticket;  // frame held by each slot (+1; 0 = none)
+    uint64_t next = 0;
+    // timing ring (rank 0's process): frame start, gather start/end, delivery start/end
+    hipEvent_t tf0[kTimeRing] = {}, tg0[kTimeRing] = {}, tg1[kTimeRing] = {}, td0[kTimeRing] = {},
+               td1[kTimeRing] = {};
+    bool owns_scenes = true;
+
+    ~rt_renderer() { release(); }
+    void release_buffers() {
+        for (void* h : host)
+            if (h) (void)hipHostFree(h);
+        host.clear();
+        gathered.clear();
+        dev_frame.clear();
+        for (LocalRank& L : ranks) {
+            DeviceGuard g(L.device);
+            L.strip.clear();
+        }
+    }
+    void release() {
+        for (LocalRank& L : ranks) {
+            DeviceGuard g(L.device);
+            if (L.compute) (void)hipStreamSynchronize(L.compute);
+            if (L.comm) (void)hipStreamSynchronize(L.comm);
+            if (L.copy) (void)hipStreamSynchronize(L.copy);
+        }
+        release_buffers();
+        for (LocalRank& L : ranks) {
+            DeviceGuard g(L.device);
+            if (L.nccl && rccl().ok) (void)rccl().CommDestroy(L.nccl);
+            L.nccl = nullptr;
+            for (hipEvent_t e : L.rendered) (void)hipEventDestroy(e);
+            for (hipEvent_t e : L.released) (void)hipEventDestroy(e);
+            L.rendered.clear();
+            L.released.clear();
+            if (L.compute) (void)hipStreamDestroy(L.compute);
+            if (L.comm) (void)hipStreamDestroy(L.comm);
+            if (L.copy) (void)hipStreamDestroy(L.copy);
+            L.compute = L.comm = L.copy = nullptr;
+            if (owns_scenes && L.scene) rt_scene_destroy(L.scene);
+            L.scene = nullptr;
+        }
+        if (!ranks.empty()) {
+            DeviceGuard g(ranks[0].device);
+            for (hipEvent_t e : delivered) (void)hipEventDestroy(e);
+            delivered.clear();
+            for (hipEvent_t* ring : {tf0, tg0, tg1, td0, td1})
+                for (int i = 0; i < kTimeRing; ++i)
+                    if (ring[i]) (void)hipEventDestroy(ring[i]), ring[i] = nullptr;
+        }
+        ranks.clear();
+    }
+    bool uses_rccl() const { return gather == RT_GATHER_RCCL && deliver != RT_DELIVER_NONE; }
+    size_t elem() const { return deliver == RT_DELIVER_F32 ? sizeof(float) : 1; }
+};
+
+extern "C" void rt_renderer_opts_default(rt_renderer_opts* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->n_devices = 1;
+    o->band_rows = 8;
+    o->deliver = RT_DELIVER_P6;
+    o->gather = RT_GATHER_AUTO;
+    o->depth = 3;
+}
+
+extern "C" int rt_comm_unique_id(void* id128) {
+    if (!id128) return set_error(RT_ERR_ARG, "rt_comm_unique_id: null");
+    const Rccl& R = rccl();
+    if (!R.ok) return set_error(RT_ERR_COMM, R.err);
+    ncclUniqueId id;
+    NCCL_TRY(R.GetUniqueId(&id));
+    static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+    std::memcpy(id128, &id, sizeof(id));
+    return RT_OK;
+}
+
+namespace {
+
+int init_comms(rt_renderer* r, const rt_renderer_opts* o) {
+    const Rccl& R = rccl();
+    if (!R.ok) return set_error(RT_ERR_COMM, R.err);
+    const int n = int(r->ranks.size());
+    std::vector<ncclComm_t> comms(n, nullptr);
+    if (r->world == n) {
+        std::vector<int> devs(n);
+        for (int i = 0; i < n; ++i) devs[i] = r->ranks[i].device;
+        NCCL_TRY(R.CommInitAll(comms.data(), n, devs.data()));
+    } else {
+        ncclUniqueId id;
+        std::memcpy(&id, o->unique_id, sizeof(id));
+        NCCL_TRY(R.GroupStart());
+        for (int i = 0; i < n; ++i) {
+            HIP_TRY(hipSetDevice(r->ranks[i].device));
+            const ncclResult_t e = R.CommInitRank(&comms[i], r->world, id, r->ranks[i].rank);
+            if (e != ncclSuccess) {
+                (void)R.GroupEnd();
+                return nccl_error(e, "ncclCommInitRank");
+            }
+        }
+        NCCL_TRY(R.GroupEnd());
+    }
+    for (int i = 0; i < n; ++i) r->ranks[i].nccl = comms[i];
+    return RT_OK;
+}
+
+// (Re)size every buffer for a W x H frame.  Waits for the frames in flight first.
+int ensure_geometry(rt_renderer* r, int W, int H) {
+    if (r->W == W && r->H == H && !r->ranks[0].strip.empty()) return RT_OK;
+    for (LocalRank& L : r->ranks) {
+        DeviceGuard g(L.device);
+        HIP_TRY(hipStreamSynchronize(L.compute));
+        HIP_TRY(hipStreamSynchronize(L.comm));
+        HIP_TRY(hipStreamSynchronize(L.copy));
+    }
+    r->release_buffers();
+    r->W = W;
+    r->H = H;
+    r->row_bytes = size_t(W) * 3 * r->elem();
+    r->frame_bytes = size_t(H) * r->row_bytes;
+    r->max_rows = rt_shard_rows(H, r->band_rows, 0, r->world);  // rank 0 holds the most bands
+    r->strip_cap = std::max<size_t>(size_t(r->max_rows) * r->row_bytes, 1);
+    int rc;
+    for (LocalRank& L : r->ranks) {
+        DeviceGuard g(L.device);
+        L.rows = rt_shard_rows(H, r->band_rows, L.rank, r->world);
+        L.strip.resize(r->depth);
+        for (DevBuf& b : L.strip)
+            if ((rc = b.alloc(r->strip_cap)) != RT_OK) return rc;
+        std::fill(L.release_recorded.begin(), L.release_recorded.end(), false);
+    }
+    if (r->rank0_local) {
+        DeviceGuard g(r->ranks[0].device);
+        if (r->uses_rccl()) {
+            r->gathered.resize(r->depth);
+            for (DevBuf& b : r->gathered)
+                if ((rc = b.alloc(size_t(r->world) * r->strip_cap)) != RT_OK) return rc;
+        }
+        if (r->deliver == RT_DELIVER_DEVICE) {
+            r->dev_frame.resize(r->depth);
+            for (DevBuf& b : r->dev_frame)
+                if ((rc = b.alloc(std::max<size_t>(r->frame_bytes, 1))) != RT_OK) return rc;
+        } else if (r->deliver != RT_DELIVER_NONE) {
+            r->host.assign(r->depth, nullptr);
+            for (void*& h : r->host)
+                HIP_TRY(hipHostMalloc(&h, std::max<size_t>(r->frame_bytes, 1), hipHostMallocPortable));
+        }
+    }
+    std::fill(r->slot_ticket.begin(), r->slot_ticket.end(), 0);
+    return RT_OK;
+}
+
+// Host wait until slot s may be reused (its previous frame fully delivered / released).
+int wait_slot(rt_renderer* r, int s) {
+    if (r->slot_ticket[s] == 0) return RT_OK;
+    for (LocalRank& L : r->ranks) {
+        DeviceGuard g(L.device);
+        if (L.release_recorded[s]) HIP_TRY(hipEventSynchronize(L.released[s]));
+    }
+    if (r->rank0_local) {
+        DeviceGuard g(r->ranks[0].device);
+        HIP_TRY(hipEventSynchronize(r->delivered[s]));
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" int rt_renderer_create(size_t P, const rt_bvh_node* nodes, const rt_aabb* aabbs, const rt_triangle* tris,
+                                  const int32_t* objids, const rt_material* mats, int nmat, const rt_light* lights,
+                                  int nlights, const rt_renderer_opts* o, rt_renderer** out) {
+    if (!out) return set_error(RT_ERR_ARG, "rt_renderer_create: null out");
+    *out = nullptr;
+    rt_renderer_opts d;
+    rt_renderer_opts_default(&d);
+    if (!o) o = &d;
+    const int n = o->n_devices;
+    if (n < 1 || n > 64) return set_error(RT_ERR_ARG, "n_devices must be in 1..64");
+    const int world = o->world_size > 0 ? o->world_size : n;
+    if (world < n || o->rank0 < 0 || o->rank0 + n > world)
+        return set_error(RT_ERR_ARG, "bad world_size / rank0 for n_devices");
+    if (world > n && !o->unique_id) return set_error(RT_ERR_ARG, "a multi-process renderer needs unique_id");
+    if (o->band_rows < 1) return set_error(RT_ERR_ARG, "band_rows must be >= 1");
+    if (o->deliver < RT_DELIVER_P6 || o->deliver > RT_DELIVER_NONE) return set_error(RT_ERR_ARG, "bad deliver");
+    if (o->gather < RT_GATHER_AUTO || o->gather > RT_GATHER_DIRECT) return set_error(RT_ERR_ARG, "bad gather");
+    const int depth = o->depth == 0 ? 3 : o->depth;
+    if (depth < 1 || depth > 8) return set_error(RT_ERR_ARG, "depth must be in 1..8");
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) devs[i] = o->devices ? o->devices[i] : i;
+    const bool distinct = std::set<int>(devs.begin(), devs.end()).size() == size_t(n);
+    int gather = o->gather;
+    if (gather == RT_GATHER_AUTO) gather = (world > 1 && distinct) ? RT_GATHER_RCCL : RT_GATHER_DIRECT;
+    if ((o->flags & RT_RENDERER_SELF_SEND) && o->gather == RT_GATHER_AUTO) gather = RT_GATHER_RCCL;
+    if (gather == RT_GATHER_DIRECT && world > n)
+        return set_error(RT_ERR_UNSUPPORTED, "RT_GATHER_DIRECT needs every rank in this process");
+    if (gather == RT_GATHER_RCCL && !distinct)
+        return set_error(RT_ERR_UNSUPPORTED, "RCCL needs one rank per device; use RT_GATHER_DIRECT for repeated ids");
+    for (int i = 0; i < n; ++i) {
+        int rc = check_device(devs[i]);
+        if (rc != RT_OK) return rc;
+    }
+    std::unique_ptr<rt_renderer> r(new (std::nothrow) rt_renderer());
+    if (!r) return set_error(RT_ERR_NOMEM, "out of memory");
+    r->world = world;
+    r->band_rows = o->band_rows;
+    r->deliver = o->deliver;
+    r->gather = gather;
+    r->depth = depth;
+    r->flags = o->flags;
+    r->rank0_local = o->rank0 == 0;
+    r->ranks.resize(n);
+    r->slot_ticket.assign(depth, 0);
+    int rc;
+    for (int i = 0; i < n; ++i) {
+        LocalRank& L = r->ranks[i];
+        L.device = devs[i];
+        L.rank = o->rank0 + i;
+        DeviceGuard g(L.device);
+        // one host repack + upload, then device-to-device clones
+        if (i == 0) rc = rt_scene_create(L.device, P, nodes, aabbs, tris, objids, mats, nmat, lights, nlights, &L.scene);
+        else rc = rt_scene_clone(r->ranks[0].scene, L.device, &L.scene);
+        if (rc != RT_OK) return rc;
+        HIP_TRY(hipStreamCreateWithFlags(&L.compute, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&L.comm, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking));
+        L.rendered.assign(depth, nullptr);
+        L.released.assign(depth, nullptr);
+        L.release_recorded.assign(depth, false);
+        for (int s = 0; s < depth; ++s) {
+            HIP_TRY(hipEventCreateWithFlags(&L.rendered[s], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&L.released[s], hipEventDisableTiming));
+        }
+    }
+    if (r->rank0_local) {
+        DeviceGuard g(r->ranks[0].device);
+        r->delivered.assign(depth, nullptr);
+        for (int s = 0; s < depth; ++s) HIP_TRY(hipEventCreateWithFlags(&r->delivered[s], hipEventDisableTiming));
+        for (hipEvent_t* ring : {r->tf0, r->tg0, r->tg1, r->td0, r->td1})
+            for (int i = 0; i < kTimeRing; ++i) HIP_TRY(hipEventCreate(&ring[i]));
+    }
+    if (r->uses_rccl() && (rc = init_comms(r.get(), o)) != RT_OK) return rc;
+    *out = r.release();
+    return RT_OK;
+}
+
+extern "C" void rt_renderer_destroy(rt_renderer* r) { delete r; }
+
+extern "C" rt_scene* rt_renderer_scene(rt_renderer* r, int i) {
+    return (r && i >= 0 && i < int(r->ranks.size())) ? r->ranks[i].scene : nullptr;
+}
+extern "C" int rt_renderer_local_ranks(const rt_renderer* r) { return r ? int(r->ranks.size()) : 0; }
+
+extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt_render_opts* opts, uint64_t* ticket) {
+    if (!r || !cam || !opts) return set_error(RT_ERR_ARG, "rt_renderer_submit: null argument");
+    if (cam->pixel_width < 1 || cam->pixel_height < 1) return set_error(RT_ERR_ARG, "camera has no pixels");
+    int rc = ensure_geometry(r, cam->pixel_width, cam->pixel_height);
+    if (rc != RT_OK) return rc;
+    const uint64_t t = r->next;
+    const int s = int(t % uint64_t(r->depth));
+    if ((rc = wait_slot(r, s)) != RT_OK) return rc;
+    const int ring = int(t % kTimeRing);
+    const bool f32 = r->deliver == RT_DELIVER_F32;
+    const bool rccl_mode = r->uses_rccl();
+    const bool self_send = rccl_mode && (r->flags & RT_RENDERER_SELF_SEND);
+    LocalRank& R0 = r->ranks[0];
+    // 1. every local rank renders its bands into strip[s]
+    for (LocalRank& L : r->ranks) {
+        DeviceGuard g(L.device);
+        if (L.release_recorded[s]) HIP_TRY(hipStreamWaitEvent(L.compute, L.released[s], 0));
+        if (&L == &R0 && r->rank0_local) HIP_TRY(hipEventRecord(r->tf0[ring], L.compute));
+        rt_render_opts o = *opts;
+        o.band_rows = r->band_rows;
+        o.band_index = L.rank;
+        o.band_count = r->world;
+        if (L.rows > 0) {
+            void* buf = L.strip[s].p;
+            rc = rt_render_device_p6(L.scene, cam, &o, f32 ? static_cast<float*>(buf) : nullptr, nullptr, nullptr,
+                                     f32 ? nullptr : static_cast<uint8_t*>(buf), L.compute);
+            if (rc != RT_OK) return rc;
+        }
+        HIP_TRY(hipEventRecord(L.rendered[s], L.compute));
+    }
+    r->slot_ticket[s] = t + 1;
+    r->next = t + 1;
+    if (ticket) *ticket = t;
+    if (r->deliver == RT_DELIVER_NONE) {
+        for (LocalRank& L : r->ranks) {
+            DeviceGuard g(L.device);
+            HIP_TRY(hipEventRecord(L.released[s], L.compute));
+            L.release_recorded[s] = true;
+        }
+        if (r->rank0_local) {
+            DeviceGuard g(R0.device);
+            HIP_TRY(hipEventRecord(r->tg0[ring], R0.compute));
+            HIP_TRY(hipEventRecord(r->tg1[ring], R0.compute));
+            HIP_TRY(hipEventRecord(r->td0[ring], R0.compute));
+            HIP_TRY(hipEventRecord(r->td1[ring], R0.compute));
+            HIP_TRY(hipEventRecord(r->delivered[s], R0.compute));
+        }
+        return RT_OK;
+    }
+    const hipMemcpyKind kind = r->deliver == RT_DELIVER_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    char* dst = nullptr;
+    if (r->rank0_local)
+        dst = static_cast<char*>(r->deliver == RT_DELIVER_DEVICE ? r->dev_frame[s].p : r->host[s]);
+    if (rccl_mode) {
+        // 2. strips -> rank 0 (one group: every send and receive of this process)
+        const Rccl& N = rccl();
+        for (LocalRank& L : r->ranks) {
+            DeviceGuard g(L.device);
+            HIP_TRY(hipStreamWaitEvent(L.comm, L.rendered[s], 0));
+            if (&L == &R0 && r->rank0_local) {
+                HIP_TRY(hipStreamWaitEvent(L.comm, r->delivered[s], 0));  // gathered[s] reuse
+                HIP_TRY(hipEventRecord(r->tg0[ring], L.comm));
+            }
+        }
+        NCCL_TRY(N.GroupStart());
+        for (LocalRank& L : r->ranks) {
+            if (L.rank == 0 && !self_send) continue;
+            const size_t bytes = size_t(L.rows) * r->row_bytes;
+            if (bytes == 0) continue;
+            const ncclResult_t e = N.Send(L.strip[s].p, bytes, ncclUint8, 0, L.nccl, L.comm);
+            if (e != ncclSuccess) {
+                (void)N.GroupEnd();
+                return nccl_error(e, "ncclSend");
+            }
+        }
+        if (r->rank0_local) {
+            char* g0 = static_cast<char*>(r->gathered[s].p);
+            for (int q = self_send ? 0 : 1; q < r->world; ++q) {
+                const size_t bytes = size_t(rt_shard_rows(r->H, r->band_rows, q, r->world)) * r->row_bytes;
+                if (bytes == 0) continue;
+                const ncclResult_t e = N.Recv(g0 + size_t(q) * r->strip_cap, bytes, ncclUint8, q, R0.nccl, R0.comm);
+                if (e != ncclSuccess) {
+                    (void)N.GroupEnd();
+                    return nccl_error(e, "ncclRecv");
+                }
+            }
+        }
+        NCCL_TRY(N.GroupEnd());
+        for (LocalRank& L : r->ranks) {
+            DeviceGuard g(L.device);
+            if (L.rank != 0 || self_send) {  // the send was the strip's last reader
+                HIP_TRY(hipEventRecord(L.released[s], L.comm));
+                L.release_recorded[s] = true;
+            }
+        }
+        // 3. rank 0: every strip to its image rows
+        if (r->rank0_local) {
+            DeviceGuard g(R0.device);
+            HIP_TRY(hipEventRecord(r->tg1[ring], R0.comm));
+            HIP_TRY(hipStreamWaitEvent(R0.copy, r->tg1[ring], 0));
+            HIP_TRY(hipStreamWaitEvent(R0.copy, R0.rendered[s], 0));
+            HIP_TRY(hipEventRecord(r->td0[ring], R0.copy));
+            const char* g0 = static_cast<const char*>(r->gathered[s].p);
+            for (int q = 0; q < r->world; ++q) {
+                const char* src = (q == 0 && !self_send) ? static_cast<const char*>(R0.strip[s].p)
+                                                         : g0 + size_t(q) * r->strip_cap;
+                HIP_TRY(scatter_strip(dst, src, q, r->world, r->H, r->band_rows, r->row_bytes, kind, R0.copy));
+            }
+            HIP_TRY(hipEventRecord(r->td1[ring], R0.copy));
+            HIP_TRY(hipEventRecord(r->delivered[s], R0.copy));
+            if (!self_send) {
+                HIP_TRY(hipEventRecord(R0.released[s], R0.copy));
+                R0.release_recorded[s] = true;
+            }
+        }
+        return RT_OK;
+    }
+    // 2'. DIRECT: every local rank copies its own bands into the frame (all ranks are local)
+    for (LocalRank& L : r->ranks) {
+        DeviceGuard g(L.device);
+        HIP_TRY(hipStreamWaitEvent(L.copy, L.rendered[s], 0));
+        if (&L == &R0) {
+            HIP_TRY(hipEventRecord(r->tg0[ring], L.copy));
+            HIP_TRY(hipEventRecord(r->tg1[ring], L.copy));
+            HIP_TRY(hipEventRecord(r->td0[ring], L.copy));
+        }
+        HIP_TRY(scatter_strip(dst, static_cast<const char*>(L.strip[s].p), L.rank, r->world, r->H, r->band_rows,
+                              r->row_bytes, kind, L.copy));
+        HIP_TRY(hipEventRecord(L.released[s], L.copy));
+        L.release_recorded[s] = true;
+    }
+    {
+        DeviceGuard g(R0.device);
+        for (size_t i = 1; i < r->ranks.size(); ++i)  // the frame is complete when every copy is
+            HIP_TRY(hipStreamWaitEvent(R0.copy, r->ranks[i].released[s], 0));
+        HIP_TRY(hipEventRecord(r->td1[ring], R0.copy));
+        HIP_TRY(hipEventRecord(r->delivered[s], R0.copy));
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_renderer_wait(rt_renderer* r, uint64_t ticket, const void** frame, size_t* bytes) {
+    if (frame) *frame = nullptr;
+    if (bytes) *bytes = 0;
+    if (!r) return set_error(RT_ERR_ARG, "rt_renderer_wait: null renderer");
+    if (ticket >= r->next || ticket + uint64_t(r->depth) < r->next)
+        return set_error(RT_ERR_ARG, "rt_renderer_wait: frame not submitted or no longer held");
+    const int s = int(ticket % uint64_t(r->depth));
+    for (LocalRank& L : r->ranks) {
+        DeviceGuard g(L.device);
+        if (L.release_recorded[s]) HIP_TRY(hipEventSynchronize(L.released[s]));
+        else HIP_TRY(hipEventSynchronize(L.rendered[s]));
+    }
+    if (r->rank0_local) {
+        DeviceGuard g(r->ranks[0].device);
+        HIP_TRY(hipEventSynchronize(r->delivered[s]));
+        if (r->deliver == RT_DELIVER_DEVICE) {
+            if (frame) *frame = r->dev_frame[s].p;
+            if (bytes) *bytes = r->frame_bytes;
+        } else if (r->deliver != RT_DELIVER_NONE) {
+            if (frame) *frame = r->host[s];
+            if (bytes) *bytes = r->frame_bytes;
+        }
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_renderer_render(rt_renderer* r, const rt_camera* cam, const rt_render_opts* opts, void* out,
+                                  size_t cap) {
+    uint64_t t = 0;
+    int rc = rt_renderer_submit(r, cam, opts, &t);
+    if (rc != RT_OK) return rc;
+    const void* f = nullptr;
+    size_t n = 0;
+    if ((rc = rt_renderer_wait(r, t, &f, &n)) != RT_OK) return rc;
+    if (!r->rank0_local || r->deliver == RT_DELIVER_NONE) return RT_OK;
+    if (!out || cap < n) return set_error(RT_ERR_ARG, "rt_renderer_render: output smaller than the frame");
+    if (r->deliver == RT_DELIVER_DEVICE) {
+        DeviceGuard g(r->ranks[0].device);
+        HIP_TRY(hipMemcpy(out, f, n, hipMemcpyDeviceToHost));
+    } else {
+        std::memcpy(out, f, n);
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_renderer_times(rt_renderer* r, int kind, float* ms_out, int max, int* n_out) {
+    if (n_out) *n_out = 0;
+    if (!r || max < 0 || (max > 0 && !ms_out) || kind < RT_TIME_GATHER || kind > RT_TIME_FRAME)
+        return set_error(RT_ERR_ARG, "rt_renderer_times: bad args");
+    if (!r->rank0_local) return RT_OK;
+    DeviceGuard g(r->ranks[0].device);
+    const uint64_t have = std::min<uint64_t>(r->next, uint64_t(kTimeRing));  // the ring keeps the last 256
+    const int n = int(std::min<uint64_t>(have, uint64_t(max)));
+    for (int k = 0; k < n; ++k) {
+        const int i = int((r->next - uint64_t(n) + uint64_t(k)) % kTimeRing);
+        hipEvent_t a = kind == RT_TIME_GATHER ? r->tg0[i] : kind == RT_TIME_DELIVER ? r->td0[i] : r->tf0[i];
+        hipEvent_t b = kind == RT_TIME_GATHER ? r->tg1[i] : r->td1[i];
+        HIP_TRY(hipEventSynchronize(b));
+        HIP_TRY(hipEventElapsedTime(&ms_out[k], a, b));
+    }
+    if (n_out) *n_out = n;
+    return RT_OK;
+}
+
+extern "C" int rt_render_reference_gpus(size_t P, int W, int H, const rt_camera* cam, rt_vec3 miss, int max_depth,
+                                        int spp, const rt_bvh_node* nodes, const rt_aabb* aabbs,
+                                        const rt_triangle* tris, const int32_t* objids, const rt_material* mats,
+                                        int nmat, const rt_light* lights, int nlights, int diffuse_bounce,
+                                        int n_gpus, rt_vec3* output) {
+    if (!cam || !output) return set_error(RT_ERR_ARG, "rt_render_reference_gpus: null argument");
+    if (W != cam->pixel_width || H != cam->pixel_height)
+        return set_error(RT_ERR_ARG, "W/H must match the camera's pixel dimensions");
+    rt_renderer_opts ro;
+    rt_renderer_opts_default(&ro);
+    ro.n_devices = n_gpus;
+    ro.deliver = RT_DELIVER_F32;
+    ro.depth = 1;
+    rt_renderer* r = nullptr;
+    int rc = rt_renderer_create(P, nodes, aabbs, tris, objids, mats, nmat, lights, nlights, &ro, &r);
+    if (rc != RT_OK) return rc;
+    rt_render_opts o;
+    rt_render_opts_default(&o);
+    o.max_depth = max_depth;
+    o.spp = spp;
+    o.diffuse_bounce = diffuse_bounce;
+    o.miss_color = miss;
+    rc = rt_renderer_render(r, cam, &o, output, size_t(W) * size_t(H) * sizeof(rt_vec3));
+    rt_renderer_destroy(r);
+    return rc;
+}

@@ -128,9 +128,10 @@ def test_gloo_p6_epilogue_on_one_gpu(world):
 @pytest.mark.gpu
 @pytest.mark.parametrize("gather", ["p6", "f32"])
 def test_bench_two_ranks_gloo_on_one_gpu(gather):
-    """bench.py's N-rank step (band shards, async gather of the frame's P6 bytes or float strips,
-    un-permute on rank 0) rehearsed with 2 gloo ranks sharing one GPU: the frame delivered by the
-    timed steps and the float frame match the reference's c3 image."""
+    """bench.py's N-rank step on the torch.distributed launcher (--comm torch: band shards, async
+    gather of the frame's P6 bytes or float strips, un-permute on rank 0, copy to host) rehearsed
+    with 2 gloo ranks sharing one GPU: the frame delivered by the timed steps matches the
+    reference's c3 image.  (The native RCCL renderer needs one GPU per rank.)"""
     import json
     import subprocess
     import sys
@@ -139,12 +140,13 @@ def test_bench_two_ranks_gloo_on_one_gpu(gather):
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", str(repo / "bench.py"), "--gpus", "2",
-           "--steps", "3", "--warmup", "1", "--backend", "gloo", "--gather", gather]
+           "--steps", "3", "--warmup", "1", "--comm", "torch", "--backend", "gloo", "--gather-payload", gather]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(repo))
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0
     par = line["parity"]
-    assert par["rgb_maxabs"] == 0.0 and par["ppm_identical"]
     if gather == "p6":
         assert par["timed_step_ppm_identical"]
+    else:
+        assert par["timed_step_rgb_maxabs"] == 0.0

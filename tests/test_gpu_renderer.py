@@ -1,0 +1,207 @@
+"""The frame renderer (rt_renderer, include/rt_mi355x.h) through the C ABI: render(scene, camera)
+-> frame in host memory, sharded over band ranks, gathered over RCCL or copied per rank.
+
+Bar: the delivered frame equals the reference's own c3 output bit for bit
+(tests/golden/scenes/c3_full: the float framebuffer of G/include/query.cu:130-166 and the P6
+file write_p6 made of it), for every rank count, gather path, delivery kind and pipeline depth.
+On one GPU several ranks share device 0 (RT_GATHER_DIRECT); the RCCL path runs at world 1 with
+rank 0's strip sent to itself (RT_RENDERER_SELF_SEND), which exercises the grouped
+ncclSend/ncclRecv sequence the N-GPU job uses.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import gzip
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, host_scene, oracle_camera
+from oracle import pyoracle as orc
+
+import raytracinginonesemester_amd as rt
+from raytracinginonesemester_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+W, H, SPP = 1920, 1080, 16
+
+
+@pytest.fixture(scope="module")
+def frog():
+    return host_scene("frog.json")
+
+
+@pytest.fixture(scope="module")
+def golden():
+    fb = np.frombuffer(gzip.open(GOLDEN / "scenes" / "c3_full" / "fb.f32.gz").read(), np.float32).reshape(H, W, 3)
+    ppm = gzip.open(GOLDEN / "scenes" / "c3_full" / "image.ppm.gz").read()
+    return fb, np.frombuffer(ppm[17:], np.uint8).reshape(H, W, 3)
+
+
+def _opts(hs, spp=SPP, max_depth=1):
+    o, jit = rt.DeviceScene.make_opts(spp=spp, max_depth=max_depth, miss_color=hs.settings["miss_color"])
+    return o, jit
+
+
+@pytest.mark.parametrize("devices", [(0,), (0, 0), (0, 0, 0), (0, 0, 0, 0), (0,) * 8])
+def test_direct_bands_reassemble_p6(frog, golden, devices):
+    """Band shards for world 1/2/3/4/8 on one GPU, each rank copying its bands into the host frame."""
+    r = rt.Renderer.from_host(frog, devices=devices, gather=rt.RT_GATHER_DIRECT)
+    try:
+        p6 = r.render(frog.camera(W, H), spp=SPP, max_depth=1, miss_color=frog.settings["miss_color"])
+        assert np.array_equal(p6, golden[1]), f"{len(devices)} ranks: P6 differs from the reference image"
+        # each rank's share of the work, for the record
+        for i in range(r.local_ranks):
+            assert len(r.scene(i).frame_times(1)) == 1
+    finally:
+        r.close()
+
+
+@pytest.mark.parametrize("devices", [(0,), (0, 0, 0)])
+def test_direct_bands_reassemble_f32(frog, golden, devices):
+    r = rt.Renderer.from_host(frog, devices=devices, gather=rt.RT_GATHER_DIRECT, deliver=rt.RT_DELIVER_F32)
+    try:
+        fb = r.render(frog.camera(W, H), spp=SPP, max_depth=1, miss_color=frog.settings["miss_color"])
+        assert fb.view(np.uint32).tobytes() == golden[0].view(np.uint32).tobytes()
+    finally:
+        r.close()
+
+
+def test_rccl_self_send(frog, golden):
+    """RCCL path at world 1: ncclCommInitAll, grouped send/recv of the strip to rank 0, 2-D copy out."""
+    r = rt.Renderer.from_host(frog, devices=(0,), gather=rt.RT_GATHER_RCCL, flags=rt.RT_RENDERER_SELF_SEND)
+    try:
+        cam = frog.camera(W, H)
+        for _ in range(3):
+            p6 = r.render(cam, spp=SPP, max_depth=1, miss_color=frog.settings["miss_color"])
+            assert np.array_equal(p6, golden[1])
+        g = r.times(rt.RT_TIME_GATHER, 3)
+        assert len(g) == 3 and np.all(g >= 0)
+    finally:
+        r.close()
+
+
+def test_rccl_multiprocess_id_world1(frog, golden):
+    """The multi-process form (ncclCommInitRank with a shared unique id) at world 1."""
+    uid = rt.comm_unique_id()
+    assert len(uid) == 128
+    r = rt.Renderer.from_host(frog, devices=(0,), world_size=1, rank0=0, unique_id=uid, gather=rt.RT_GATHER_RCCL,
+                              flags=rt.RT_RENDERER_SELF_SEND)
+    try:
+        p6 = r.render(frog.camera(W, H), spp=SPP, max_depth=1, miss_color=frog.settings["miss_color"])
+        assert np.array_equal(p6, golden[1])
+    finally:
+        r.close()
+
+
+def test_rccl_rejects_repeated_devices(frog):
+    with pytest.raises(rt.RTError) as e:
+        rt.Renderer.from_host(frog, devices=(0, 0), gather=rt.RT_GATHER_RCCL)
+    assert e.value.code == -7
+
+
+def test_pipelined_frames_all_identical(frog, golden):
+    """depth 3: frames k+1, k+2 render while frame k is copied; every delivered frame is the image."""
+    r = rt.Renderer.from_host(frog, devices=(0, 0), gather=rt.RT_GATHER_DIRECT, depth=3)
+    try:
+        cam = frog.camera(W, H)
+        o, _j = _opts(frog)
+        tickets = [r.submit(cam, o) for _ in range(2)]
+        n_checked = 0
+        for k in range(10):
+            t = tickets.pop(0)
+            addr, n = r.wait(t)
+            assert n == W * H * 3
+            got = np.ctypeslib.as_array((C.c_uint8 * n).from_address(addr)).reshape(H, W, 3)
+            assert np.array_equal(got, golden[1]), f"frame {t}"
+            n_checked += 1
+            tickets.append(r.submit(cam, o))
+        for t in tickets:
+            r.wait(t)
+        assert n_checked == 10
+        d = r.times(rt.RT_TIME_DELIVER, 12)
+        f = r.times(rt.RT_TIME_FRAME, 12)
+        assert len(d) == 12 and len(f) == 12 and np.all(f >= d)
+    finally:
+        r.close()
+
+
+def test_wait_rejects_stale_ticket(frog):
+    r = rt.Renderer.from_host(frog, devices=(0,), depth=2)
+    try:
+        cam = frog.camera(64, 36)
+        o, _j = _opts(frog, spp=4)
+        ts = [r.submit(cam, o) for _ in range(4)]
+        with pytest.raises(rt.RTError):
+            r.wait(ts[0])  # slot reused by ts[2]
+        r.wait(ts[3])
+    finally:
+        r.close()
+
+
+def test_device_delivery_and_partial_band(frog):
+    """RT_DELIVER_DEVICE (frame assembled in rank 0's HBM) and an image height that is not a
+    multiple of the band height (a partial last band), against the oracle."""
+    cam = frog.camera(160, 37)
+    o, _j = _opts(frog, spp=4)
+    oc = oracle_camera(cam)
+    ref, _, _ = orc.render_g(frog.num_triangles, oc, frog.nodes, frog.aabbs, frog.triangles, frog.tri_object_ids,
+                             frog.materials, frog.lights, spp=4, max_depth=1, miss=frog.settings["miss_color"],
+                             aov=True)
+    want = orc.ppm_quantize(ref, 255, True, True).astype(np.uint8).reshape(37, 160, 3)
+    for devices in [(0,), (0, 0, 0)]:
+        r = rt.Renderer.from_host(frog, devices=devices, gather=rt.RT_GATHER_DIRECT, deliver=rt.RT_DELIVER_DEVICE)
+        try:
+            got = r.render(cam, spp=4, max_depth=1, miss_color=frog.settings["miss_color"])
+            assert np.array_equal(got, want), devices
+        finally:
+            r.close()
+        r = rt.Renderer.from_host(frog, devices=devices, gather=rt.RT_GATHER_DIRECT, deliver=rt.RT_DELIVER_F32)
+        try:
+            got = r.render(cam, spp=4, max_depth=1, miss_color=frog.settings["miss_color"])
+            assert float(np.abs(got - ref).max()) <= 2e-6
+        finally:
+            r.close()
+
+
+def test_reference_signature_multi_gpu(frog, golden):
+    """rt_render_reference_gpus (the reference signature + n_gpus) at n_gpus 1 equals the reference."""
+    cam = frog.camera(W, H)
+    out = np.zeros(W * H * 3, np.float32)
+    mats = frog.materials
+    rt.render(frog.num_triangles, W, H, cam, frog.settings["miss_color"], 1, SPP, frog.nodes, frog.aabbs,
+              frog.triangles, frog.tri_object_ids, mats, len(mats), frog.lights, len(frog.lights), True, out)
+    assert out.view(np.uint32).tobytes() == golden[0].view(np.uint32).tobytes()
+    dev = rt.device_count()
+    if dev >= 2:
+        out2 = np.zeros_like(out)
+        rt.render(frog.num_triangles, W, H, cam, frog.settings["miss_color"], 1, SPP, frog.nodes, frog.aabbs,
+                  frog.triangles, frog.tri_object_ids, mats, len(mats), frog.lights, len(frog.lights), True, out2,
+                  n_gpus=min(dev, 8))
+        assert out2.view(np.uint32).tobytes() == out.view(np.uint32).tobytes()
+
+
+def test_scene_frames_on_two_streams(frog, golden):
+    """Back-to-back frames of one scene on two streams (the scene's tile lists are reused per
+    frame: the second frame must wait for the first)."""
+    ds = rt.DeviceScene.from_host(frog, device=0)
+    cam = frog.camera(W, H)
+    o, _j = _opts(frog)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.zeros((H, W, 3), dtype=torch.float32, device="cuda") for _ in range(4)]
+    for k, buf in enumerate(outs):
+        st = (s1 if k % 2 == 0 else s2).cuda_stream
+        ds.render_device(cam, o, buf.data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    for buf in outs:
+        assert buf.cpu().numpy().view(np.uint32).tobytes() == golden[0].view(np.uint32).tobytes()
+    ds.close()
+
+
+def test_renderer_exports():
+    lib = L.lib()
+    for name in ["rt_renderer_create", "rt_renderer_submit", "rt_renderer_wait", "rt_renderer_times",
+                 "rt_render_reference_gpus", "rt_comm_unique_id", "rt_scene_clone"]:
+        assert hasattr(lib, name)

@@ -2221,6 +2221,17 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     return rc;
 }
 
+void rt::scene_frame_events(const rt_scene* s, hipEvent_t* first, hipEvent_t* last) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (s && s->launches > 0) {
+        const int slot = int((s->launches - 1) % rt_scene::kRing);
+        a = s->ev0[slot];
+        b = s->ev1[slot];
+    }
+    if (first) *first = a;
+    if (last) *last = b;
+}
+
 namespace {
 int event_times(const rt_scene* s, const hipEvent_t* from, float* ms_out, int max, int* n_out) {
     if (!s || max < 0 || (max > 0 && !ms_out)) return set_error(RT_ERR_ARG, "kernel times: bad args");

@@ -63,5 +63,10 @@ struct DeviceGuard {
     ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
+// The HIP events around the most recent frame of a scene (rt_render_device*, rt_device.hip):
+// before its first launch and after its render kernel, both on the frame's stream and owned
+// by the scene (valid for the scene's next 255 frames); nullptr before the first frame.
+// rt_renderer synchronises on these instead of recording events of its own on that stream.
+void scene_frame_events(const rt_scene* s, hipEvent_t* first, hipEvent_t* last);
 
 }  // namespace rt

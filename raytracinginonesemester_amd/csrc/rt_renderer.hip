@@ -128,9 +128,12 @@ struct LocalRank {
     ncclComm_t nccl = nullptr;
     int rows = 0;                      // rows of this rank's strip for the current geometry
     std::vector<DevBuf> strip;         // per slot: rows*W*3 bytes (P6) or floats (F32)
-    std::vector<hipEvent_t> rendered;  // per slot, on compute
-    std::vector<hipEvent_t> released;  // per slot: the last reader of the strip finished
-    std::vector<bool> release_recorded;
+    // Per slot.  The compute stream carries nothing but the scene's frame (its launches and its
+    // own timing events): `rendered` is the scene's event after the frame's render kernel
+    // (owned by the scene), nullptr when the rank has no rows.  `released` is what frees the
+    // strip for reuse: released_ev (owned, recorded on comm/copy after the strip's last reader),
+    // an alias of `rendered` (nothing reads the strip) or nullptr.
+    std::vector<hipEvent_t> rendered, released, released_ev;
 };
 
 }  // namespace
@@ -151,12 +154,15 @@ struct rt_renderer {
     std::vector<DevBuf> gathered;       // RCCL: world strips of strip_cap bytes
     std::vector<DevBuf> dev_frame;      // RT_DELIVER_DEVICE
     std::vector<void*> host;            // pinned host frames
-    std::vector<hipEvent_t> delivered;  // on ranks[0].copy
+    std::vector<hipEvent_t> delivered;  // per slot: delivered_ev[s], or rank 0's `rendered` (deliver none)
+    std::vector<hipEvent_t> delivered_ev;  // owned, on ranks[0].copy
     std::vector<uint64_t> slot_ticket;  // frame held by each slot (+1; 0 = none)
     uint64_t next = 0;
-    // timing ring (rank 0's process): frame start, gather start/end, delivery start/end
-    hipEvent_t tf0[kTimeRing] = {}, tg0[kTimeRing] = {}, tg1[kTimeRing] = {}, td0[kTimeRing] = {},
-               td1[kTimeRing] = {};
+    // timing ring (rank 0's process): owned events on the comm / copy streams (gather start/end,
+    // delivery start/end), and per frame and RT_TIME_* kind the (start, end) pair to read
+    // (nullptr: the step did not run, 0 ms).  The frame's start is the scene's own first event.
+    hipEvent_t tg0[kTimeRing] = {}, tg1[kTimeRing] = {}, td0[kTimeRing] = {}, td1[kTimeRing] = {};
+    hipEvent_t ta[3][kTimeRing] = {}, tb[3][kTimeRing] = {};
     bool owns_scenes = true;
 
     ~rt_renderer() { release(); }
@@ -183,10 +189,10 @@ struct rt_renderer {
             DeviceGuard g(L.device);
             if (L.nccl && rccl().ok) (void)rccl().CommDestroy(L.nccl);
             L.nccl = nullptr;
-            for (hipEvent_t e : L.rendered) (void)hipEventDestroy(e);
-            for (hipEvent_t e : L.released) (void)hipEventDestroy(e);
+            for (hipEvent_t e : L.released_ev) (void)hipEventDestroy(e);
             L.rendered.clear();
             L.released.clear();
+            L.released_ev.clear();
             if (L.compute) (void)hipStreamDestroy(L.compute);
             if (L.comm) (void)hipStreamDestroy(L.comm);
             if (L.copy) (void)hipStreamDestroy(L.copy);
@@ -196,9 +202,10 @@ struct rt_renderer {
         }
         if (!ranks.empty()) {
             DeviceGuard g(ranks[0].device);
-            for (hipEvent_t e : delivered) (void)hipEventDestroy(e);
+            for (hipEvent_t e : delivered_ev) (void)hipEventDestroy(e);
             delivered.clear();
-            for (hipEvent_t* ring : {tf0, tg0, tg1, td0, td1})
+            delivered_ev.clear();
+            for (hipEvent_t* ring : {tg0, tg1, td0, td1})
                 for (int i = 0; i < kTimeRing; ++i)
                     if (ring[i]) (void)hipEventDestroy(ring[i]), ring[i] = nullptr;
         }
@@ -281,8 +288,10 @@ int ensure_geometry(rt_renderer* r, int W, int H) {
         L.strip.resize(r->depth);
         for (DevBuf& b : L.strip)
             if ((rc = b.alloc(r->strip_cap)) != RT_OK) return rc;
-        std::fill(L.release_recorded.begin(), L.release_recorded.end(), false);
+        std::fill(L.rendered.begin(), L.rendered.end(), nullptr);
+        std::fill(L.released.begin(), L.released.end(), nullptr);
     }
+    std::fill(r->delivered.begin(), r->delivered.end(), nullptr);
     if (r->rank0_local) {
         DeviceGuard g(r->ranks[0].device);
         if (r->uses_rccl()) {
@@ -309,9 +318,9 @@ int wait_slot(rt_renderer* r, int s) {
     if (r->slot_ticket[s] == 0) return RT_OK;
     for (LocalRank& L : r->ranks) {
         DeviceGuard g(L.device);
-        if (L.release_recorded[s]) HIP_TRY(hipEventSynchronize(L.released[s]));
+        if (L.released[s]) HIP_TRY(hipEventSynchronize(L.released[s]));
     }
-    if (r->rank0_local) {
+    if (r->rank0_local && r->delivered[s]) {
         DeviceGuard g(r->ranks[0].device);
         HIP_TRY(hipEventSynchronize(r->delivered[s]));
     }
@@ -379,17 +388,15 @@ extern "C" int rt_renderer_create(size_t P, const rt_bvh_node* nodes, const rt_a
         HIP_TRY(hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking));
         L.rendered.assign(depth, nullptr);
         L.released.assign(depth, nullptr);
-        L.release_recorded.assign(depth, false);
-        for (int s = 0; s < depth; ++s) {
-            HIP_TRY(hipEventCreateWithFlags(&L.rendered[s], hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&L.released[s], hipEventDisableTiming));
-        }
+        L.released_ev.assign(depth, nullptr);
+        for (int s = 0; s < depth; ++s) HIP_TRY(hipEventCreateWithFlags(&L.released_ev[s], hipEventDisableTiming));
     }
     if (r->rank0_local) {
         DeviceGuard g(r->ranks[0].device);
         r->delivered.assign(depth, nullptr);
-        for (int s = 0; s < depth; ++s) HIP_TRY(hipEventCreateWithFlags(&r->delivered[s], hipEventDisableTiming));
-        for (hipEvent_t* ring : {r->tf0, r->tg0, r->tg1, r->td0, r->td1})
+        r->delivered_ev.assign(depth, nullptr);
+        for (int s = 0; s < depth; ++s) HIP_TRY(hipEventCreateWithFlags(&r->delivered_ev[s], hipEventDisableTiming));
+        for (hipEvent_t* ring : {r->tg0, r->tg1, r->td0, r->td1})
             for (int i = 0; i < kTimeRing; ++i) HIP_TRY(hipEventCreate(&ring[i]));
     }
     if (r->uses_rccl() && (rc = init_comms(r.get(), o)) != RT_OK) return rc;
@@ -411,46 +418,40 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
     if (rc != RT_OK) return rc;
     const uint64_t t = r->next;
     const int s = int(t % uint64_t(r->depth));
+    // The slot's previous frame is waited for here, on the host: the streams below need no
+    // waits for buffer reuse (every wait or event on the compute stream costs GPU time between
+    // the frame's kernels).
     if ((rc = wait_slot(r, s)) != RT_OK) return rc;
     const int ring = int(t % kTimeRing);
     const bool f32 = r->deliver == RT_DELIVER_F32;
     const bool rccl_mode = r->uses_rccl();
     const bool self_send = rccl_mode && (r->flags & RT_RENDERER_SELF_SEND);
     LocalRank& R0 = r->ranks[0];
-    // 1. every local rank renders its bands into strip[s]
+    for (int k = 0; k < 3; ++k) r->ta[k][ring] = r->tb[k][ring] = nullptr;
+    // 1. every local rank renders its bands into strip[s]: the scene's frame and nothing else
     for (LocalRank& L : r->ranks) {
+        L.rendered[s] = L.released[s] = nullptr;
+        if (&L == &R0 && r->rank0_local) r->delivered[s] = nullptr;
+        if (L.rows == 0) continue;
         DeviceGuard g(L.device);
-        if (L.release_recorded[s]) HIP_TRY(hipStreamWaitEvent(L.compute, L.released[s], 0));
-        if (&L == &R0 && r->rank0_local) HIP_TRY(hipEventRecord(r->tf0[ring], L.compute));
         rt_render_opts o = *opts;
         o.band_rows = r->band_rows;
         o.band_index = L.rank;
         o.band_count = r->world;
-        if (L.rows > 0) {
-            void* buf = L.strip[s].p;
-            rc = rt_render_device_p6(L.scene, cam, &o, f32 ? static_cast<float*>(buf) : nullptr, nullptr, nullptr,
-                                     f32 ? nullptr : static_cast<uint8_t*>(buf), L.compute);
-            if (rc != RT_OK) return rc;
-        }
-        HIP_TRY(hipEventRecord(L.rendered[s], L.compute));
+        void* buf = L.strip[s].p;
+        rc = rt_render_device_p6(L.scene, cam, &o, f32 ? static_cast<float*>(buf) : nullptr, nullptr, nullptr,
+                                 f32 ? nullptr : static_cast<uint8_t*>(buf), L.compute);
+        if (rc != RT_OK) return rc;
+        hipEvent_t first = nullptr;
+        rt::scene_frame_events(L.scene, &first, &L.rendered[s]);
+        if (&L == &R0 && r->rank0_local) r->ta[RT_TIME_FRAME][ring] = first;
     }
     r->slot_ticket[s] = t + 1;
     r->next = t + 1;
     if (ticket) *ticket = t;
     if (r->deliver == RT_DELIVER_NONE) {
-        for (LocalRank& L : r->ranks) {
-            DeviceGuard g(L.device);
-            HIP_TRY(hipEventRecord(L.released[s], L.compute));
-            L.release_recorded[s] = true;
-        }
-        if (r->rank0_local) {
-            DeviceGuard g(R0.device);
-            HIP_TRY(hipEventRecord(r->tg0[ring], R0.compute));
-            HIP_TRY(hipEventRecord(r->tg1[ring], R0.compute));
-            HIP_TRY(hipEventRecord(r->td0[ring], R0.compute));
-            HIP_TRY(hipEventRecord(r->td1[ring], R0.compute));
-            HIP_TRY(hipEventRecord(r->delivered[s], R0.compute));
-        }
+        for (LocalRank& L : r->ranks) L.released[s] = L.rendered[s];
+        if (r->rank0_local) r->delivered[s] = r->tb[RT_TIME_FRAME][ring] = R0.rendered[s];
         return RT_OK;
     }
     const hipMemcpyKind kind = r->deliver == RT_DELIVER_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -462,11 +463,8 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
         const Rccl& N = rccl();
         for (LocalRank& L : r->ranks) {
             DeviceGuard g(L.device);
-            HIP_TRY(hipStreamWaitEvent(L.comm, L.rendered[s], 0));
-            if (&L == &R0 && r->rank0_local) {
-                HIP_TRY(hipStreamWaitEvent(L.comm, r->delivered[s], 0));  // gathered[s] reuse
-                HIP_TRY(hipEventRecord(r->tg0[ring], L.comm));
-            }
+            if (L.rendered[s]) HIP_TRY(hipStreamWaitEvent(L.comm, L.rendered[s], 0));
+            if (&L == &R0 && r->rank0_local) HIP_TRY(hipEventRecord(r->tg0[ring], L.comm));
         }
         NCCL_TRY(N.GroupStart());
         for (LocalRank& L : r->ranks) {
@@ -493,10 +491,10 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
         }
         NCCL_TRY(N.GroupEnd());
         for (LocalRank& L : r->ranks) {
-            DeviceGuard g(L.device);
-            if (L.rank != 0 || self_send) {  // the send was the strip's last reader
-                HIP_TRY(hipEventRecord(L.released[s], L.comm));
-                L.release_recorded[s] = true;
+            if ((L.rank != 0 || self_send) && L.rows > 0) {  // the send was the strip's last reader
+                DeviceGuard g(L.device);
+                HIP_TRY(hipEventRecord(L.released_ev[s], L.comm));
+                L.released[s] = L.released_ev[s];
             }
         }
         // 3. rank 0: every strip to its image rows
@@ -504,7 +502,7 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
             DeviceGuard g(R0.device);
             HIP_TRY(hipEventRecord(r->tg1[ring], R0.comm));
             HIP_TRY(hipStreamWaitEvent(R0.copy, r->tg1[ring], 0));
-            HIP_TRY(hipStreamWaitEvent(R0.copy, R0.rendered[s], 0));
+            if (!self_send && R0.rendered[s]) HIP_TRY(hipStreamWaitEvent(R0.copy, R0.rendered[s], 0));
             HIP_TRY(hipEventRecord(r->td0[ring], R0.copy));
             const char* g0 = static_cast<const char*>(r->gathered[s].p);
             for (int q = 0; q < r->world; ++q) {
@@ -513,34 +511,43 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
                 HIP_TRY(scatter_strip(dst, src, q, r->world, r->H, r->band_rows, r->row_bytes, kind, R0.copy));
             }
             HIP_TRY(hipEventRecord(r->td1[ring], R0.copy));
-            HIP_TRY(hipEventRecord(r->delivered[s], R0.copy));
-            if (!self_send) {
-                HIP_TRY(hipEventRecord(R0.released[s], R0.copy));
-                R0.release_recorded[s] = true;
-            }
+            HIP_TRY(hipEventRecord(r->delivered_ev[s], R0.copy));
+            r->delivered[s] = r->delivered_ev[s];
+            if (!self_send && R0.rows > 0) R0.released[s] = r->delivered_ev[s];
+            r->ta[RT_TIME_GATHER][ring] = r->tg0[ring];
+            r->tb[RT_TIME_GATHER][ring] = r->tg1[ring];
+            r->ta[RT_TIME_DELIVER][ring] = r->td0[ring];
+            r->tb[RT_TIME_DELIVER][ring] = r->tb[RT_TIME_FRAME][ring] = r->td1[ring];
         }
         return RT_OK;
     }
     // 2'. DIRECT: every local rank copies its own bands into the frame (all ranks are local)
+    {
+        DeviceGuard g(R0.device);
+        if (R0.rendered[s]) HIP_TRY(hipStreamWaitEvent(R0.copy, R0.rendered[s], 0));
+        HIP_TRY(hipEventRecord(r->td0[ring], R0.copy));
+    }
     for (LocalRank& L : r->ranks) {
+        if (!L.rendered[s]) continue;
         DeviceGuard g(L.device);
-        HIP_TRY(hipStreamWaitEvent(L.copy, L.rendered[s], 0));
-        if (&L == &R0) {
-            HIP_TRY(hipEventRecord(r->tg0[ring], L.copy));
-            HIP_TRY(hipEventRecord(r->tg1[ring], L.copy));
-            HIP_TRY(hipEventRecord(r->td0[ring], L.copy));
-        }
+        if (&L != &R0) HIP_TRY(hipStreamWaitEvent(L.copy, L.rendered[s], 0));
         HIP_TRY(scatter_strip(dst, static_cast<const char*>(L.strip[s].p), L.rank, r->world, r->H, r->band_rows,
                               r->row_bytes, kind, L.copy));
-        HIP_TRY(hipEventRecord(L.released[s], L.copy));
-        L.release_recorded[s] = true;
+        if (&L != &R0) {
+            HIP_TRY(hipEventRecord(L.released_ev[s], L.copy));
+            L.released[s] = L.released_ev[s];
+        }
     }
     {
         DeviceGuard g(R0.device);
         for (size_t i = 1; i < r->ranks.size(); ++i)  // the frame is complete when every copy is
-            HIP_TRY(hipStreamWaitEvent(R0.copy, r->ranks[i].released[s], 0));
+            if (r->ranks[i].released[s]) HIP_TRY(hipStreamWaitEvent(R0.copy, r->ranks[i].released[s], 0));
         HIP_TRY(hipEventRecord(r->td1[ring], R0.copy));
-        HIP_TRY(hipEventRecord(r->delivered[s], R0.copy));
+        HIP_TRY(hipEventRecord(r->delivered_ev[s], R0.copy));
+        r->delivered[s] = r->delivered_ev[s];
+        if (R0.rendered[s]) R0.released[s] = r->delivered_ev[s];
+        r->ta[RT_TIME_DELIVER][ring] = r->td0[ring];
+        r->tb[RT_TIME_DELIVER][ring] = r->tb[RT_TIME_FRAME][ring] = r->td1[ring];
     }
     return RT_OK;
 }
@@ -554,12 +561,12 @@ extern "C" int rt_renderer_wait(rt_renderer* r, uint64_t ticket, const void** fr
     const int s = int(ticket % uint64_t(r->depth));
     for (LocalRank& L : r->ranks) {
         DeviceGuard g(L.device);
-        if (L.release_recorded[s]) HIP_TRY(hipEventSynchronize(L.released[s]));
-        else HIP_TRY(hipEventSynchronize(L.rendered[s]));
+        if (L.released[s]) HIP_TRY(hipEventSynchronize(L.released[s]));
+        else if (L.rendered[s]) HIP_TRY(hipEventSynchronize(L.rendered[s]));
     }
     if (r->rank0_local) {
         DeviceGuard g(r->ranks[0].device);
-        HIP_TRY(hipEventSynchronize(r->delivered[s]));
+        if (r->delivered[s]) HIP_TRY(hipEventSynchronize(r->delivered[s]));
         if (r->deliver == RT_DELIVER_DEVICE) {
             if (frame) *frame = r->dev_frame[s].p;
             if (bytes) *bytes = r->frame_bytes;
@@ -600,8 +607,9 @@ extern "C" int rt_renderer_times(rt_renderer* r, int kind, float* ms_out, int ma
     const int n = int(std::min<uint64_t>(have, uint64_t(max)));
     for (int k = 0; k < n; ++k) {
         const int i = int((r->next - uint64_t(n) + uint64_t(k)) % kTimeRing);
-        hipEvent_t a = kind == RT_TIME_GATHER ? r->tg0[i] : kind == RT_TIME_DELIVER ? r->td0[i] : r->tf0[i];
-        hipEvent_t b = kind == RT_TIME_GATHER ? r->tg1[i] : r->td1[i];
+        hipEvent_t a = r->ta[kind][i], b = r->tb[kind][i];
+        ms_out[k] = 0.0f;  // a step that did not run (no gather in DIRECT mode, no copy at deliver none)
+        if (!a || !b) continue;
         HIP_TRY(hipEventSynchronize(b));
         HIP_TRY(hipEventElapsedTime(&ms_out[k], a, b));
     }

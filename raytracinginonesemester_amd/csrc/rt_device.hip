@@ -144,6 +144,22 @@ __device__ unsigned long long g_rt_stats[24];
 // active at traversal start (primary), 14 (shadow), 15 primary traversals with no lane hitting,
 // 16 their pops, 17 primary traversals whose root test no lane passes
 
+#ifdef RT_WAVE_TIMES  // instrumented variant builds only: per-wave start / end (wall clock, 100 MHz),
+// per-wave phase ends (primary traversal, whole sample) and per tile the number of cut boxes
+// its rays may meet (tile_cut_kernel)
+__device__ unsigned long long* g_wave_times;
+__device__ unsigned long long* g_wave_phase;
+__device__ int* g_cut_counts;
+#define RT_PHASE(P, x, y, k)                                                                           \
+    do {                                                                                               \
+        if (g_wave_phase && lane_id() == 0)                                                            \
+            g_wave_phase[(((size_t)((y) / (P).tile_h) * (P).tiles_x + (x) / (P).tile_w) * 4 + threadIdx.x / 64) * 2 + (k)] = \
+                wall_clock64();                                                                        \
+    } while (0)
+#else
+#define RT_PHASE(P, x, y, k) do { } while (0)
+#endif
+
 // ---- node accessors ---------------------------------------------------------------------
 // Scene arrays are immutable while a frame renders: read them through the constant address
 // space, so wave-uniform node addresses become scalar loads even inside loops that also
@@ -455,6 +471,11 @@ __device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, b
 }
 
 // Full hit record of the winning leaf (intersectTriangle's tail, query.h:110-130).
+// Triangle index of a leaf (the primary-hit AOV).
+__device__ __forceinline__ int32_t leaf_tri(const SceneView& sc, int32_t slot) {
+    return __float_as_int(sc.leaf[4 * (size_t)slot].w);
+}
+
 struct SurfHit {
     f3 p, n;
     int32_t tri;
@@ -520,14 +541,9 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid, const 
     f3 radiance = mk(0.f, 0.f, 0.f);
     if (valid && !hit) radiance = add(radiance, mul(mk(1.f, 1.f, 1.f), P.miss));
     if (ballot(hit) == 0) return clamp01(radiance);
-    SurfHit sh;
-    sh.tri = -1;
-    if (hit) sh = resolve_hit(sc, ray, hs.slot);
-    f3 N = mk(0.f, 0.f, 1.f), V = N, Lo = mk(0.f, 0.f, 0.f);
+    f3 Lo = mk(0.f, 0.f, 0.f);
     if (hit) {
-        const DevMaterial m = material_of(sc, sh.tri);
-        N = unit(sh.n);
-        V = unit(sub(ray.o, sh.p));
+        const DevMaterial m = material_of(sc, leaf_tri(sc, hs.slot));
         Lo = add(Lo, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 0.05f));
         Lo = add(Lo, mk(m.emission[0], m.emission[1], m.emission[2]));
     }
@@ -541,11 +557,15 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid, const 
         // results are never read), and copying the camera ray in would keep it live.
         RayPre sray;
         if (hit) {
+            // The hit record (point, normals, material) is rebuilt per light from the leaf and
+            // the camera ray (the accepting test's own t/u/v), so none of it stays live across the
+            // shadow traversal (it was spilled there: ~100 B of scratch per lane).
+            const SurfHit sh = resolve_hit(sc, ray, hs.slot);
+            const f3 N = unit(sh.n);
+            const f3 V = unit(sub(ray.o, sh.p));
             const f3 L = unit(sub(lpos, sh.p));
             const float NdotL = fmaxf(dot(N, L), 0.0f);
             if (NdotL > 0.0f) {
-                // The light's term, added below if the shadow ray is clear (the material is
-                // re-read per light so it is not live across the traversal).
                 const DevMaterial m = material_of(sc, sh.tri);
                 const f3 f = eval_brdf(m, sh.n, V, L);
                 const f3 rad = scale(mk(lt.color[0], lt.color[1], lt.color[2]), (float)lt.intensity);
@@ -572,10 +592,6 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid, const 
     return clamp01(radiance);
 }
 
-// Triangle index of a leaf (the primary-hit AOV).
-__device__ __forceinline__ int32_t leaf_tri(const SceneView& sc, int32_t slot) {
-    return __float_as_int(sc.leaf[4 * (size_t)slot].w);
-}
 
 // One camera sample through TraceRayIterative (query.h:156-220) + ShadeDirect (shader.h).
 // All lanes of a wave call it; `valid` marks lanes owning a sample.  D1: max_depth == 1 (no
@@ -589,6 +605,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
     if constexpr (D1) {
         HitState hs;
         traverse<MODE>(sc, ray, valid, false, 0.0f, hs);
+        RT_PHASE(P, x, y, 0);
 #ifdef RT_STATS
         if constexpr (MODE != RT_KERNEL_LANE) {
             if (ballot(valid) != 0 && ballot(valid && hs.slot >= 0) == 0) {
@@ -1030,6 +1047,12 @@ __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
             const int xb = min(xa + P.tile_w, P.W) - 1, rb = min(ra + P.tile_h, P.rows) - 1;
             const TileDirsF T = tile_dirs_f(P, xa, xb, global_row(P, ra), global_row(P, rb));
             const bool hit = (int)lane < P.sc.ncut && !tile_misses_box_f(T, box);
+#ifdef RT_WAVE_TIMES
+            {
+                const uint64_t hm = ballot(hit);
+                if (g_cut_counts && lane == 0) g_cut_counts[tile] = __popcll(hm);
+            }
+#endif
             if (ballot(hit) == 0) {
                 write_culled_tile(P, tile, (int)lane, 64);
                 culled |= 1ull << j;
@@ -1091,11 +1114,21 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
         if (s == 0) kpix[t >> P.spp_log2] = pix;
         const int64_t aov = valid && P.hit_idx ? (int64_t)pix * P.spp + s : -1;
         const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, aov);
+        RT_PHASE(P, x, r, 1);
         col[3 * t] = c.x;
         col[3 * t + 1] = c.y;
         col[3 * t + 2] = c.z;
     }
-    __syncthreads();
+    if (P.spp <= 64) {
+        // A pixel's samples are consecutive lanes of one wave: only this wave's LDS writes are
+        // read below, so the wave synchronises alone (its siblings in the block may still be
+        // tracing; a block barrier here cost 13 % of the waves' time on c3).
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
     if ((t & (P.spp - 1)) == 0) {
         const int pix = kpix[t >> P.spp_log2];
         if (pix >= 0) {
@@ -1172,6 +1205,9 @@ template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES>
 __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
     __shared__ int kpix[SAMPLES ? BLOCK : 1];
+#ifdef RT_WAVE_TIMES
+    const unsigned long long wt0 = wall_clock64();
+#endif
     const int b = (int)blockIdx.x;
     if (b >= P.tiles_virtual) return;
     const int q = P.nqueues == 1 ? 0 : (b & 7);
@@ -1181,6 +1217,13 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
     if (P.sc.ncut > 0 && P.cut_flag[(size_t)q * P.queue_cap + i]) return;  // culled by tile_cut_kernel
     if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col, kpix);
     else pixels_tile<MODE, D1>(P, tile);
+#ifdef RT_WAVE_TIMES
+    if (g_wave_times && lane_id() == 0) {
+        const size_t k = ((size_t)tile * (BLOCK / 64) + threadIdx.x / 64) * 2;
+        g_wave_times[k] = wt0;
+        g_wave_times[k + 1] = wall_clock64();
+    }
+#endif
 }
 
 // ---- HW1 brute force (HW1/src/render.cpp:72-116) ----------------------------------------
@@ -2272,6 +2315,18 @@ extern "C" int rt_debug_stats(unsigned long long* out, int reset) {
         unsigned long long z[24] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rt_stats), z, sizeof(z)));
     }
+    return RT_OK;
+}
+#endif
+
+#ifdef RT_WAVE_TIMES
+extern "C" int rt_debug_wave_phase_set(void* dev_ptr) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wave_phase), &dev_ptr, sizeof(dev_ptr)));
+    return RT_OK;
+}
+extern "C" int rt_debug_wave_times_set(void* dev_ptr, void* cut_counts_ptr) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wave_times), &dev_ptr, sizeof(dev_ptr)));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_cut_counts), &cut_counts_ptr, sizeof(cut_counts_ptr)));
     return RT_OK;
 }
 #endif

@@ -63,7 +63,8 @@ void hexv(FILE* f, const char* name, const Vec3& v) {
 int usage() {
     std::fprintf(stderr,
         "usage: ref_g jitter <spp> <seed>\n"
-        "       ref_g scene <scene.json> <project_dir> <outdir> [W H spp max_depth diffuse(0/1|-1) hits(0/1)]\n");
+        "       ref_g scene <scene.json> <project_dir> <outdir> [W H spp max_depth diffuse(0/1|-1) hits(0/1)]\n"
+        "       ref_g arrays <indir> <outdir> W H spp max_depth diffuse(0/1)\n");
     return 2;
 }
 
@@ -246,11 +247,91 @@ int cmd_scene(int argc, char** argv) {
     return ok ? 0 : 1;
 }
 
+template <class T>
+bool read_bin(const std::string& path, std::vector<T>& out) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    out.resize(size_t(n) / sizeof(T));
+    const size_t r = out.empty() ? 0 : std::fread(out.data(), sizeof(T), out.size(), f);
+    std::fclose(f);
+    return r == out.size() && size_t(n) % sizeof(T) == 0;
+}
+
+// Caller-supplied scene arrays (any tree, e.g. one deeper than SearchBVH's 512-entry stack)
+// straight into the reference render() and SearchBVH (G/include/query.cu:79-167,
+// G/include/query.h:224-311): <indir>/{nodes,aabbs,tris,triobj,mats,lights}.bin in the
+// reference layouts and <indir>/camera.txt = "pos(3) look_at(3) up(3) focal_mm sensor_mm" (%a).
+int cmd_arrays(int argc, char** argv) {
+    if (argc < 9) return usage();
+    const std::string indir = argv[2], outdir = argv[3];
+    const int W = std::atoi(argv[4]), H = std::atoi(argv[5]), spp = std::atoi(argv[6]);
+    const int max_depth = std::atoi(argv[7]);
+    const bool diffuse_bounce = std::atoi(argv[8]) != 0;
+    std::vector<BVHNode> nodes;
+    std::vector<AABB> aabbs;
+    std::vector<Triangle> tris;
+    std::vector<int32_t> triobj;
+    std::vector<Material> mats;
+    std::vector<Light> lights;
+    if (!read_bin(indir + "/nodes.bin", nodes) || !read_bin(indir + "/aabbs.bin", aabbs) ||
+        !read_bin(indir + "/tris.bin", tris) || !read_bin(indir + "/triobj.bin", triobj) ||
+        !read_bin(indir + "/mats.bin", mats) || !read_bin(indir + "/lights.bin", lights)) {
+        std::fprintf(stderr, "cannot read the arrays in %s\n", indir.c_str());
+        return 1;
+    }
+    double c[11];
+    FILE* cf = std::fopen((indir + "/camera.txt").c_str(), "r");
+    if (!cf) return 1;
+    for (double& v : c)
+        if (std::fscanf(cf, "%la", &v) != 1) { std::fclose(cf); return 1; }
+    std::fclose(cf);
+    const Camera cam(make_vec3(float(c[0]), float(c[1]), float(c[2])), make_vec3(float(c[3]), float(c[4]), float(c[5])),
+                     make_vec3(float(c[6]), float(c[7]), float(c[8])), c[9], c[10], W, H);
+    const size_t P = tris.size();
+    const Vec3 miss_color = make_vec3(0.0f, 0.0f, 0.0f);
+    std::vector<Vec3> image((size_t)W * H, make_vec3(0, 0, 0));
+    render(P, W, H, cam, miss_color, max_depth, spp, nodes.data(), aabbs.data(), tris.data(), triobj.data(),
+           mats.data(), (int)mats.size(), lights.data(), (int)lights.size(), diffuse_bounce, image.data());
+    const size_t ns = (size_t)W * H * spp;
+    std::vector<int32_t> hit_idx(ns);
+    std::vector<float> hit_t(ns);
+    auto offsets = jittered_samples(spp, 42u);
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x)
+            for (int si = 0; si < spp; ++si) {
+                const Ray ray = cam.get_ray(float(x) + offsets[si].first, float(y) + offsets[si].second);
+                HitRecord rec;
+                SearchBVH((int)P, ray, nodes.data(), aabbs.data(), tris.data(), rec);
+                const size_t k = ((size_t)y * W + x) * spp + si;
+                hit_idx[k] = rec.hit ? rec.triangleIdx : -1;
+                hit_t[k] = rec.hit ? (float)rec.t : -1.0f;
+            }
+    bool ok = write_bin(outdir + "/fb.f32", image.data(), image.size() * sizeof(Vec3));
+    ok &= write_bin(outdir + "/hits.i32", hit_idx.data(), ns * sizeof(int32_t));
+    ok &= write_bin(outdir + "/hitt.f32", hit_t.data(), ns * sizeof(float));
+    FILE* m = std::fopen((outdir + "/meta.json").c_str(), "w");
+    if (!m) return 1;
+    std::fprintf(m, "{\n");
+    std::fprintf(m, "  \"num_triangles\": %zu,\n  \"width\": %d,\n  \"height\": %d,\n", P, W, H);
+    std::fprintf(m, "  \"spp\": %d,\n  \"max_depth\": %d,\n  \"diffuse_bounce\": %d,\n", spp, max_depth, (int)diffuse_bounce);
+    hexv(m, "center", cam.center);
+    hexv(m, "pixel00_loc", cam.pixel00_loc);
+    hexv(m, "pixel_delta_u", cam.pixel_delta_u);
+    hexv(m, "pixel_delta_v", cam.pixel_delta_v);
+    std::fprintf(m, "  \"num_lights\": %zu\n}\n", lights.size());
+    std::fclose(m);
+    return ok ? 0 : 1;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
     if (argc < 2) return usage();
     if (!std::strcmp(argv[1], "jitter")) return cmd_jitter(argc, argv);
     if (!std::strcmp(argv[1], "scene")) return cmd_scene(argc, argv);
+    if (!std::strcmp(argv[1], "arrays")) return cmd_arrays(argc, argv);
     return usage();
 }

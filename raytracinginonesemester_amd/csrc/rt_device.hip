@@ -57,6 +57,12 @@ constexpr int BLOCK = 256;
 // A compile-time choice, so each kernel holds one traversal loop per ray kind.
 constexpr int MODE_WIDE = 16;
 constexpr int MODE_PACKED = 32;  // box tests with packed FMAs (box_ends_pk): the big-scene kernels
+// Trees whose DFS needs more than STACK_CAP entries: SearchBVH literally, per lane, with the
+// reference's 512-entry stack, its overflow rule and brute-force completion (traverse_deep).
+constexpr int MODE_DEEP = 64;
+constexpr int REF_STACK = 512;                // query.h:245
+constexpr uint32_t INV_LEAF = 0xFFFFFFFEu;    // deep stack entry: a leaf naming no triangle (query.h:263)
+constexpr uint32_t BRUTE_BIT = 0x40000000u;   // HitState::slot of a brute-force hit: BRUTE_BIT | triangle
 constexpr float kRayTMin = 1e-4f;             // query.h:233
 constexpr float RT_EPS = 1e-3f;               // shader.h:22
 
@@ -84,6 +90,7 @@ struct SceneView {
     int32_t wide;
     const float* __restrict__ cut;  // tile culling: boxes of a cut of the tree (6 floats each)
     int32_t ncut;
+    const float4* __restrict__ tri;  // deep trees: v0 | e1, e2.x | e2.y, e2.z by triangle index (brute force)
 };
 
 __device__ __forceinline__ f3 scene_bmax(const SceneView& sc) { return mk(sc.bmax[0], sc.bmax[1], sc.bmax[2]); }
@@ -462,17 +469,81 @@ __device__ __forceinline__ void traverse_lane(const SceneView& sc, const RayPre&
     }
 }
 
+// ---- DEEP traversal: SearchBVH (G/include/query.h:224-311) as written, per lane ---------
+// For trees whose DFS may need more than STACK_CAP entries.  A 512-entry private stack; the
+// root is pushed unconditionally (:249); every pop tests the node's own box with the current
+// bestT (:255); a leaf naming no triangle still occupies its stack entry (it was pushed after
+// its box passed, :263); an internal node pushes left then right when the child's box passes,
+// or sets the overflow flag when the stack is full (:277-295); after the loop an overflow is
+// completed by every triangle in index order with t <= bestT (:298-308).  A shadow query stops
+// once bestT < dist (bestT only decreases afterwards, so `hit && t < dist` is decided).
+__device__ void traverse_deep(const SceneView& sc, const RayPre& r, bool active, bool any_hit, float any_hit_dist,
+                              HitState& hs) {
+    hs.bestT = FLT_MAX;
+    hs.slot = -1;
+    if (!active) return;
+    uint32_t st[REF_STACK];
+    int sp = 0;
+    bool overflow = false;
+    st[sp++] = sc.root_ref;
+    while (sp > 0) {
+        const uint32_t ref = st[--sp];
+        if (ref == INV_LEAF) continue;  // its box test decides nothing
+        if (!box_hit(r, own_box(sc, ref, false), kRayTMin, hs.bestT)) continue;
+        if (ref & LEAF_BIT) {
+            const uint32_t slot = ref & ~LEAF_BIT;
+            const float4* L = sc.leaf + 4 * (size_t)slot;
+            const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
+            float t, u, v;
+            if (mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin, hs.bestT, t, u, v)) {
+                hs.bestT = t;
+                hs.slot = (int32_t)slot;
+                if (any_hit && t < any_hit_dist) return;
+            }
+            continue;
+        }
+        const float4* N = sc.inode + 4 * (size_t)ref;
+        const float4 q0 = ldc(N), q1 = ldc(N + 1), q2 = ldc(N + 2);
+        const uint4 q3 = ldc_u(N + 3);  // left ref, right ref, invalid-leaf flags (bit 0 left, bit 1 right)
+        if ((q3.x != NO_REF || (q3.z & 1u)) && box_hit(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, kRayTMin, hs.bestT)) {
+            if (sp < REF_STACK) st[sp++] = (q3.z & 1u) ? INV_LEAF : q3.x;
+            else overflow = true;
+        }
+        if ((q3.y != NO_REF || (q3.z & 2u)) && box_hit(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, kRayTMin, hs.bestT)) {
+            if (sp < REF_STACK) st[sp++] = (q3.z & 2u) ? INV_LEAF : q3.y;
+            else overflow = true;
+        }
+    }
+    if (overflow) {
+        for (int i = 0; i < sc.num_tris; ++i) {
+            const float4* T = sc.tri + 3 * (size_t)i;
+            const float4 a = ldc(T), b = ldc(T + 1), c = ldc(T + 2);
+            float t, u, v;
+            if (mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin, hs.bestT, t, u, v)) {
+                hs.bestT = t;
+                hs.slot = (int32_t)(BRUTE_BIT | (uint32_t)i);
+                if (any_hit && t < any_hit_dist) return;
+            }
+        }
+    }
+}
+
 // any_hit (wave-uniform): shadow query, stop a lane once bestT < any_hit_dist.
 template <int MODE>
 __device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, bool active, bool any_hit,
                                          float any_hit_dist, HitState& hs) {
-    if constexpr (MODE == RT_KERNEL_LANE) traverse_lane(sc, r, active, any_hit, any_hit_dist, hs);
+    if constexpr ((MODE & MODE_DEEP) != 0) traverse_deep(sc, r, active, any_hit, any_hit_dist, hs);
+    else if constexpr (MODE == RT_KERNEL_LANE) traverse_lane(sc, r, active, any_hit, any_hit_dist, hs);
     else traverse_wave_impl<(MODE & MODE_WIDE) != 0, (MODE & MODE_PACKED) != 0>(sc, r, active, any_hit, any_hit_dist, hs);
 }
 
-// Full hit record of the winning leaf (intersectTriangle's tail, query.h:110-130).
-// Triangle index of a leaf (the primary-hit AOV).
+// Triangle index of a hit (the primary-hit AOV): the leaf's, or (DEEP kernels) the triangle a
+// brute-force completion accepted.
+template <bool DEEP = false>
 __device__ __forceinline__ int32_t leaf_tri(const SceneView& sc, int32_t slot) {
+    if constexpr (DEEP) {
+        if ((uint32_t)slot & BRUTE_BIT) return (int32_t)((uint32_t)slot & ~BRUTE_BIT);
+    }
     return __float_as_int(sc.leaf[4 * (size_t)slot].w);
 }
 
@@ -481,14 +552,21 @@ struct SurfHit {
     int32_t tri;
 };
 
+// Full hit record of the winning triangle (intersectTriangle's tail, query.h:110-130).
+template <bool DEEP = false>
 __device__ __forceinline__ SurfHit resolve_hit(const SceneView& sc, const RayPre& r, int32_t slot) {
     const float4* L = sc.leaf + 4 * (size_t)slot;
+    bool brute = false;
+    if constexpr (DEEP) {
+        brute = ((uint32_t)slot & BRUTE_BIT) != 0;
+        if (brute) L = sc.tri + 3 * (size_t)((uint32_t)slot & ~BRUTE_BIT);
+    }
     const float4 a = L[0], b = L[1], c = L[2];
     const f3 v0 = mk(a.x, a.y, a.z), e1 = mk(b.x, b.y, b.z), e2 = mk(b.w, c.x, c.y);
     float t = 0.f, u = 0.f, v = 0.f;
     mt_g(r, v0, e1, e2, -FLT_MAX, FLT_MAX, t, u, v);  // same t/u/v as the accepting test
     SurfHit s;
-    s.tri = __float_as_int(a.w);
+    s.tri = brute ? (int32_t)((uint32_t)slot & ~BRUTE_BIT) : __float_as_int(a.w);
     const float4* Nn = sc.tnorm + 3 * (size_t)s.tri;
     const float4 n0 = Nn[0], n1 = Nn[1], n2 = Nn[2];
     hit_frame(r, e1, e2, mk(n0.x, n0.y, n0.z), mk(n1.x, n1.y, n1.z), mk(n2.x, n2.y, n2.z), t, u, v, s.p, s.n);
@@ -543,7 +621,7 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid, const 
     if (ballot(hit) == 0) return clamp01(radiance);
     f3 Lo = mk(0.f, 0.f, 0.f);
     if (hit) {
-        const DevMaterial m = material_of(sc, leaf_tri(sc, hs.slot));
+        const DevMaterial m = material_of(sc, leaf_tri<(MODE & MODE_DEEP) != 0>(sc, hs.slot));
         Lo = add(Lo, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 0.05f));
         Lo = add(Lo, mk(m.emission[0], m.emission[1], m.emission[2]));
     }
@@ -560,7 +638,7 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid, const 
             // The hit record (point, normals, material) is rebuilt per light from the leaf and
             // the camera ray (the accepting test's own t/u/v), so none of it stays live across the
             // shadow traversal (it was spilled there: ~100 B of scratch per lane).
-            const SurfHit sh = resolve_hit(sc, ray, hs.slot);
+            const SurfHit sh = resolve_hit<(MODE & MODE_DEEP) != 0>(sc, ray, hs.slot);
             const f3 N = unit(sh.n);
             const f3 V = unit(sub(ray.o, sh.p));
             const f3 L = unit(sub(lpos, sh.p));
@@ -607,7 +685,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
         traverse<MODE>(sc, ray, valid, false, 0.0f, hs);
         RT_PHASE(P, x, y, 0);
 #ifdef RT_STATS
-        if constexpr (MODE != RT_KERNEL_LANE) {
+        if constexpr (MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0) {
             if (ballot(valid) != 0 && ballot(valid && hs.slot >= 0) == 0) {
                 RT_STAT(15, 1);
                 RT_STAT(16, hs.pops);
@@ -616,7 +694,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
 #endif
         if (valid) {
             if (aov >= 0) {
-                P.hit_idx[aov] = hs.slot >= 0 ? leaf_tri(sc, hs.slot) : -1;
+                P.hit_idx[aov] = hs.slot >= 0 ? leaf_tri<(MODE & MODE_DEEP) != 0>(sc, hs.slot) : -1;
                 P.hit_t[aov] = hs.slot >= 0 ? hs.bestT : -1.0f;
             }
         }
@@ -638,7 +716,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
         const bool hit = alive && hs.slot >= 0;
         SurfHit sh;
         sh.tri = -1;
-        if (hit) sh = resolve_hit(sc, ray, hs.slot);
+        if (hit) sh = resolve_hit<(MODE & MODE_DEEP) != 0>(sc, ray, hs.slot);
         if (depth == 0 && valid) {
             if (aov >= 0) {
                 P.hit_idx[aov] = hit ? sh.tri : -1;
@@ -1681,6 +1759,8 @@ struct rt_scene {
     DevBuf inode, wnode, ibox, leaf, tnorm, objids, mats, lights, jitter;
     DevBuf cut;  // tile culling: boxes of a cut of the tree (6 floats each)
     int ncut = 0;
+    bool deep = false;  // the DFS may need more than STACK_CAP entries: MODE_DEEP kernels
+    DevBuf tri;         // deep: triangles by index (brute-force completion)
     bool wide = false;
     DevBuf work;  // live tile list counters + the lists
     int64_t last_tiles_total = 0;
@@ -1726,8 +1806,9 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     if (nmat < 0 || nlights < 0 || (nmat > 0 && !mats) || (nlights > 0 && !lights))
         return set_error(RT_ERR_ARG, "rt_scene_create: bad material/light arrays");
     const size_t NN = 2 * P - 1;
-    // Classify nodes, give internal/leaf nodes compact ids, and check the reachable graph
-    // is a finite tree whose DFS fits the 64-entry wave stack (SearchBVH's push/pop order).
+    // Classify nodes, give internal/leaf nodes compact ids, and check the reachable graph is
+    // a finite tree; a tree whose DFS may need more than the 64-entry wave stack (SearchBVH's
+    // push/pop order) is rendered by the MODE_DEEP kernels (the reference's 512-entry stack).
     std::vector<uint32_t> cid(NN, NO_REF);
     size_t n_int = 0, n_leaf = 0;
     for (size_t n = 0; n < NN; ++n) {
@@ -1766,7 +1847,7 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
                o.min_corner.z <= i.min_corner.z && o.max_corner.x >= i.max_corner.x &&
                o.max_corner.y >= i.max_corner.y && o.max_corner.z >= i.max_corner.z;
     };
-    bool wide_ok = true;
+    bool wide_ok = true, deep = false;
     {
         std::vector<uint8_t> state(NN, 0);  // 0 new, 1 on path, 2 done
         std::vector<int> S(NN, 0), SW(NN, 0);
@@ -1809,9 +1890,8 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
                 }
             }
         }
-        if (std::max(1, S[0]) > STACK_CAP)
-            return set_error(RT_ERR_UNSUPPORTED, "BVH needs a DFS stack deeper than 64 entries");
-        if (std::max(1, SW[0]) > STACK_CAP) wide_ok = false;
+        deep = std::max(1, S[0]) > STACK_CAP;
+        if (deep || std::max(1, SW[0]) > STACK_CAP) wide_ok = false;
     }
     std::vector<float4> hin(4 * std::max<size_t>(n_int, 1)), hib(2 * std::max<size_t>(n_int, 1));
     std::vector<float4> hwn(wide_ok ? 8 * std::max<size_t>(n_int, 1) : 0);
@@ -1828,7 +1908,11 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
             q[0] = make_float4(lb.min_corner.x, lb.max_corner.x, lb.min_corner.y, lb.max_corner.y);
             q[1] = make_float4(lb.min_corner.z, lb.max_corner.z, rb.min_corner.x, rb.max_corner.x);
             q[2] = make_float4(rb.min_corner.y, rb.max_corner.y, rb.min_corner.z, rb.max_corner.z);
-            uint32_t refs[4] = {ref_of(nd.left_idx), ref_of(nd.right_idx), 0u, 0u};
+            // z: children that are leaves naming no triangle (pushed by SearchBVH all the same:
+            // the deep kernels keep their stack entries)
+            const uint32_t inv = (nd.left_idx != NO_REF && ref_of(nd.left_idx) == NO_REF ? 1u : 0u) |
+                                 (nd.right_idx != NO_REF && ref_of(nd.right_idx) == NO_REF ? 2u : 0u);
+            uint32_t refs[4] = {ref_of(nd.left_idx), ref_of(nd.right_idx), inv, 0u};
             std::memcpy(&q[3], refs, 16);
             const rt_aabb& ob = aabbs[n];
             hib[2 * c] = make_float4(ob.min_corner.x, ob.max_corner.x, ob.min_corner.y, ob.max_corner.y);
@@ -1945,6 +2029,17 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     if ((rc = s->inode.upload(hin.data(), hin.size() * sizeof(float4))) != RT_OK) return rc;
     if (wide_ok && (rc = s->wnode.upload(hwn.data(), hwn.size() * sizeof(float4))) != RT_OK) return rc;
     s->wide = wide_ok && !(s->root_ref & LEAF_BIT);
+    s->deep = deep;
+    if (deep) {  // v0 | e1, e2.x | e2.y, e2.z by triangle index, e1/e2 as intersectTriangle computes them
+        std::vector<float4> ht(3 * P);
+        for (size_t t = 0; t < P; ++t) {
+            const rt_triangle& tr = tris[t];
+            ht[3 * t] = make_float4(tr.v0.x, tr.v0.y, tr.v0.z, 0.f);
+            ht[3 * t + 1] = make_float4(tr.v1.x - tr.v0.x, tr.v1.y - tr.v0.y, tr.v1.z - tr.v0.z, tr.v2.x - tr.v0.x);
+            ht[3 * t + 2] = make_float4(tr.v2.y - tr.v0.y, tr.v2.z - tr.v0.z, 0.f, 0.f);
+        }
+        if ((rc = s->tri.upload(ht.data(), ht.size() * sizeof(float4))) != RT_OK) return rc;
+    }
     if ((rc = s->ibox.upload(hib.data(), hib.size() * sizeof(float4))) != RT_OK) return rc;
     if ((rc = s->leaf.upload(hlf.data(), hlf.size() * sizeof(float4))) != RT_OK) return rc;
     if ((rc = s->tnorm.upload(hnm.data(), hnm.size() * sizeof(float4))) != RT_OK) return rc;
@@ -1978,6 +2073,7 @@ extern "C" int rt_scene_clone(const rt_scene* src, int device, rt_scene** out) {
     std::memcpy(s->bmax, src->bmax, sizeof(s->bmax));
     s->ncut = src->ncut;
     s->wide = src->wide;
+    s->deep = src->deep;
     s->cus = src->cus;
     s->bytes = src->bytes;
     // device-to-device copies of the packed arrays (over xGMI when the devices differ)
@@ -1985,7 +2081,7 @@ extern "C" int rt_scene_clone(const rt_scene* src, int device, rt_scene** out) {
                                                       {&s->ibox, &src->ibox},   {&s->leaf, &src->leaf},
                                                       {&s->tnorm, &src->tnorm}, {&s->objids, &src->objids},
                                                       {&s->mats, &src->mats},   {&s->lights, &src->lights},
-                                                      {&s->cut, &src->cut}};
+                                                      {&s->cut, &src->cut},     {&s->tri, &src->tri}};
     for (const auto& [d, q] : bufs) {
         if ((rc = d->alloc(q->n)) != RT_OK) return rc;
         if (q->n) HIP_TRY(hipMemcpyPeer(d->p, device, q->p, src->device, q->n));
@@ -2053,7 +2149,7 @@ template <int MODE, bool SAMPLES>
 void launch_mode(const RenderParams& P, bool big, hipStream_t st) {
     const dim3 grid((P.tiles_virtual + 7) / 8 * 8);
     if (P.max_depth == 1) {
-        if constexpr (SAMPLES && MODE != RT_KERNEL_LANE) {
+        if constexpr (SAMPLES && MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0) {
             if (big) {  // more waves and packed box tests (c5 faster with each; both slower on c3)
                 hipLaunchKernelGGL((render_tiles_kernel<MODE | MODE_PACKED, SAMPLES, true, RT_BIG_WAVES>), grid,
                                    dim3(BLOCK), 0, st, P);
@@ -2162,6 +2258,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.sc.root_ref = s->root_ref;
     std::memcpy(P.sc.root_box, s->root_box, sizeof(P.sc.root_box));
     P.sc.cut = static_cast<const float*>(s->cut.p);
+    P.sc.tri = static_cast<const float4*>(s->tri.p);
     double max_cov = 0.3;  // RT_CULL_COVERAGE: tests force the cut pass on (>= 1: always, untested candidates none)
     if (const char* e = std::getenv("RT_CULL_COVERAGE")) max_cov = std::atof(e);
     P.sc.ncut = s->ncut > 0 && root_box_coverage(s->root_box, cam) <= max_cov ? s->ncut : 0;
@@ -2251,7 +2348,8 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         }
         HIP_TRY(hipEventRecord(s->evm[slot], st));
         const bool big = big_scene_waves(s);
-        if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, big, st);
+        if (s->deep) launch<MODE_DEEP>(P, samples, false, st);
+        else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, big, st);
         else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, big, st);
         else launch<RT_KERNEL_WAVE>(P, samples, big, st);
         HIP_TRY(hipGetLastError());

@@ -140,6 +140,29 @@ def gen_hw1(name: str) -> None:
         (dst / "meta.json").write_text(json.dumps(meta, indent=1) + "\n")
 
 
+def gen_chain(name: str) -> None:
+    """Caterpillar BVHs deeper than 64 / 512 DFS entries (tests/golden/chain_bvh.py) through the
+    reference render() and SearchBVH (ref_g arrays)."""
+    sys.path.insert(0, str(HERE))
+    import chain_bvh
+
+    P, W, H, spp, depth = chain_bvh.FIXTURES[name]
+    dst = HERE / "scenes" / name
+    dst.mkdir(parents=True, exist_ok=True)
+    with tempfile.TemporaryDirectory() as td:
+        t = Path(td)
+        chain_bvh.write_arrays(chain_bvh.chain_scene(P), t)
+        run([REF / "ref_g", "arrays", t, t, W, H, spp, depth, 1])
+        meta = json.loads((t / "meta.json").read_text())
+        meta["generator"] = "tests/golden/chain_bvh.py chain_scene(%d)" % P
+        meta["sha256"] = {k: sha256(t / k) for k in
+                          ("nodes.bin", "aabbs.bin", "tris.bin", "triobj.bin", "mats.bin", "lights.bin",
+                           "fb.f32", "hits.i32", "hitt.f32")}
+        for k in ("fb.f32", "hits.i32", "hitt.f32"):
+            gz(t / k, dst / (k + ".gz"))
+        (dst / "meta.json").write_text(json.dumps(meta, indent=1) + "\n")
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", nargs="*")
@@ -147,6 +170,12 @@ def main() -> None:
     if not (REF / "ref_g").exists():
         sys.exit("build the reference drivers first: make -C oracle ref")
     want = set(a.only) if a.only else None
+    sys.path.insert(0, str(HERE))
+    import chain_bvh
+
+    for n in chain_bvh.FIXTURES:
+        if not want or n in want:
+            gen_chain(n)
     if not want or "jitter" in want:
         gen_jitter()
     if not want or "kat" in want:

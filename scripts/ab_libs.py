@@ -41,6 +41,7 @@ for spec in a.libs:
     h = _lib.lib()
     builds.append((name, h, rt.DeviceScene.from_host(hs)))
 times = {n: [] for n, _, _ in builds}
+ftimes = {n: [] for n, _, _ in builds}
 ref = None
 for r in range(a.rounds):
     for name, h, ds in builds:
@@ -48,6 +49,7 @@ for r in range(a.rounds):
         for _ in range(a.reps):
             img = ds.render(cam, spp=cfg["spp"], max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"])
         times[name] += list(ds.kernel_times(a.reps))
+        ftimes[name] += list(ds.frame_times(a.reps))
         if ref is None:
             ref = img
         if not a.no_check:
@@ -57,4 +59,5 @@ for name, _, _ in builds:
     t = np.array(times[name])
     print(json.dumps({"config": a.config, "build": name, "median_ms": round(float(np.median(t)), 4),
                       "min_ms": round(float(t.min()), 4),
+                      "frame_median_ms": round(float(np.median(ftimes[name])), 4),
                       "Gsamples_s": round(float(samples / np.median(t) / 1e6), 3)}), flush=True)

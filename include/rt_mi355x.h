@@ -225,7 +225,10 @@ int rt_shard_rows(int height, int band_rows, int band_index, int band_count);
  * host sync.  rgb_dev: rows*W*3 floats.  hit_idx_dev / hit_t_dev (optional, rows*W*spp):
  * primary-ray triangle index (-1 = miss) and t per (pixel, sample).
  * Frames of one scene are ordered: a call on another stream than the scene's previous frame
- * makes its stream wait for that frame first (the scene's tile lists are reused per frame). */
+ * makes its stream wait for that frame first.  A frame's tile pre-passes (which write the culled
+ * tiles' pixels) run on the scene's own stream, overlapping the previous frame's render kernel
+ * unless the two frames' output buffers overlap; hip_stream waits for them before the render
+ * kernel, so the frame is complete when hip_stream reaches the end of this call's work. */
 int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt,
                      float* rgb_dev, int32_t* hit_idx_dev, float* hit_t_dev, void* hip_stream);
 

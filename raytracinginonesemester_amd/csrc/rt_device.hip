@@ -1062,9 +1062,9 @@ __device__ __forceinline__ void append_live(const RenderParams& P, bool live, in
 // Pass 1, one lane per tile: the root test; the survivors go to the live lists.
 __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
     const int tile = (int)(blockIdx.x * BLOCK + threadIdx.x);
-    // Counters are double-buffered across frames (no reset launch): this frame's set was zeroed
-    // by the previous frame's pass; zero the other one for the next frame (the previous frame,
-    // its last user, finished before this kernel started: same stream).
+    // Counter sets rotate over three frames (no reset launch): this frame's set was zeroed by
+    // the previous frame's pass; zero the next frame's (its last user, frame k-2, has finished:
+    // the scene's prep stream waited for it).
     if (blockIdx.x == 0 && threadIdx.x < 9) P.next_count[threadIdx.x * COUNTER_STRIDE] = 0u;
     bool live = false;
     if (tile < P.tiles_total) {
@@ -1762,29 +1762,53 @@ struct rt_scene {
     bool deep = false;  // the DFS may need more than STACK_CAP entries: MODE_DEEP kernels
     DevBuf tri;         // deep: triangles by index (brute-force completion)
     bool wide = false;
-    DevBuf work;  // live tile list counters + the lists
+    DevBuf work;  // kSets x (counter set | live lists | cut flags)
     int64_t last_tiles_total = 0;
     int cus = 256;
     int jitter_spp = -1;
     std::vector<float> jitter_host;
-    // Ring of HIP event pairs around each render kernel, recorded on the launch stream.
+    // Ring of HIP events per frame.  A frame's pre-passes (tile_cull_kernel, tile_cut_kernel)
+    // run on the scene's own high-priority `prep` stream, its render kernel on the caller's:
+    //   prep:   [wait ev1 of frame k-2 (k-1 too if the outputs overlap)] ev0 | cull | cut | pdone
+    //   caller: [wait pdone] evm | render kernel | ev1
+    // so frame k's pre-passes overlap frame k-1's render kernel (its tail leaves CUs idle).
     static constexpr int kRing = 256;
-    // ev0 | tile_cull_kernel (+ tile_cut_kernel) | evm | render kernel | ev1
-    hipEvent_t ev0[kRing] = {}, evm[kRing] = {}, ev1[kRing] = {};
+    hipEvent_t ev0[kRing] = {}, evm[kRing] = {}, ev1[kRing] = {}, pdone[kRing] = {};
+    hipStream_t prep = nullptr;
     uint64_t launches = 0;
     size_t bytes = 0;
-    // The work buffers (live lists, counters) are per scene, so frames of one scene must run in
-    // order: a frame launched on another stream than the previous one first waits for that
-    // frame's last event.  A frame whose launches failed part-way leaves the counter sets in an
-    // unknown state: the next frame zeroes both.
+    // Work buffers rotate over kSets per frame (frame k: set k % 3; its cull pass zeroes the
+    // counters of set k+1, last used by frame k-2).  A frame launched on another stream than
+    // the previous one first waits for that frame.  A frame whose launches failed part-way
+    // leaves the counter sets unknown: the next frame zeroes them all.
+    static constexpr int kSets = 3;
     hipStream_t last_stream = nullptr;
     bool counters_dirty = false;
+    // the previous frame's output ranges (device byte ranges): overlapping outputs serialise
+    struct Range { uintptr_t lo = 0, hi = 0; };
+    Range prev_out[4];
+    size_t set_bytes = 0;  // bytes of one set of lists for the current geometry
     ~rt_scene() {
+        if (prep) (void)hipStreamSynchronize(prep);
         for (int i = 0; i < kRing; ++i) {
             if (ev0[i]) (void)hipEventDestroy(ev0[i]);
             if (evm[i]) (void)hipEventDestroy(evm[i]);
             if (ev1[i]) (void)hipEventDestroy(ev1[i]);
+            if (pdone[i]) (void)hipEventDestroy(pdone[i]);
         }
+        if (prep) (void)hipStreamDestroy(prep);
+    }
+    int create_sync() {  // streams and events (rt_scene_create / rt_scene_clone)
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&prep, hipStreamNonBlocking, hi));
+        for (int i = 0; i < kRing; ++i) {
+            HIP_TRY(hipEventCreate(&ev0[i]));
+            HIP_TRY(hipEventCreate(&evm[i]));
+            HIP_TRY(hipEventCreate(&ev1[i]));
+            HIP_TRY(hipEventCreateWithFlags(&pdone[i], hipEventDisableTiming));
+        }
+        return RT_OK;
     }
 };
 
@@ -2046,11 +2070,7 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     if (objids && (rc = s->objids.upload(objids, P * sizeof(int32_t))) != RT_OK) return rc;
     if (nmat > 0 && (rc = s->mats.upload(mats, size_t(nmat) * sizeof(rt_material))) != RT_OK) return rc;
     if (nlights > 0 && (rc = s->lights.upload(lights, size_t(nlights) * sizeof(rt_light))) != RT_OK) return rc;
-    for (int i = 0; i < rt_scene::kRing; ++i) {
-        HIP_TRY(hipEventCreate(&s->ev0[i]));
-        HIP_TRY(hipEventCreate(&s->evm[i]));
-        HIP_TRY(hipEventCreate(&s->ev1[i]));
-    }
+    if ((rc = s->create_sync()) != RT_OK) return rc;
     s->bytes = s->inode.n + s->wnode.n + s->ibox.n + s->leaf.n + s->tnorm.n + s->objids.n + s->mats.n + s->lights.n;
     *out = s.release();
     return RT_OK;
@@ -2086,11 +2106,7 @@ extern "C" int rt_scene_clone(const rt_scene* src, int device, rt_scene** out) {
         if ((rc = d->alloc(q->n)) != RT_OK) return rc;
         if (q->n) HIP_TRY(hipMemcpyPeer(d->p, device, q->p, src->device, q->n));
     }
-    for (int i = 0; i < rt_scene::kRing; ++i) {
-        HIP_TRY(hipEventCreate(&s->ev0[i]));
-        HIP_TRY(hipEventCreate(&s->evm[i]));
-        HIP_TRY(hipEventCreate(&s->ev1[i]));
-    }
+    if ((rc = s->create_sync()) != RT_OK) return rc;
     *out = s.release();
     return RT_OK;
 }
@@ -2310,42 +2326,72 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.nqueues = P.tile_order == RT_TILES_LINEAR ? 1 : 8;
     P.queue_cap = P.tiles_total;
     P.tiles_virtual = P.nqueues == 1 ? P.tiles_total : 8 * P.tiles_x * ((tiles_y + 7) / 8);
-    // two counter sets (8 live lists + candidates each), alternating by frame
+    // kSets counter sets (8 live lists + one spare each) at fixed offsets, then kSets x (live
+    // lists | cut flags) sized for this geometry; rotating by frame
     constexpr size_t kCounterBytes = 9 * COUNTER_STRIDE * sizeof(uint32_t);
     const size_t list_bytes = size_t(P.nqueues) * size_t(P.queue_cap) * sizeof(int32_t);
-    const size_t work_bytes = 2 * kCounterBytes + list_bytes + size_t(P.nqueues) * size_t(P.queue_cap);
+    const size_t flag_bytes = (size_t(P.nqueues) * size_t(P.queue_cap) + 255) / 256 * 256;
+    const size_t set_bytes = list_bytes + flag_bytes;
+    const size_t work_bytes = rt_scene::kSets * (kCounterBytes + set_bytes);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (s->launches > 0 && st != s->last_stream)  // the previous frame of this scene ran elsewhere
-        HIP_TRY(hipStreamWaitEvent(st, s->ev1[(s->launches - 1) % rt_scene::kRing], 0));
+    const uint64_t k = s->launches;
+    auto ev1_of = [&](uint64_t f) { return s->ev1[f % rt_scene::kRing]; };
+    if (k > 0 && st != s->last_stream)  // the previous frame of this scene ran elsewhere
+        HIP_TRY(hipStreamWaitEvent(st, ev1_of(k - 1), 0));
     s->last_stream = st;
     if (s->work.n < work_bytes) {
-        if (s->launches > 0) HIP_TRY(hipStreamSynchronize(st));  // the old buffer may still be read
+        if (k > 0) {  // the old buffers may still be read
+            HIP_TRY(hipStreamSynchronize(s->prep));
+            HIP_TRY(hipEventSynchronize(ev1_of(k - 1)));
+        }
         if ((rc = s->work.alloc(work_bytes)) != RT_OK) return rc;
         s->counters_dirty = true;
     }
-    if (s->counters_dirty) {
-        HIP_TRY(hipMemsetAsync(s->work.p, 0, 2 * kCounterBytes, st));
-        s->counters_dirty = false;
-    }
-    const int set = int(s->launches & 1);
-    P.live_count = reinterpret_cast<uint32_t*>(static_cast<char*>(s->work.p) + set * kCounterBytes);
-    P.next_count = reinterpret_cast<uint32_t*>(static_cast<char*>(s->work.p) + (1 - set) * kCounterBytes);
+    // This frame's outputs against the previous frame's: overlapping ranges (a caller reusing
+    // one buffer) make the pre-passes, which write the culled tiles' pixels, wait for the
+    // previous render kernel; distinct buffers (rt_renderer's frame slots) let them overlap it.
+    const size_t npx = size_t(rows) * size_t(W);
+    const rt_scene::Range out_now[4] = {
+        {uintptr_t(rgb), uintptr_t(rgb) + (rgb ? npx * 3 * sizeof(float) : 0)},
+        {uintptr_t(p6), uintptr_t(p6) + (p6 ? npx * 3 : 0)},
+        {uintptr_t(hit_idx), uintptr_t(hit_idx) + (hit_idx ? npx * size_t(o->spp) * sizeof(int32_t) : 0)},
+        {uintptr_t(hit_t), uintptr_t(hit_t) + (hit_t ? npx * size_t(o->spp) * sizeof(float) : 0)}};
+    // a new list layout may place this frame's lists over the previous frame's: serialise too
+    bool overlap = s->set_bytes != set_bytes || std::getenv("RT_EXP_SERIAL_PREP") != nullptr;
+    for (const auto& a : out_now)
+        for (const auto& b : s->prev_out)
+            overlap = overlap || (a.lo < a.hi && b.lo < b.hi && a.lo < b.hi && b.lo < a.hi);
+    const int set = int(k % rt_scene::kSets), nset = int((k + 1) % rt_scene::kSets);
+    char* base = static_cast<char*>(s->work.p);
+    char* lists = base + rt_scene::kSets * kCounterBytes + set * set_bytes;
+    P.live_count = reinterpret_cast<uint32_t*>(base + set * kCounterBytes);
+    P.next_count = reinterpret_cast<uint32_t*>(base + nset * kCounterBytes);
     s->last_tiles_total = P.tiles_total;
-    P.live_tiles = reinterpret_cast<int32_t*>(static_cast<char*>(s->work.p) + 2 * kCounterBytes);
-    P.cut_flag = reinterpret_cast<uint8_t*>(static_cast<char*>(s->work.p) + 2 * kCounterBytes + list_bytes);
+    P.live_tiles = reinterpret_cast<int32_t*>(lists);
+    P.cut_flag = reinterpret_cast<uint8_t*>(lists + list_bytes);
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
-    const int slot = int(s->launches % rt_scene::kRing);
+    const int slot = int(k % rt_scene::kRing);
     // From the cull launch on, a failure leaves the counter sets unknown (counters_dirty).
     auto frame = [&]() -> int {
-        HIP_TRY(hipEventRecord(s->ev0[slot], st));
-        hipLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, P);
+        hipStream_t pp = s->prep;
+        // set k was last read by frame k-3, set k+1 (zeroed by this cull pass) by frame k-2
+        if (k >= 2) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 2), 0));
+        if (k >= 1 && overlap) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 1), 0));
+        if (s->counters_dirty) {
+            HIP_TRY(hipMemsetAsync(base, 0, rt_scene::kSets * kCounterBytes, pp));
+            s->counters_dirty = false;
+        }
+        HIP_TRY(hipEventRecord(s->ev0[slot], pp));
+        hipLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, pp, P);
         HIP_TRY(hipGetLastError());
         if (P.cull && P.sc.ncut > 0) {
             // 16 waves per CU; each takes (list, group) pairs grid-stride (c3: about one each)
             const int cut_blocks = 4 * s->cus;
-            hipLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, st, P);
+            hipLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, pp, P);
             HIP_TRY(hipGetLastError());
         }
+        HIP_TRY(hipEventRecord(s->pdone[slot], pp));
+        HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
         HIP_TRY(hipEventRecord(s->evm[slot], st));
         const bool big = big_scene_waves(s);
         if (s->deep) launch<MODE_DEEP>(P, samples, false, st);
@@ -2356,6 +2402,8 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         HIP_TRY(hipEventRecord(s->ev1[slot], st));
         return RT_OK;
     };
+    std::copy(std::begin(out_now), std::end(out_now), std::begin(s->prev_out));
+    s->set_bytes = set_bytes;
     rc = frame();
     s->launches++;  // the events of this slot belong to this frame even when it failed
     if (rc != RT_OK) s->counters_dirty = true;
@@ -2398,8 +2446,9 @@ extern "C" int rt_live_tiles(const rt_scene* s, int64_t* live, int64_t* total) {
     const int slot = int((s->launches - 1) % rt_scene::kRing);
     HIP_TRY(hipEventSynchronize(s->ev1[slot]));
     uint32_t c[8 * COUNTER_STRIDE];
-    const size_t set_bytes = 9 * COUNTER_STRIDE * sizeof(uint32_t);  // the last frame's counter set
-    HIP_TRY(hipMemcpy(c, static_cast<const char*>(s->work.p) + ((s->launches - 1) & 1) * set_bytes, sizeof(c),
+    // the last frame's counter set (the sets sit at the start of the work buffer)
+    const size_t counter_bytes = 9 * COUNTER_STRIDE * sizeof(uint32_t);
+    HIP_TRY(hipMemcpy(c, static_cast<const char*>(s->work.p) + ((s->launches - 1) % rt_scene::kSets) * counter_bytes, sizeof(c),
                       hipMemcpyDeviceToHost));
     for (int k = 0; k < 8; ++k) *live += c[k * COUNTER_STRIDE];
     return RT_OK;

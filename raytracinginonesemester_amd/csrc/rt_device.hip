@@ -78,6 +78,7 @@ struct SceneView {
     const float4* __restrict__ inode;
     const float4* __restrict__ wnode;  // 4-ary records (8 x float4) by internal index, if wide
     const float4* __restrict__ ibox;
+    const float4* __restrict__ rootb;  // the root's box, pairs (x | y, z), after ibox's entries
     const float4* __restrict__ leaf;
     const float4* __restrict__ tnorm;
     const int32_t* __restrict__ objids;
@@ -207,14 +208,15 @@ __device__ __forceinline__ uint32_t ldc_u32(const uint32_t* p) {
 __device__ __forceinline__ v2f lo2(float4 q) { return (v2f){q.x, q.y}; }
 __device__ __forceinline__ v2f hi2(float4 q) { return (v2f){q.z, q.w}; }
 
-// Box of a node for the pop-time re-test: the root's from the kernel arguments, a leaf's from
+// Box of a node for the pop-time re-test: the root's from rootb, a leaf's from
 // its record, an internal node's from ibox.
 __device__ __forceinline__ BoxP own_box(const SceneView& sc, uint32_t ref, bool is_root) {
     BoxP b;
     if (is_root) {
-        b.x = (v2f){sc.root_box[0], sc.root_box[3]};
-        b.y = (v2f){sc.root_box[1], sc.root_box[4]};
-        b.z = (v2f){sc.root_box[2], sc.root_box[5]};
+        const float4 p = ldc(sc.rootb), q = ldc(sc.rootb + 1);
+        b.x = lo2(p);
+        b.y = hi2(p);
+        b.z = lo2(q);
     } else if (ref & LEAF_BIT) {
         const float4* L = sc.leaf + 4 * (size_t)(ref & ~LEAF_BIT);
         const float4 c = ldc(L + 2), d = ldc(L + 3);
@@ -612,16 +614,44 @@ __device__ __forceinline__ RayPre camera_ray(const RenderParams& P, bool valid, 
 // missColor on a miss (query.h:181-183), else ShadeDirect (shader.h:65-110) with one shadow
 // ray per light; the bounce has no effect at depth 1 and is not traced.  All lanes of a wave
 // call it (the shadow traversals are wave-wide).
+// Per-lane state parked in LDS across a shadow traversal (PARK_SLOTS floats per lane, struct
+// of arrays with stride BLOCK): the traversal needs every VGPR the kernel's occupancy allows, and
+// values kept live across it were spilled to scratch (private memory through L2/HBM); LDS is a
+// few tens of cycles away and otherwise unused by the render kernels.
+constexpr int PARK_SLOTS = 12;
+struct Park {
+    float* p;  // this lane's slot 0 (LDS)
+    __device__ __forceinline__ void put(int k, float v) const { p[k * BLOCK] = v; }
+    __device__ __forceinline__ float get(int k) const { return p[k * BLOCK]; }
+    // The traversal between put and get writes no LDS, so without this the compiler would
+    // forward the stored values and keep them in registers after all.
+    __device__ __forceinline__ static void fence() { asm volatile("" ::: "memory"); }
+};
+
 template <int MODE>
-__device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid, const RayPre& ray, const HitState& hs) {
+__device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, const RayPre& ray, const HitState& hs,
+                                       float* park_lds) {
     const SceneView& sc = P.sc;
-    const bool hit = valid && hs.slot >= 0;
-    f3 radiance = mk(0.f, 0.f, 0.f);
-    if (valid && !hit) radiance = add(radiance, mul(mk(1.f, 1.f, 1.f), P.miss));
-    if (ballot(hit) == 0) return clamp01(radiance);
+    const Park pk{park_lds + threadIdx.x};
+    bool valid = valid_in;
+    bool hit = valid && hs.slot >= 0;
+    // radiance = 0 + (1,1,1) * missColor on a miss (query.h:181-183), 0 + (1,1,1) * Lo on a hit:
+    // made once the lights are done, so nothing but Lo is live across the shadow traversals
+    auto radiance_of = [&](f3 Lo) {
+        f3 radiance = mk(0.f, 0.f, 0.f);
+        if (valid && !hit) radiance = add(radiance, mul(mk(1.f, 1.f, 1.f), P.miss));
+        if (hit) radiance = add(radiance, mul(mk(1.f, 1.f, 1.f), Lo));
+        return clamp01(radiance);
+    };
+    if (ballot(hit) == 0) return radiance_of(mk(0.f, 0.f, 0.f));
+    int32_t slot = hs.slot;
+    // The camera ray's origin is the (uniform) camera centre; only its direction is per lane.
+    RayPre cray;
+    cray.o = ray.o;
+    cray.d = ray.d;
     f3 Lo = mk(0.f, 0.f, 0.f);
     if (hit) {
-        const DevMaterial m = material_of(sc, leaf_tri<(MODE & MODE_DEEP) != 0>(sc, hs.slot));
+        const DevMaterial m = material_of(sc, leaf_tri<(MODE & MODE_DEEP) != 0>(sc, slot));
         Lo = add(Lo, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 0.05f));
         Lo = add(Lo, mk(m.emission[0], m.emission[1], m.emission[2]));
     }
@@ -630,24 +660,25 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid, const 
         const f3 lpos = mk(lt.pos[0], lt.pos[1], lt.pos[2]);
         float dist = 0.f;
         bool need = false, lit = false;
-        f3 contrib = mk(0.f, 0.f, 0.f);
+        f3 Lo_lit = Lo;
         // Lanes without a shadow ray leave sray unset: the traversal masks them out (their
         // results are never read), and copying the camera ray in would keep it live.
         RayPre sray;
         if (hit) {
             // The hit record (point, normals, material) is rebuilt per light from the leaf and
             // the camera ray (the accepting test's own t/u/v), so none of it stays live across the
-            // shadow traversal (it was spilled there: ~100 B of scratch per lane).
-            const SurfHit sh = resolve_hit<(MODE & MODE_DEEP) != 0>(sc, ray, hs.slot);
+            // shadow traversal.
+            const SurfHit sh = resolve_hit<(MODE & MODE_DEEP) != 0>(sc, cray, slot);
             const f3 N = unit(sh.n);
-            const f3 V = unit(sub(ray.o, sh.p));
+            const f3 V = unit(sub(cray.o, sh.p));
             const f3 L = unit(sub(lpos, sh.p));
             const float NdotL = fmaxf(dot(N, L), 0.0f);
             if (NdotL > 0.0f) {
                 const DevMaterial m = material_of(sc, sh.tri);
                 const f3 f = eval_brdf(m, sh.n, V, L);
                 const f3 rad = scale(mk(lt.color[0], lt.color[1], lt.color[2]), (float)lt.intensity);
-                contrib = scale(mul(rad, f), NdotL);
+                // Lo + contrib, taken below if the shadow ray is clear (the same single add)
+                Lo_lit = add(Lo, scale(mul(rad, f), NdotL));
                 lit = true;
                 // IsInShadow (shader.h:44-62)
                 const f3 toL = sub(lpos, sh.p);
@@ -661,13 +692,32 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid, const 
 #ifdef RT_EXP_NO_SHADOW  // timing experiments only (wrong output): skip the shadow traversal
         need = false;
 #endif
+        pk.put(0, cray.d.x);
+        pk.put(1, cray.d.y);
+        pk.put(2, cray.d.z);
+        pk.put(3, __int_as_float(slot));
+        pk.put(4, Lo.x);
+        pk.put(5, Lo.y);
+        pk.put(6, Lo.z);
+        pk.put(7, Lo_lit.x);
+        pk.put(8, Lo_lit.y);
+        pk.put(9, Lo_lit.z);
+        pk.put(10, __int_as_float((valid ? 1 : 0) | (hit ? 2 : 0) | (lit ? 4 : 0)));
+        Park::fence();
         HitState shs;
         traverse<MODE>(sc, sray, need, true, dist, shs);
         const bool occluded = need && shs.slot >= 0 && shs.bestT < dist;
-        if (lit && !occluded) Lo = add(Lo, contrib);
+        Park::fence();
+        const int fl = __float_as_int(pk.get(10));
+        valid = (fl & 1) != 0;
+        hit = (fl & 2) != 0;
+        lit = (fl & 4) != 0;
+        const bool take = lit && !occluded;
+        Lo = take ? mk(pk.get(7), pk.get(8), pk.get(9)) : mk(pk.get(4), pk.get(5), pk.get(6));
+        slot = __float_as_int(pk.get(3));
+        cray.d = mk(pk.get(0), pk.get(1), pk.get(2));
     }
-    if (hit) radiance = add(radiance, mul(mk(1.f, 1.f, 1.f), Lo));
-    return clamp01(radiance);
+    return radiance_of(Lo);
 }
 
 
@@ -677,7 +727,7 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid, const 
 template <int MODE, bool D1>
 // The primary-hit AOV (P.hit_idx / P.hit_t at element aov, when aov >= 0) is written as soon as
 // the camera ray's traversal ends, so nothing of it stays live across the shading.
-__device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int64_t aov) {
+__device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int64_t aov, float* park) {
     const SceneView& sc = P.sc;
     RayPre ray = camera_ray(P, valid, x, y, s);
     if constexpr (D1) {
@@ -701,7 +751,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
 #ifdef RT_EXP_NO_SHADE  // timing experiments only (wrong output): primary traversal only
         return mk(hs.bestT, 0.f, 0.f);
 #endif
-        return shade_d1<MODE>(P, valid, ray, hs);
+        return shade_d1<MODE>(P, valid, ray, hs, park);
     }
     uint32_t rng = make_rng_seed(x, y, s);
 
@@ -1161,7 +1211,7 @@ __device__ __forceinline__ int planned_tile(const RenderParams& P, int len, int 
 // One sample per lane: a block covers a tile_w x tile_h pixel tile x spp samples (spp a power
 // of two <= 256, tile_w*tile_h*spp == BLOCK); per-pixel sums run in sample order from LDS.
 template <int MODE, bool D1>
-__device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, float* col, int* kpix) {
+__device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, float* col, int* kpix, float* park) {
     const int t = (int)threadIdx.x;
     {
         const int s = t & (P.spp - 1);  // spp and tile_w are powers of two here
@@ -1191,7 +1241,7 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
         // it, or addresses made from it, live (and spilled) across the shading.
         if (s == 0) kpix[t >> P.spp_log2] = pix;
         const int64_t aov = valid && P.hit_idx ? (int64_t)pix * P.spp + s : -1;
-        const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, aov);
+        const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, aov, park);
         RT_PHASE(P, x, r, 1);
         col[3 * t] = c.x;
         col[3 * t + 1] = c.y;
@@ -1235,7 +1285,7 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
 
 // General spp: one pixel per lane looping over its samples in order (query.cu:146-163).
 template <int MODE, bool D1>
-__device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
+__device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, float* park) {
     const int t = (int)threadIdx.x;
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int x = tx * P.tile_w + t % P.tile_w;
@@ -1245,7 +1295,7 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile) {
     f3 acc = mk(0.f, 0.f, 0.f);
     for (int s = 0; s < P.spp; ++s) {
         const int64_t aov = valid && P.hit_idx ? ((int64_t)r * P.W + x) * P.spp + s : -1;
-        acc = add(acc, trace_sample<MODE, D1>(P, valid, x, y, s, aov));
+        acc = add(acc, trace_sample<MODE, D1>(P, valid, x, y, s, aov, park));
     }
     if (valid) {
         const float fs = (float)P.spp;
@@ -1283,6 +1333,7 @@ template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES>
 __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
     __shared__ int kpix[SAMPLES ? BLOCK : 1];
+    __shared__ float park[D1 ? PARK_SLOTS * BLOCK : 1];  // shade_d1's state across shadow rays
 #ifdef RT_WAVE_TIMES
     const unsigned long long wt0 = wall_clock64();
 #endif
@@ -1293,8 +1344,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
     const int tile = planned_tile(P, list_length(P, q), q, i);
     if (tile < 0) return;
     if (P.sc.ncut > 0 && P.cut_flag[(size_t)q * P.queue_cap + i]) return;  // culled by tile_cut_kernel
-    if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col, kpix);
-    else pixels_tile<MODE, D1>(P, tile);
+    if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col, kpix, park);
+    else pixels_tile<MODE, D1>(P, tile, park);
 #ifdef RT_WAVE_TIMES
     if (g_wave_times && lane_id() == 0) {
         const size_t k = ((size_t)tile * (BLOCK / 64) + threadIdx.x / 64) * 2;
@@ -2064,6 +2115,10 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
         }
         if ((rc = s->tri.upload(ht.data(), ht.size() * sizeof(float4))) != RT_OK) return rc;
     }
+    // the root's box (pair layout) after the internal boxes: the traversals' first test reads it
+    // with scalar loads like any other box (SceneView::rootb)
+    hib.push_back(make_float4(s->root_box[0], s->root_box[3], s->root_box[1], s->root_box[4]));
+    hib.push_back(make_float4(s->root_box[2], s->root_box[5], 0.f, 0.f));
     if ((rc = s->ibox.upload(hib.data(), hib.size() * sizeof(float4))) != RT_OK) return rc;
     if ((rc = s->leaf.upload(hlf.data(), hlf.size() * sizeof(float4))) != RT_OK) return rc;
     if ((rc = s->tnorm.upload(hnm.data(), hnm.size() * sizeof(float4))) != RT_OK) return rc;
@@ -2161,9 +2216,10 @@ int prepare_jitter(rt_scene* s, const rt_render_opts* o) {
 }
 
 // tiles_virtual blocks (rounded up to a multiple of 8), one per planned virtual block.
+int g_exp_grid = 0;  // RT_EXP_GRID experiment: render grid override (0 = tiles_virtual)
 template <int MODE, bool SAMPLES>
 void launch_mode(const RenderParams& P, bool big, hipStream_t st) {
-    const dim3 grid((P.tiles_virtual + 7) / 8 * 8);
+    const dim3 grid(g_exp_grid > 0 ? g_exp_grid : (P.tiles_virtual + 7) / 8 * 8);
     if (P.max_depth == 1) {
         if constexpr (SAMPLES && MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0) {
             if (big) {  // more waves and packed box tests (c5 faster with each; both slower on c3)
@@ -2263,6 +2319,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.sc.wnode = static_cast<const float4*>(s->wnode.p);
     P.sc.wide = s->wide && !(o->flags & RT_FLAG_BINARY) ? 1 : 0;
     P.sc.ibox = static_cast<const float4*>(s->ibox.p);
+    P.sc.rootb = static_cast<const float4*>(s->ibox.p) + s->ibox.n / sizeof(float4) - 2;
     P.sc.leaf = static_cast<const float4*>(s->leaf.p);
     P.sc.tnorm = static_cast<const float4*>(s->tnorm.p);
     P.sc.objids = static_cast<const int32_t*>(s->objids.p);
@@ -2391,6 +2448,19 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipEventRecord(s->pdone[slot], pp));
+        g_exp_grid = 0;
+        if (const char* e = std::getenv("RT_EXP_GRID")) {  // experiment: "exact" = 8 x longest list
+            if (std::strcmp(e, "exact") == 0 && P.nqueues == 8) {
+                uint32_t c[8 * COUNTER_STRIDE];
+                HIP_TRY(hipEventSynchronize(s->pdone[slot]));
+                HIP_TRY(hipMemcpy(c, P.live_count, sizeof(c), hipMemcpyDeviceToHost));
+                uint32_t m = 0;
+                for (int q = 0; q < 8; ++q) m = std::max(m, c[q * COUNTER_STRIDE]);
+                g_exp_grid = int(8 * std::max(m, 1u));
+            } else {
+                g_exp_grid = (std::atoi(e) + 7) / 8 * 8;
+            }
+        }
         HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
         HIP_TRY(hipEventRecord(s->evm[slot], st));
         const bool big = big_scene_waves(s);

@@ -402,6 +402,23 @@ __host__ __device__ __forceinline__ float asf(uint32_t u) { float f; __builtin_m
 __host__ __device__ __forceinline__ uint64_t asu64(double f) { uint64_t u; __builtin_memcpy(&u, &f, 8); return u; }
 __host__ __device__ __forceinline__ double asd(uint64_t u) { double f; __builtin_memcpy(&f, &u, 8); return f; }
 
+// A double constant of the powf polynomials.  On the device it is made by two s_mov_b32 in
+// volatile asm where it is used: otherwise the compiler hoists the constants out of the shading
+// loop into VGPR pairs that stay live across the shadow traversal and spills them to scratch.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RT_KF64(name, val)                                                                     \
+    double name;                                                                               \
+    {                                                                                          \
+        constexpr uint64_t b_ = __builtin_bit_cast(uint64_t, (double)(val));                   \
+        uint32_t lo_, hi_;                                                                     \
+        asm volatile("s_mov_b32 %0, %1" : "=s"(lo_) : "i"((uint32_t)b_));                      \
+        asm volatile("s_mov_b32 %0, %1" : "=s"(hi_) : "i"((uint32_t)(b_ >> 32)));              \
+        name = __builtin_bit_cast(double, ((uint64_t)hi_ << 32) | lo_);                        \
+    }
+#else
+#define RT_KF64(name, val) const double name = (val);
+#endif
+
 __host__ __device__ __forceinline__ double log2_inline(uint32_t ix) {
     const uint32_t tmp = ix - 0x3f330000u;
     const int i = int((tmp >> 19) % 16u);
@@ -410,8 +427,11 @@ __host__ __device__ __forceinline__ double log2_inline(uint32_t ix) {
     const int k = int32_t(top) >> 23;
     const LogEntry e = log_tab(i);
     const double z = double(asf(iz));
-    const double A0 = 0x1.27616c9496e0bp-2, A1 = -0x1.71969a075c67ap-2, A2 = 0x1.ec70a6ca7baddp-2,
-                 A3 = -0x1.7154748bef6c8p-1, A4 = 0x1.71547652ab82bp+0;
+    RT_KF64(A0, 0x1.27616c9496e0bp-2)
+    RT_KF64(A1, -0x1.71969a075c67ap-2)
+    RT_KF64(A2, 0x1.ec70a6ca7baddp-2)
+    RT_KF64(A3, -0x1.7154748bef6c8p-1)
+    RT_KF64(A4, 0x1.71547652ab82bp+0)
     const double r = fma(z, e.invc, -1.0);
     const double y0 = e.logc + double(k);
     const double r2 = r * r;
@@ -426,7 +446,9 @@ __host__ __device__ __forceinline__ double log2_inline(uint32_t ix) {
 
 __host__ __device__ __forceinline__ float exp2_inline(double xd, uint32_t sign_bias) {
     const double SHIFT = 0x1.8p+47;  // 0x1.8p52 / 32
-    const double C0 = 0x1.c6af84b912394p-5, C1 = 0x1.ebfce50fac4f3p-3, C2 = 0x1.62e42ff0c52d6p-1;
+    RT_KF64(C0, 0x1.c6af84b912394p-5)
+    RT_KF64(C1, 0x1.ebfce50fac4f3p-3)
+    RT_KF64(C2, 0x1.62e42ff0c52d6p-1)
     double kd = xd + SHIFT;
     const uint64_t ki = asu64(kd);
     kd -= SHIFT;

@@ -1,7 +1,7 @@
 """Interleaved in-process A/B of run-time settings the library reads per call (environment
 variables), one device scene, frames checked bit-identical across settings.
 
-    python scripts/env_ab.py [--config c3] [--rounds 5] [--reps 20] '{"name": {"VAR": "value"}, ...}'
+    python scripts/env_ab.py [--config c3] [--rounds 5] [--reps 20] '{"name": {"VAR": "value"}, ...}' | @file.json
 
 Per setting: median render-kernel ms, device-frame ms (HIP events) and wall ms per frame of a
 back-to-back loop on one stream.
@@ -28,7 +28,7 @@ ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("settings")
 a = ap.parse_args()
-settings = json.loads(a.settings)
+settings = json.loads(Path(a.settings[1:]).read_text() if a.settings.startswith("@") else a.settings)
 
 cfg = configs.G_CONFIGS[a.config]
 sp = configs.scene_path(cfg["scene"])

@@ -391,6 +391,10 @@ int rt_frame_times(const rt_scene* s, float* ms_out, int max, int* n_out);
  * all tiles (the tree-cut pass may still cull some of the survivors; those are flagged, not
  * removed from the lists).  Waits for that call to finish. */
 int rt_live_tiles(const rt_scene* s, int64_t* live, int64_t* total);
+/* Tiles of the most recent rt_render_device call that its render kernel took first (heavy-first
+ * dispatch: tiles whose waves took >= 1/4 of the previous finished frame's render kernel in the
+ * last frame that rendered them; their order only, never their pixels).  Waits for that call. */
+int rt_heavy_tiles(const rt_scene* s, int64_t* heavy);
 
 int rt_device_count(int* n);
 const char* rt_last_error(void);

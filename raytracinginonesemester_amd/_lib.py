@@ -164,6 +164,7 @@ SIGNATURES = {
     "rt_kernel_times": (I, [P, P, I, P]),
     "rt_frame_times": (I, [P, P, I, P]),
     "rt_live_tiles": (I, [P, P, P]),
+    "rt_heavy_tiles": (I, [P, P]),
     "rt_device_count": (I, [P]),
     "rt_last_error": (C.c_char_p, []),
     "rt_abi_version": (I, []),

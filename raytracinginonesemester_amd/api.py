@@ -285,6 +285,12 @@ class DeviceScene:
         check(lib().rt_live_tiles(self._h, C.byref(live), C.byref(total)))
         return live.value, total.value
 
+    def heavy_tiles(self) -> int:
+        """Tiles the most recent render dispatched first (heavy-first order, speed only)."""
+        n = C.c_int64()
+        check(lib().rt_heavy_tiles(self._h, C.byref(n)))
+        return n.value
+
     def frame_times(self, max_launches: int = 256) -> np.ndarray:
         """ms of the whole device frame (list reset, cull pre-pass, render kernel)."""
         out = np.zeros(max_launches, np.float32)

@@ -111,7 +111,7 @@ struct RenderParams {
     f3 miss_pixel;                                    // pixel value when all spp samples miss
     uint32_t* live_count;                             // [k * COUNTER_STRIDE], tile_cull_kernel
     int32_t* live_tiles;                              // nqueues lists of queue_cap entries
-    uint8_t* cut_flag;    // per list slot: 1 = tile_cut_kernel culled the tile (read when sc.ncut > 0)
+    int32_t* cut_tiles;   // tile_cut_kernel's survivors (not culled, not heavy), per list (sc.ncut > 0)
     uint32_t* next_count; // the other counter set, zeroed by tile_cull_kernel for the next frame
     int32_t cut_force;    // test every candidate in tile_cut_kernel (no pass-through)
     int32_t nqueues;
@@ -122,6 +122,16 @@ struct RenderParams {
     float* __restrict__ hit_t;
     uint8_t* __restrict__ p6;  // optional: write_p6-default samples of the pixels (rows*W*3 bytes)
     uint8_t miss_p6[4];        // the culled pixels' samples
+    // Heavy-first dispatch (speed only, an approximate longest-first schedule): render waves
+    // record their duration per tile (tile_cost, 4 x u16 per tile, 10 ns ticks); the next frame's
+    // cut pass moves tiles whose last cost is >= heavy_ticks[c] (descending) to list q's class-c
+    // heavy list (heavy_tiles, heavy_cap entries per (class, list), lengths in counter slots
+    // heavy_counter(c, q)).  The first 8 * NCLASS * heavy_cap render blocks take the heavy tiles,
+    // each list's heaviest class first, so the longest tiles start first.  heavy_cap == 0: off.
+    uint16_t* __restrict__ tile_cost;
+    int32_t* heavy_tiles;
+    int32_t heavy_cap;
+    uint32_t heavy_ticks[4];  // NCLASS thresholds, descending
 };
 
 // ---- wave primitives ------------------------------------------------------------------
@@ -266,7 +276,11 @@ __device__ __forceinline__ uint64_t box_hit_mask(const RayPre& r, const BoxP& b,
     amb &= ~h2;
     if (amb == 0) return hit;
     RT_STAT(12, 1);
-    return hit | (ballot(box_hit_exact(r, b, (double)kRayTMin, (double)tmax)) & amb);
+    // double(tmin), double(FLT_MAX): made here (RT_KF64), not hoisted into spilled VGPR pairs
+    RT_KF64(tmin_d, (double)kRayTMin)
+    RT_KF64(fltmax_d, (double)FLT_MAX)
+    const double tmax_d = tmax == FLT_MAX ? fltmax_d : (double)tmax;
+    return hit | (ballot(box_hit_exact(r, b, tmin_d, tmax_d)) & amb);
 }
 
 // Result of one closest-hit query.
@@ -625,7 +639,11 @@ struct Park {
     __device__ __forceinline__ float get(int k) const { return p[k * BLOCK]; }
     // The traversal between put and get writes no LDS, so without this the compiler would
     // forward the stored values and keep them in registers after all.
-    __device__ __forceinline__ static void fence() { asm volatile("" ::: "memory"); }
+    __device__ __forceinline__ static void fence() {
+#ifndef RT_EXP_NO_PARK  // experiment: let the compiler forward the parked values (registers)
+        asm volatile("" ::: "memory");
+#endif
+    }
 };
 
 template <int MODE>
@@ -1035,6 +1053,14 @@ __device__ __forceinline__ int global_row(const RenderParams& P, int r) {
 // The lists' length counters sit 256 B apart (separate channels) so the appends do not
 // serialise.
 constexpr int COUNTER_STRIDE = 64;
+constexpr int NCLASS = 3;                        // heavy cost classes
+// A counter set: 9 list counters COUNTER_STRIDE apart (8 live lists + a spare), then the
+// heavy list lengths packed (class-major, 8 per class: the render blocks read them all with a
+// few wide scalar loads; their appends are few).
+constexpr int HEAVY_SLOT0 = 9;
+constexpr int CUT_SLOT0 = HEAVY_SLOT0 + 8 * NCLASS;  // then 8: lengths of the cut pass's survivor lists
+constexpr int COUNTER_SET_U32 = (CUT_SLOT0 + 8) * COUNTER_STRIDE;
+__host__ __device__ constexpr int heavy_counter(int k, int q) { return (HEAVY_SLOT0 + 8 * k + q) * COUNTER_STRIDE; }
 __device__ __forceinline__ int queue_of_tile(const RenderParams& P, int tile) {
     if (P.nqueues == 1) return 0;
     if (P.tile_order == RT_TILES_XCD_CHUNK) return (int)((int64_t)tile * 8 / P.tiles_total);
@@ -1115,7 +1141,7 @@ __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
     // Counter sets rotate over three frames (no reset launch): this frame's set was zeroed by
     // the previous frame's pass; zero the next frame's (its last user, frame k-2, has finished:
     // the scene's prep stream waited for it).
-    if (blockIdx.x == 0 && threadIdx.x < 9) P.next_count[threadIdx.x * COUNTER_STRIDE] = 0u;
+    if (blockIdx.x == 0 && threadIdx.x < CUT_SLOT0 + 8) P.next_count[threadIdx.x * COUNTER_STRIDE] = 0u;
     bool live = false;
     if (tile < P.tiles_total) {
         const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
@@ -1131,10 +1157,11 @@ __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
 // Pass 2 (sc.ncut > 0), one wave per CUT_GROUP consecutive slots of a live list, one lane
 // per box of the cut (sc.cut, <= 64 boxes that hold every leaf exactly once): a tile is culled
 // when every lane proves its box missed by every ray of the tile (tile_misses_box_f; the tile
-// bounds are wave-uniform).  A culled tile gets its miss pixels here and the flag of its slot,
-// which the render block of that slot reads before anything else; the lists are not
-// compacted, so there are no atomics (appending the survivors to fresh lists cost c3 ~15 us of
-// counter contention).
+// bounds are wave-uniform).  A culled tile gets its miss pixels here; the others go to list q's
+// heavy lists (below) or its survivor list, one atomic per (wave, list): the render kernel's
+// blocks then find only real tiles (a block for a culled or moved slot that leaves at once still
+// cost its launch and loads).  The pass runs on the scene's prep stream, overlapping the
+// previous frame's render kernel, so its atomics are off the critical path.
 #ifndef RT_CUT_GROUP
 #define RT_CUT_GROUP 8
 #endif
@@ -1186,7 +1213,41 @@ __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
                 culled |= 1ull << j;
             }
         }
-        if ((int)lane < m) P.cut_flag[slot0 + lane] = (uint8_t)((culled >> lane) & 1ull);
+        // Heavy-first: surviving tiles whose last render took >= heavy_ticks[c] go to list q's
+        // class-c heavy list (a full heavy list leaves the tile to the survivor list).
+        bool heavy = false;
+        if (P.heavy_cap > 0) {
+            int cls = NCLASS;
+            if ((int)lane < m && !((culled >> lane) & 1ull)) {
+                const uint2 c = *reinterpret_cast<const uint2*>(P.tile_cost + 4 * (size_t)my_tile);
+                const uint32_t mx = max(max(c.x & 0xffffu, c.x >> 16), max(c.y & 0xffffu, c.y >> 16));
+                for (int k = NCLASS - 1; k >= 0; --k)
+                    if (mx >= P.heavy_ticks[k]) cls = k;
+            }
+            for (int k = 0; k < NCLASS; ++k) {
+                const uint64_t hm = ballot(cls == k);
+                if (hm == 0) continue;
+                const uint32_t leader = (uint32_t)__builtin_ctzll(hm);
+                uint32_t base = 0;
+                if (lane == leader)
+                    base = atomicAdd(&P.live_count[heavy_counter(k, q)], (uint32_t)__popcll(hm));
+                const uint32_t idx = rdlane(base, leader) + (uint32_t)__popcll(hm & ((1ull << lane) - 1));
+                if (cls == k && idx < (uint32_t)P.heavy_cap) {
+                    P.heavy_tiles[((size_t)k * 8 + q) * P.heavy_cap + idx] = my_tile;
+                    heavy = true;
+                }
+            }
+        }
+        // the rest go to list q's survivor list (the render kernel's normal phase)
+        const bool keep = (int)lane < m && !((culled >> lane) & 1ull) && !heavy;
+        const uint64_t km = ballot(keep);
+        if (km != 0) {
+            const uint32_t leader = (uint32_t)__builtin_ctzll(km);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&P.live_count[(CUT_SLOT0 + q) * COUNTER_STRIDE], (uint32_t)__popcll(km));
+            if (keep)
+                P.cut_tiles[(size_t)q * P.queue_cap + rdlane(base, leader) + (uint32_t)__popcll(km & ((1ull << lane) - 1))] = my_tile;
+        }
     }
 }
 
@@ -1318,13 +1379,14 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, flo
 // at once.  (Looping a block over several slots measured no faster on c3 and, by keeping the
 // per-sample invariants live across the loop, spilled 224 B instead of 144 B per lane: c5 -6 %
 // without the loop.)
-// WAVES: waves per SIMD the kernel is compiled for.  6 (80 VGPRs) is fastest for scenes whose
-// nodes stay in L2 (c3: 6 > 5, 7 > 4 waves); scenes far larger than the L2s (c5, 345 MB) gain
-// from more waves of latency hiding despite more spills, so the depth-1 sample kernels are
-// also built for RT_BIG_WAVES with packed box tests (c5: 8 waves 94.5 ms < 7 waves 96.4 <
-// 6 waves 99.9; launch picks by scene size, big_scene_waves).
+// WAVES: waves per SIMD the kernel is compiled for.  With the shading spills removed (8 B of
+// scratch per lane left at 80 VGPRs, 28 B at 72) 7 waves (72 VGPRs) is fastest for scenes whose
+// nodes stay in L2: c3 7 waves 0.267 ms < 6 waves 0.273 < 5 waves 0.294 (one box, interleaved;
+// before the spill fixes 6 waves 0.290).  Scenes far larger than the L2s (c5, 345 MB) gain from
+// 8 waves of latency hiding with packed box tests despite 60 B of spills (c5: 8 waves 85.5 ms <
+// 7 waves 88.0 < 6 waves 89.2; launch picks by scene size, big_scene_waves).
 #ifndef RT_RENDER_WAVES
-#define RT_RENDER_WAVES 6
+#define RT_RENDER_WAVES 7
 #endif
 #ifndef RT_BIG_WAVES
 #define RT_BIG_WAVES 8
@@ -1337,15 +1399,53 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
 #ifdef RT_WAVE_TIMES
     const unsigned long long wt0 = wall_clock64();
 #endif
+    // the wave's start time goes through LDS (an SGPR pair live across the whole tile spilled)
+    __shared__ uint32_t t_start[BLOCK / 64], t_tile[BLOCK / 64];
+    if (P.tile_cost && lane_id() == 0) t_start[threadIdx.x / 64] = (uint32_t)wall_clock64();
     const int b = (int)blockIdx.x;
-    if (b >= P.tiles_virtual) return;
+    if (b >= P.tiles_virtual + 8 * NCLASS * P.heavy_cap) return;
+    int tile = -1;
+    // Virtual index i = b >> 3 of list q = b & 7 (the block's XCD).  Heavy phase: the first
+    // NCLASS * heavy_cap indices, list q's heavy entries (its classes in order, heaviest first)
+    // and then nothing; then the list's slots.  Dispatch is in block order across the XCDs, so
+    // every list's heavy tiles go before any list's normal slots.  A block reads only its own
+    // list's counters: empty blocks must leave at once (every extra scalar load of the ~10^5
+    // empty blocks showed in the kernel time).
     const int q = P.nqueues == 1 ? 0 : (b & 7);
-    const int i = P.nqueues == 1 ? b : (b >> 3);
-    const int tile = planned_tile(P, list_length(P, q), q, i);
-    if (tile < 0) return;
-    if (P.sc.ncut > 0 && P.cut_flag[(size_t)q * P.queue_cap + i]) return;  // culled by tile_cut_kernel
+    int i = P.nqueues == 1 ? b : (b >> 3);
+    if (P.heavy_cap > 0) {
+        if (i < NCLASS * P.heavy_cap) {
+            int k = 0;
+            for (; k < NCLASS; ++k) {
+                const int n = min((int)ldc_u32(P.live_count + heavy_counter(k, q)), P.heavy_cap);
+                if (i < n) break;
+                i -= n;
+            }
+            if (k == NCLASS) return;
+            tile = (int)ldc_u32(reinterpret_cast<const uint32_t*>(P.heavy_tiles) + ((size_t)k * 8 + q) * P.heavy_cap + i);
+            i = -1;
+        } else {
+            i -= NCLASS * P.heavy_cap;
+        }
+    }
+    if (i >= 0) {
+        if (P.sc.ncut > 0) {  // the cut pass's survivors
+            const int len = (int)ldc_u32(&P.live_count[(CUT_SLOT0 + q) * COUNTER_STRIDE]);
+            if (i >= len) return;
+            tile = (int)ldc_u32(reinterpret_cast<const uint32_t*>(P.cut_tiles) + (size_t)q * P.queue_cap + i);
+        } else {
+            tile = planned_tile(P, list_length(P, q), q, i);
+            if (tile < 0) return;
+        }
+    }
+    if (P.tile_cost && lane_id() == 0) t_tile[threadIdx.x / 64] = (uint32_t)tile;
     if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col, kpix, park);
     else pixels_tile<MODE, D1>(P, tile, park);
+    if (P.tile_cost && lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
+        asm volatile("" ::: "memory");
+        const uint32_t d = (uint32_t)wall_clock64() - t_start[threadIdx.x / 64];
+        P.tile_cost[4 * (size_t)t_tile[threadIdx.x / 64] + threadIdx.x / 64] = (uint16_t)(d < 0xffffu ? d : 0xffffu);
+    }
 #ifdef RT_WAVE_TIMES
     if (g_wave_times && lane_id() == 0) {
         const size_t k = ((size_t)tile * (BLOCK / 64) + threadIdx.x / 64) * 2;
@@ -1816,6 +1916,12 @@ struct rt_scene {
     DevBuf work;  // kSets x (counter set | live lists | cut flags)
     int64_t last_tiles_total = 0;
     int cus = 256;
+    // heavy-first dispatch: per-tile wave durations of the last frames (4 x u16 per tile) for
+    // the tile geometry cost_key, and the latest finished frame's render-kernel time
+    DevBuf cost;
+    uint64_t cost_key = 0;
+    float kernel_ms_est = 0.f;
+    int last_heavy_cap = 0;
     int jitter_spp = -1;
     std::vector<float> jitter_host;
     // Ring of HIP events per frame.  A frame's pre-passes (tile_cull_kernel, tile_cut_kernel)
@@ -2215,11 +2321,13 @@ int prepare_jitter(rt_scene* s, const rt_render_opts* o) {
     return RT_OK;
 }
 
-// tiles_virtual blocks (rounded up to a multiple of 8), one per planned virtual block.
-int g_exp_grid = 0;  // RT_EXP_GRID experiment: render grid override (0 = tiles_virtual)
+// 8 * NCLASS * heavy_cap heavy-phase blocks, then tiles_virtual blocks (rounded up to a multiple of 8),
+// one per planned virtual block.
+// (A grid sized to the longest list, read back on the host, measured no faster on c3 than the
+// full virtual grid: the empty blocks leave at once.)
 template <int MODE, bool SAMPLES>
 void launch_mode(const RenderParams& P, bool big, hipStream_t st) {
-    const dim3 grid(g_exp_grid > 0 ? g_exp_grid : (P.tiles_virtual + 7) / 8 * 8);
+    const dim3 grid((P.tiles_virtual + 7) / 8 * 8 + 8 * NCLASS * P.heavy_cap);
     if (P.max_depth == 1) {
         if constexpr (SAMPLES && MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0) {
             if (big) {  // more waves and packed box tests (c5 faster with each; both slower on c3)
@@ -2381,18 +2489,67 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     if (!P.cull) P.sc.ncut = 0;  // the render kernel reads the cut flags only when the cut pass ran
     P.miss_pixel = miss_pixel_value(o);
     P.nqueues = P.tile_order == RT_TILES_LINEAR ? 1 : 8;
-    P.queue_cap = P.tiles_total;
+    // a list holds at most tiles_x * ceil(tiles_y / 8) tiles (RT_TILES_ROWS) or ceil(tiles / 8)
+    // (RT_TILES_XCD_CHUNK): tiles_virtual / 8 bounds both
+    P.queue_cap = P.tile_order == RT_TILES_LINEAR ? P.tiles_total : P.tiles_x * ((tiles_y + 7) / 8);
     P.tiles_virtual = P.nqueues == 1 ? P.tiles_total : 8 * P.tiles_x * ((tiles_y + 7) / 8);
-    // kSets counter sets (8 live lists + one spare each) at fixed offsets, then kSets x (live
-    // lists | cut flags) sized for this geometry; rotating by frame
-    constexpr size_t kCounterBytes = 9 * COUNTER_STRIDE * sizeof(uint32_t);
+    // Heavy-first dispatch needs the cut pass (it builds the heavy lists) and the 8 lists.
+    // RT_HEAVY_FRAC (speed experiments): a tile is in heavy class c when one of its waves took
+    // at least 2^(NCLASS-1-c) times this fraction of the latest finished frame's render kernel
+    // (0: off).
+    double heavy_frac = 0.08;
+    if (const char* e = std::getenv("RT_HEAVY_FRAC")) heavy_frac = std::atof(e);
+    const bool costs = P.cull && P.sc.ncut > 0 && P.nqueues == 8 && heavy_frac > 0.0;
+    int heavy_cap = 512;  // RT_HEAVY_CAP: entries per (class, list) (speed experiments)
+    if (const char* e = std::getenv("RT_HEAVY_CAP")) heavy_cap = std::max(1, std::atoi(e));
+    P.heavy_cap = costs ? std::min(P.queue_cap, heavy_cap) : 0;
+    // kSets counter sets (8 live lists, one spare, 8 heavy lists each) at fixed offsets, then
+    // kSets x (live lists | cut flags | heavy lists) sized for this geometry; rotating by frame
+    constexpr size_t kCounterBytes = COUNTER_SET_U32 * sizeof(uint32_t);
     const size_t list_bytes = size_t(P.nqueues) * size_t(P.queue_cap) * sizeof(int32_t);
-    const size_t flag_bytes = (size_t(P.nqueues) * size_t(P.queue_cap) + 255) / 256 * 256;
-    const size_t set_bytes = list_bytes + flag_bytes;
+    const size_t cut_bytes = P.sc.ncut > 0 ? list_bytes : 0;
+    const size_t heavy_bytes = size_t(8 * NCLASS) * size_t(P.heavy_cap) * sizeof(int32_t);
+    const size_t set_bytes = list_bytes + cut_bytes + heavy_bytes;
     const size_t work_bytes = rt_scene::kSets * (kCounterBytes + set_bytes);
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint64_t k = s->launches;
     auto ev1_of = [&](uint64_t f) { return s->ev1[f % rt_scene::kRing]; };
+    // The latest finished frame's render-kernel time sets the heavy threshold (non-blocking
+    // queries; none finished yet: the previous estimate, or no heavy lists).
+    bool cost_reset = false;
+    if (costs) {
+        for (uint64_t back = 1; back <= 3 && back <= k; ++back) {
+            const int f = int((k - back) % rt_scene::kRing);
+            if (hipEventQuery(s->ev1[f]) != hipSuccess) continue;
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, s->evm[f], s->ev1[f]) == hipSuccess) s->kernel_ms_est = ms;
+            break;
+        }
+        (void)hipGetLastError();  // a not-ready query is not an error of this call
+        // 10 ns ticks (wall_clock64 runs at 100 MHz)
+        for (int c = 0; c < NCLASS; ++c) {
+            const double ticks = std::ldexp(heavy_frac, NCLASS - 1 - c) * double(s->kernel_ms_est) * 1e5;
+            P.heavy_ticks[c] = s->kernel_ms_est > 0.f ? uint32_t(std::clamp(ticks, 1.0, 65535.0)) : 0xffffffffu;
+        }
+        // the costs are per tile of this geometry
+        const uint64_t key = (uint64_t(uint32_t(P.tiles_total)) * 0x9E3779B97F4A7C15ull) ^
+                             (uint64_t(uint32_t(P.tiles_x)) << 40) ^ (uint64_t(uint32_t(W)) << 20) ^
+                             uint64_t(uint32_t(rows)) ^ (uint64_t(uint32_t(P.band_index)) << 52) ^
+                             (uint64_t(uint32_t(P.band_count)) << 58) ^ (uint64_t(uint32_t(P.spp)) << 32);
+        const size_t cost_bytes = size_t(P.tiles_total) * 4 * sizeof(uint16_t);
+        if (s->cost.n < cost_bytes) {
+            if (k > 0) {  // the old buffer may still be written
+                HIP_TRY(hipStreamSynchronize(s->prep));
+                HIP_TRY(hipEventSynchronize(ev1_of(k - 1)));
+            }
+            if ((rc = s->cost.alloc(cost_bytes)) != RT_OK) return rc;
+            s->cost_key = ~key;
+        }
+        cost_reset = s->cost_key != key;
+        s->cost_key = key;
+        P.tile_cost = static_cast<uint16_t*>(s->cost.p);
+    }
+    s->last_heavy_cap = P.heavy_cap;
     if (k > 0 && st != s->last_stream)  // the previous frame of this scene ran elsewhere
         HIP_TRY(hipStreamWaitEvent(st, ev1_of(k - 1), 0));
     s->last_stream = st;
@@ -2414,7 +2571,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         {uintptr_t(hit_idx), uintptr_t(hit_idx) + (hit_idx ? npx * size_t(o->spp) * sizeof(int32_t) : 0)},
         {uintptr_t(hit_t), uintptr_t(hit_t) + (hit_t ? npx * size_t(o->spp) * sizeof(float) : 0)}};
     // a new list layout may place this frame's lists over the previous frame's: serialise too
-    bool overlap = s->set_bytes != set_bytes || std::getenv("RT_EXP_SERIAL_PREP") != nullptr;
+    bool overlap = s->set_bytes != set_bytes || cost_reset || std::getenv("RT_EXP_SERIAL_PREP") != nullptr;
     for (const auto& a : out_now)
         for (const auto& b : s->prev_out)
             overlap = overlap || (a.lo < a.hi && b.lo < b.hi && a.lo < b.hi && b.lo < a.hi);
@@ -2425,7 +2582,8 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.next_count = reinterpret_cast<uint32_t*>(base + nset * kCounterBytes);
     s->last_tiles_total = P.tiles_total;
     P.live_tiles = reinterpret_cast<int32_t*>(lists);
-    P.cut_flag = reinterpret_cast<uint8_t*>(lists + list_bytes);
+    P.cut_tiles = reinterpret_cast<int32_t*>(lists + list_bytes);
+    P.heavy_tiles = reinterpret_cast<int32_t*>(lists + list_bytes + cut_bytes);
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
     const int slot = int(k % rt_scene::kRing);
     // From the cull launch on, a failure leaves the counter sets unknown (counters_dirty).
@@ -2438,6 +2596,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             HIP_TRY(hipMemsetAsync(base, 0, rt_scene::kSets * kCounterBytes, pp));
             s->counters_dirty = false;
         }
+        if (cost_reset) HIP_TRY(hipMemsetAsync(s->cost.p, 0, s->cost.n, pp));  // no heavy tiles yet
         HIP_TRY(hipEventRecord(s->ev0[slot], pp));
         hipLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, pp, P);
         HIP_TRY(hipGetLastError());
@@ -2448,19 +2607,6 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipEventRecord(s->pdone[slot], pp));
-        g_exp_grid = 0;
-        if (const char* e = std::getenv("RT_EXP_GRID")) {  // experiment: "exact" = 8 x longest list
-            if (std::strcmp(e, "exact") == 0 && P.nqueues == 8) {
-                uint32_t c[8 * COUNTER_STRIDE];
-                HIP_TRY(hipEventSynchronize(s->pdone[slot]));
-                HIP_TRY(hipMemcpy(c, P.live_count, sizeof(c), hipMemcpyDeviceToHost));
-                uint32_t m = 0;
-                for (int q = 0; q < 8; ++q) m = std::max(m, c[q * COUNTER_STRIDE]);
-                g_exp_grid = int(8 * std::max(m, 1u));
-            } else {
-                g_exp_grid = (std::atoi(e) + 7) / 8 * 8;
-            }
-        }
         HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
         HIP_TRY(hipEventRecord(s->evm[slot], st));
         const bool big = big_scene_waves(s);
@@ -2507,7 +2653,8 @@ int event_times(const rt_scene* s, const hipEvent_t* from, float* ms_out, int ma
 }
 }  // namespace
 
-extern "C" int rt_live_tiles(const rt_scene* s, int64_t* live, int64_t* total) {
+namespace {
+int live_tiles(const rt_scene* s, int64_t* live, int64_t* heavy, int64_t* total) {
     if (!s || !live || !total) return set_error(RT_ERR_ARG, "rt_live_tiles: null argument");
     *live = 0;
     *total = s->last_tiles_total;
@@ -2515,13 +2662,31 @@ extern "C" int rt_live_tiles(const rt_scene* s, int64_t* live, int64_t* total) {
     DeviceGuard g(s->device);
     const int slot = int((s->launches - 1) % rt_scene::kRing);
     HIP_TRY(hipEventSynchronize(s->ev1[slot]));
-    uint32_t c[8 * COUNTER_STRIDE];
+    uint32_t c[COUNTER_SET_U32];
     // the last frame's counter set (the sets sit at the start of the work buffer)
-    const size_t counter_bytes = 9 * COUNTER_STRIDE * sizeof(uint32_t);
+    const size_t counter_bytes = COUNTER_SET_U32 * sizeof(uint32_t);
     HIP_TRY(hipMemcpy(c, static_cast<const char*>(s->work.p) + ((s->launches - 1) % rt_scene::kSets) * counter_bytes, sizeof(c),
                       hipMemcpyDeviceToHost));
     for (int k = 0; k < 8; ++k) *live += c[k * COUNTER_STRIDE];
+    if (heavy) {
+        *heavy = 0;
+        if (s->last_heavy_cap > 0)
+            for (int k = 0; k < 8 * NCLASS; ++k)
+                *heavy += std::min<int64_t>(c[(HEAVY_SLOT0 + k) * COUNTER_STRIDE], s->last_heavy_cap);
+    }
     return RT_OK;
+}
+}  // namespace
+
+extern "C" int rt_live_tiles(const rt_scene* s, int64_t* live, int64_t* total) {
+    return live_tiles(s, live, nullptr, total);
+}
+
+extern "C" int rt_heavy_tiles(const rt_scene* s, int64_t* heavy) {
+    if (!heavy) return set_error(RT_ERR_ARG, "rt_heavy_tiles: null argument");
+    int64_t live = 0, total = 0;
+    *heavy = 0;
+    return live_tiles(s, &live, heavy, &total);
 }
 
 #ifdef RT_STATS

@@ -39,7 +39,7 @@ ds = rt.DeviceScene.from_host(hs)
 opts, _j = ds.make_opts(spp=cfg["spp"], max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"])
 rgb = torch.zeros((H * W * 3,), dtype=torch.float32, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
-res = {k: {"kernel": [], "frame": [], "wall": []} for k in settings}
+res = {k: {"kernel": [], "frame": [], "wall": [], "heavy": []} for k in settings}
 ref = None
 base_env = dict(os.environ)
 for _ in range(a.rounds):
@@ -58,6 +58,7 @@ for _ in range(a.rounds):
         res[name]["wall"].append((time.perf_counter() - t0) / a.reps * 1e3)
         res[name]["kernel"].extend(ds.kernel_times(a.reps))
         res[name]["frame"].extend(ds.frame_times(a.reps))
+        res[name]["heavy"].append(ds.heavy_tiles())
         img = rgb.cpu().numpy()
         if ref is None:
             ref = img
@@ -65,4 +66,5 @@ for _ in range(a.rounds):
 for name, r in res.items():
     print(json.dumps({"config": a.config, "setting": name, "kernel_ms": round(float(np.median(r["kernel"])), 4),
                       "frame_ms": round(float(np.median(r["frame"])), 4),
-                      "wall_ms": round(float(np.median(r["wall"])), 4)}), flush=True)
+                      "wall_ms": round(float(np.median(r["wall"])), 4),
+                      "heavy_tiles": int(np.median(r["heavy"]))}), flush=True)

@@ -47,6 +47,46 @@ for st in glob.glob(os.path.join(a.prof, "trace", "*kernel_stats.csv")):
     os.makedirs(a.out, exist_ok=True)
     Path(a.out, f"{a.config}_kernel_stats.csv").write_text(Path(st).read_text())
 k = summary.get(a.kernel, {})
+
+SIMDS, CUS = 1024, 256  # MI355X: 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
+
+
+def issue(c):
+    """Issue-side fractions of the kernel from one launch's SQ counters (summed over the 8 XCDs
+    by rocprofv3).  cycles = GRBM_GUI_ACTIVE / 8 (per-XCD busy cycles ~ the launch's duration).
+    VALU: a wave64 VALU instruction holds its SIMD 2 cycles at full throughput (MI355X_MICROARCH.md,
+    per-instruction cycle constants: v_fma_f32 wave64 2 cyc), so valu_issue = 2 * SQ_INSTS_VALU /
+    (SIMDs * cycles).  SALU: one scalar instruction per cycle per CU.  The wave-state ratios are
+    SQ_WAIT_ANY, SQ_WAIT_INST_ANY and SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES (same quad-cycle unit);
+    waves_per_simd = 4 * SQ_WAVE_CYCLES / (SIMDs * cycles)."""
+    need = ("GRBM_GUI_ACTIVE", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY")
+    if not all(n in c for n in need):
+        return None
+    cyc = c["GRBM_GUI_ACTIVE"] / 8
+    out = {"cycles_per_xcd": round(cyc),
+           "valu_issue": round(2 * c["SQ_INSTS_VALU"] / (SIMDS * cyc), 4),
+           "salu_issue": round(c["SQ_INSTS_SALU"] / (CUS * cyc), 4),
+           "wait_any": round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4),
+           "waves_per_simd": round(4 * c["SQ_WAVE_CYCLES"] / (SIMDS * cyc), 3)}
+    for n, key in (("SQ_WAIT_INST_ANY", "wait_inst_any"), ("SQ_ACTIVE_INST_ANY", "active_inst_any")):
+        if n in c:
+            out[key] = round(c[n] / c["SQ_WAVE_CYCLES"], 4)
+    if "SQ_INSTS_SMEM" in c:
+        out["smem_per_wave"] = round(c["SQ_INSTS_SMEM"] / c.get("SQ_WAVES", 1), 1)
+    out["counters"] = {n: c[n] for n in sorted(c) if n.startswith(("SQ_", "GRBM_"))}
+    return out
+
+
+def binding(i):
+    """Name the resource that bounds the kernel: the largest of the pipe fractions, or latency
+    when no pipe is near saturation and waves spend most cycles waiting."""
+    pipes = {"VALU issue": i["valu_issue"], "SALU issue": i["salu_issue"]}
+    name, frac = max(pipes.items(), key=lambda kv: kv[1])
+    if frac >= 0.8:
+        return f"{name} ({frac:.2f} of peak)"
+    return (f"latency (dependent scalar node loads in the wave DFS): no pipe saturated "
+            f"(VALU issue {i['valu_issue']:.2f}, SALU {i['salu_issue']:.2f} of peak), waves waiting "
+            f"{i['wait_any']:.2f} of their cycles at {i['waves_per_simd']:.1f} waves/SIMD")
 if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
     fetch = 2 * k["FETCH_SIZE"] * 1024
     write = k["WRITE_SIZE"] * 1024
@@ -56,6 +96,10 @@ if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
                       "fetch_bytes": round(fetch), "write_bytes": round(write),
                       "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
                                 f"{os.path.basename(a.prof.rstrip('/'))}; FETCH_SIZE x2 (gfx950), KiB->B"}
+    iss = issue(k)
+    if iss:
+        data[a.config]["issue"] = iss
+        data[a.config]["binding"] = binding(iss)
     tf.write_text(json.dumps(data, indent=1) + "\n")
     print(json.dumps(data[a.config]))
 for name, cs in summary.items():

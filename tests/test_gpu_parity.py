@@ -109,6 +109,34 @@ def test_c3_full_frame_matches_reference(flags, tiles):
     assert diff.max() <= 1
 
 
+@pytest.mark.parametrize("env", [{}, {"RT_HEAVY_CAP": "8"}, {"RT_HEAVY_FRAC": "0.0001"}])
+def test_heavy_first_dispatch_changes_nothing(env, monkeypatch):
+    """Heavy-first dispatch (the previous frames' per-tile costs order the render blocks; full
+    heavy lists spill into the survivor lists; a tiny threshold makes every tile heavy): frames
+    after the first take the heavy path and still equal the reference's c3 frame, also after
+    the camera moved (stale costs) and back."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    meta = golden_meta("c3_full")
+    hs = host_scene("frog.json")
+    cam = hs.camera(1920, 1080)
+    moved = rt.Camera(tuple(np.add(cam.pos, (0.05, 0.02, 0.0))), cam.look_at, cam.up, cam.focal_length_mm,
+                      cam.sensor_height_mm, 1920, 1080)
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    heavy = []
+    for c in (cam, cam, moved, cam, cam):
+        rgb, hi, ht = ds.render(c, spp=16, max_depth=1, aov=True)
+        heavy.append(ds.heavy_tiles())
+        if c is cam:
+            assert hashlib.sha256(hi.tobytes()).hexdigest() == meta["sha256"]["hits.i32"]
+            assert hashlib.sha256(ht.tobytes()).hexdigest() == meta["sha256"]["hitt.f32"]
+            _check_fb(rgb, golden_array("c3_full", "fb.f32.gz", np.float32))
+    assert heavy[0] == 0 and heavy[1] > 0 and heavy[4] > 0, heavy
+    if "RT_HEAVY_CAP" in env:
+        assert heavy[4] <= 8 * 3 * int(env["RT_HEAVY_CAP"])
+    ds.close()
+
+
 @pytest.mark.parametrize("tiles", [rt.RT_TILES_ROWS, rt.RT_TILES_LINEAR])
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("spp,W,H", [(1, 37, 23), (3, 40, 21), (64, 9, 7), (2, 1, 1), (16, 65, 3)])

@@ -217,11 +217,12 @@ def native(a, hs, cam, cfg, world, rank, local, dev):
     r = make(deliver)
     elapsed, last = timed_native(r, cam, opts, a.steps, a.warmup, a.depth, dev, world)
     sc = r.scene(0)
-    kt, ft = sc.kernel_times(a.steps), sc.frame_times(a.steps)
+    kt, ft, pt = sc.kernel_times(a.steps), sc.frame_times(a.steps), sc.prepass_times(a.steps)
     res = {"elapsed": elapsed,
            "kernel_ms": float(kt.mean()) if len(kt) else float("nan"),
            "frame_ms": float(ft.mean()) if len(ft) else float("nan"),
-           "live_tiles": list(sc.live_tiles())}
+           "prepass_ms": float(pt.mean()) if len(pt) else float("nan"),
+           "live_tiles": list(sc.live_tiles()), "heavy_tiles": sc.heavy_tiles()}
     if rank == 0:
         g, d, f = (r.times(k, a.steps) for k in (rt.RT_TIME_GATHER, rt.RT_TIME_DELIVER, rt.RT_TIME_FRAME))
         res.update(gather_ms=float(g.mean()), deliver_ms=float(d.mean()), frame_latency_ms=float(f.mean()))
@@ -475,6 +476,11 @@ def main():
         op = res["other_payload"]
         extra[f"{op['deliver']}_host_value"] = round(samples * op["steps"] / m[4] / 1e6, 3)
     extra["live_tiles"] = res.get("live_tiles")
+    if "prepass_ms" in res:
+        extra["prepass_ms"] = round(res["prepass_ms"], 4)
+        extra["heavy_tiles"] = res["heavy_tiles"]
+        extra["note"] = ("frame_ms = the frame's device work: cull pre-passes (prep stream, overlapping the "
+                         "previous frame's render kernel) + render kernel; ms_per_step is the delivered rate")
     if shards:
         extra["band_shards_one_gpu"] = shards
     line["timing"] = extra

@@ -384,9 +384,13 @@ int rt_box_test_host(const float* rays, const float* boxes, const float* tminmax
  * rt_render_device calls on this scene, oldest first, measured with HIP events recorded
  * on the launch stream around the kernel.  Waits for those launches to finish. */
 int rt_kernel_times(const rt_scene* s, float* ms_out, int max, int* n_out);
-/* The same for the whole device frame: the root-box cull pass, the tree-cut cull pass (when it
- * runs) and the render kernel. */
+/* The same for the whole device frame: the root-box cull pass and the tree-cut cull pass (when
+ * it runs), timed on the scene's prep stream, plus the render kernel.  (A frame's pre-passes
+ * overlap the previous frame's render kernel, so this is the frame's device work, not the
+ * span from its first launch to its end.) */
 int rt_frame_times(const rt_scene* s, float* ms_out, int max, int* n_out);
+/* The pre-passes alone (root-box cull + tree-cut cull). */
+int rt_prepass_times(const rt_scene* s, float* ms_out, int max, int* n_out);
 /* Pixel tiles of the most recent rt_render_device call that survived the root-box cull, and
  * all tiles (the tree-cut pass may still cull some of the survivors; those are flagged, not
  * removed from the lists).  Waits for that call to finish. */

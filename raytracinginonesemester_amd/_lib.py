@@ -163,6 +163,7 @@ SIGNATURES = {
     "rt_box_test_host": (I, [P, P, P, I, P, P, P]),
     "rt_kernel_times": (I, [P, P, I, P]),
     "rt_frame_times": (I, [P, P, I, P]),
+    "rt_prepass_times": (I, [P, P, I, P]),
     "rt_live_tiles": (I, [P, P, P]),
     "rt_heavy_tiles": (I, [P, P]),
     "rt_device_count": (I, [P]),

@@ -292,10 +292,17 @@ class DeviceScene:
         return n.value
 
     def frame_times(self, max_launches: int = 256) -> np.ndarray:
-        """ms of the whole device frame (list reset, cull pre-pass, render kernel)."""
+        """ms of the frame's device work (cull pre-passes + render kernel)."""
         out = np.zeros(max_launches, np.float32)
         n = C.c_int()
         check(lib().rt_frame_times(self._h, ptr(out), max_launches, C.byref(n)))
+        return out[:n.value]
+
+    def prepass_times(self, max_launches: int = 256) -> np.ndarray:
+        """ms of the cull pre-passes (root-box cull + tree-cut cull) alone."""
+        out = np.zeros(max_launches, np.float32)
+        n = C.c_int()
+        check(lib().rt_prepass_times(self._h, ptr(out), max_launches, C.byref(n)))
         return out[:n.value]
 
     def close(self) -> None:

@@ -25,6 +25,7 @@
 // Pop-time box re-tests are skipped when no lane's bestT changed since the push (the
 // re-test would repeat the push-time computation with the same inputs).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cfloat>
 #include <cmath>
@@ -1963,7 +1964,7 @@ struct rt_scene {
             HIP_TRY(hipEventCreate(&ev0[i]));
             HIP_TRY(hipEventCreate(&evm[i]));
             HIP_TRY(hipEventCreate(&ev1[i]));
-            HIP_TRY(hipEventCreateWithFlags(&pdone[i], hipEventDisableTiming));
+            HIP_TRY(hipEventCreate(&pdone[i]));
         }
         return RT_OK;
     }
@@ -2325,27 +2326,37 @@ int prepare_jitter(rt_scene* s, const rt_render_opts* o) {
 // one per planned virtual block.
 // (A grid sized to the longest list, read back on the host, measured no faster on c3 than the
 // full virtual grid: the empty blocks leave at once.)
+// The render kernel's start / end events (rt_kernel_times) go into its dispatch
+// (hipExtLaunchKernel): no separate event packets on the stream between the frames' kernels.
+struct Launch {
+    hipStream_t st;
+    hipEvent_t start, stop;
+};
+template <typename K>
+void launch_render(K kernel, const dim3& grid, const RenderParams& P, const Launch& L) {
+    hipExtLaunchKernelGGL(kernel, grid, dim3(BLOCK), 0, L.st, L.start, L.stop, 0, P);
+}
+
 template <int MODE, bool SAMPLES>
-void launch_mode(const RenderParams& P, bool big, hipStream_t st) {
+void launch_mode(const RenderParams& P, bool big, const Launch& L) {
     const dim3 grid((P.tiles_virtual + 7) / 8 * 8 + 8 * NCLASS * P.heavy_cap);
     if (P.max_depth == 1) {
         if constexpr (SAMPLES && MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0) {
             if (big) {  // more waves and packed box tests (c5 faster with each; both slower on c3)
-                hipLaunchKernelGGL((render_tiles_kernel<MODE | MODE_PACKED, SAMPLES, true, RT_BIG_WAVES>), grid,
-                                   dim3(BLOCK), 0, st, P);
+                launch_render(render_tiles_kernel<MODE | MODE_PACKED, SAMPLES, true, RT_BIG_WAVES>, grid, P, L);
                 return;
             }
         }
-        hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES, true>), grid, dim3(BLOCK), 0, st, P);
+        launch_render(render_tiles_kernel<MODE, SAMPLES, true>, grid, P, L);
     } else {
-        hipLaunchKernelGGL((render_tiles_kernel<MODE, SAMPLES, false>), grid, dim3(BLOCK), 0, st, P);
+        launch_render(render_tiles_kernel<MODE, SAMPLES, false>, grid, P, L);
     }
 }
 
 template <int MODE>
-void launch(const RenderParams& P, bool samples, bool big, hipStream_t st) {
-    if (samples) launch_mode<MODE, true>(P, big, st);
-    else launch_mode<MODE, false>(P, big, st);
+void launch(const RenderParams& P, bool samples, bool big, const Launch& L) {
+    if (samples) launch_mode<MODE, true>(P, big, L);
+    else launch_mode<MODE, false>(P, big, L);
 }
 
 // Scene data well beyond the eight 4 MB L2s (c5: 345 MB; frog: 6.6 MB): the 7-wave build.
@@ -2521,8 +2532,15 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         for (uint64_t back = 1; back <= 3 && back <= k; ++back) {
             const int f = int((k - back) % rt_scene::kRing);
             if (hipEventQuery(s->ev1[f]) != hipSuccess) continue;
-            float ms = 0.f;
-            if (hipEventElapsedTime(&ms, s->evm[f], s->ev1[f]) == hipSuccess) s->kernel_ms_est = ms;
+            // the render kernel's time, or the frame period when shorter (overlapping frames:
+            // RT_FLAG_OVERLAP starts a kernel while the previous one still runs)
+            float ms = 0.f, period = 0.f;
+            if (hipEventElapsedTime(&ms, s->evm[f], s->ev1[f]) == hipSuccess) {
+                const int f0 = int((k - back - 1) % rt_scene::kRing);
+                if (k - back >= 1 && hipEventElapsedTime(&period, s->ev1[f0], s->ev1[f]) == hipSuccess && period > 0.f)
+                    ms = std::min(ms, period);
+                s->kernel_ms_est = ms;
+            }
             break;
         }
         (void)hipGetLastError();  // a not-ready query is not an error of this call
@@ -2550,9 +2568,6 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         P.tile_cost = static_cast<uint16_t*>(s->cost.p);
     }
     s->last_heavy_cap = P.heavy_cap;
-    if (k > 0 && st != s->last_stream)  // the previous frame of this scene ran elsewhere
-        HIP_TRY(hipStreamWaitEvent(st, ev1_of(k - 1), 0));
-    s->last_stream = st;
     if (s->work.n < work_bytes) {
         if (k > 0) {  // the old buffers may still be read
             HIP_TRY(hipStreamSynchronize(s->prep));
@@ -2575,6 +2590,11 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     for (const auto& a : out_now)
         for (const auto& b : s->prev_out)
             overlap = overlap || (a.lo < a.hi && b.lo < b.hi && a.lo < b.hi && b.lo < a.hi);
+    // the previous frame of this scene ran on another stream: wait for it.  (Letting two frames'
+    // render kernels overlap on two streams, the next filling the CUs the last waves of the
+    // previous one leave idle, measured slower for rt_renderer: 0.257 vs 0.246 ms per c3 frame.)
+    if (k > 0 && st != s->last_stream) HIP_TRY(hipStreamWaitEvent(st, ev1_of(k - 1), 0));
+    s->last_stream = st;
     const int set = int(k % rt_scene::kSets), nset = int((k + 1) % rt_scene::kSets);
     char* base = static_cast<char*>(s->work.p);
     char* lists = base + rt_scene::kSets * kCounterBytes + set * set_bytes;
@@ -2597,25 +2617,28 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             s->counters_dirty = false;
         }
         if (cost_reset) HIP_TRY(hipMemsetAsync(s->cost.p, 0, s->cost.n, pp));  // no heavy tiles yet
-        HIP_TRY(hipEventRecord(s->ev0[slot], pp));
-        hipLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, pp, P);
+        // ev0 / pdone: the pre-passes' start and end, recorded by the dispatches themselves
+        const bool cut = P.cull && P.sc.ncut > 0;
+        hipExtLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, pp,
+                              s->ev0[slot], cut ? nullptr : s->pdone[slot], 0, P);
         HIP_TRY(hipGetLastError());
-        if (P.cull && P.sc.ncut > 0) {
+        if (cut) {
             // 16 waves per CU; each takes (list, group) pairs grid-stride (c3: about one each)
             const int cut_blocks = 4 * s->cus;
-            hipLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, pp, P);
+            hipExtLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, pp, nullptr, s->pdone[slot], 0, P);
             HIP_TRY(hipGetLastError());
         }
-        HIP_TRY(hipEventRecord(s->pdone[slot], pp));
         HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
-        HIP_TRY(hipEventRecord(s->evm[slot], st));
+        const bool sep = std::getenv("RT_EXP_EVENT_RECORD") != nullptr;  // A/B: separate event records
+        if (sep) HIP_TRY(hipEventRecord(s->evm[slot], st));
+        const Launch L{st, sep ? nullptr : s->evm[slot], sep ? nullptr : s->ev1[slot]};
         const bool big = big_scene_waves(s);
-        if (s->deep) launch<MODE_DEEP>(P, samples, false, st);
-        else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, big, st);
-        else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, big, st);
-        else launch<RT_KERNEL_WAVE>(P, samples, big, st);
+        if (s->deep) launch<MODE_DEEP>(P, samples, false, L);
+        else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, big, L);
+        else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, big, L);
+        else launch<RT_KERNEL_WAVE>(P, samples, big, L);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(s->ev1[slot], st));
+        if (sep) HIP_TRY(hipEventRecord(s->ev1[slot], st));
         return RT_OK;
     };
     std::copy(std::begin(out_now), std::end(out_now), std::begin(s->prev_out));
@@ -2638,7 +2661,10 @@ void rt::scene_frame_events(const rt_scene* s, hipEvent_t* first, hipEvent_t* la
 }
 
 namespace {
-int event_times(const rt_scene* s, const hipEvent_t* from, float* ms_out, int max, int* n_out) {
+// what: 0 render kernel (evm -> ev1), 1 pre-passes (ev0 -> pdone), 2 both (the frame's device
+// work: its pre-passes overlap the previous frame's render kernel, so the span ev0 -> ev1 would
+// include the wait for it)
+int event_times(const rt_scene* s, int what, float* ms_out, int max, int* n_out) {
     if (!s || max < 0 || (max > 0 && !ms_out)) return set_error(RT_ERR_ARG, "kernel times: bad args");
     DeviceGuard g(s->device);
     const uint64_t have = std::min<uint64_t>(s->launches, uint64_t(rt_scene::kRing));
@@ -2646,7 +2672,10 @@ int event_times(const rt_scene* s, const hipEvent_t* from, float* ms_out, int ma
     for (int k = 0; k < n; ++k) {  // oldest first among the n most recent
         const int slot = int((s->launches - uint64_t(n) + uint64_t(k)) % rt_scene::kRing);
         HIP_TRY(hipEventSynchronize(s->ev1[slot]));
-        HIP_TRY(hipEventElapsedTime(&ms_out[k], from[slot], s->ev1[slot]));
+        float kern = 0.f, prep = 0.f;
+        if (what != 1) HIP_TRY(hipEventElapsedTime(&kern, s->evm[slot], s->ev1[slot]));
+        if (what != 0) HIP_TRY(hipEventElapsedTime(&prep, s->ev0[slot], s->pdone[slot]));
+        ms_out[k] = kern + prep;
     }
     if (n_out) *n_out = n;
     return RT_OK;
@@ -2714,11 +2743,15 @@ extern "C" int rt_debug_wave_times_set(void* dev_ptr, void* cut_counts_ptr) {
 #endif
 
 extern "C" int rt_kernel_times(const rt_scene* s, float* ms_out, int max, int* n_out) {
-    return event_times(s, s ? s->evm : nullptr, ms_out, max, n_out);
+    return event_times(s, 0, ms_out, max, n_out);
 }
 
 extern "C" int rt_frame_times(const rt_scene* s, float* ms_out, int max, int* n_out) {
-    return event_times(s, s ? s->ev0 : nullptr, ms_out, max, n_out);
+    return event_times(s, 2, ms_out, max, n_out);
+}
+
+extern "C" int rt_prepass_times(const rt_scene* s, float* ms_out, int max, int* n_out) {
+    return event_times(s, 1, ms_out, max, n_out);
 }
 
 extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, float* rgb_host,

@@ -113,6 +113,7 @@ struct RenderParams {
     uint32_t* live_count;                             // [k * COUNTER_STRIDE], tile_cull_kernel
     int32_t* live_tiles;                              // nqueues lists of queue_cap entries
     int32_t* cut_tiles;   // tile_cut_kernel's survivors (not culled, not heavy), per list (sc.ncut > 0)
+    uint8_t* cut_flag;    // per cull-list slot: 1 = culled by tile_cut_kernel (the big-scene kernels' form)
     uint32_t* next_count; // the other counter set, zeroed by tile_cull_kernel for the next frame
     int32_t cut_force;    // test every candidate in tile_cut_kernel (no pass-through)
     int32_t nqueues;
@@ -278,9 +279,13 @@ __device__ __forceinline__ uint64_t box_hit_mask(const RayPre& r, const BoxP& b,
     if (amb == 0) return hit;
     RT_STAT(12, 1);
     // double(tmin), double(FLT_MAX): made here (RT_KF64), not hoisted into spilled VGPR pairs
+#ifndef RT_EXP_NO_KF64
     RT_KF64(tmin_d, (double)kRayTMin)
     RT_KF64(fltmax_d, (double)FLT_MAX)
     const double tmax_d = tmax == FLT_MAX ? fltmax_d : (double)tmax;
+#else
+    const double tmin_d = (double)kRayTMin, tmax_d = (double)tmax;
+#endif
     return hit | (ballot(box_hit_exact(r, b, tmin_d, tmax_d)) & amb);
 }
 
@@ -1239,7 +1244,9 @@ __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
                 }
             }
         }
-        // the rest go to list q's survivor list (the render kernel's normal phase)
+        // the rest go to list q's survivor list (the render kernel's normal phase); the slot flags
+        // serve the big-scene kernels, which read the cull lists
+        if ((int)lane < m) P.cut_flag[slot0 + lane] = (uint8_t)((culled >> lane) & 1ull);
         const bool keep = (int)lane < m && !((culled >> lane) & 1ull) && !heavy;
         const uint64_t km = ballot(keep);
         if (km != 0) {
@@ -1392,7 +1399,11 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, flo
 #ifndef RT_BIG_WAVES
 #define RT_BIG_WAVES 8
 #endif
-template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES>
+// HEAVY: the kernel takes heavy lists and records tile costs (heavy-first dispatch).  The
+// big-scene (MODE_PACKED) kernels leave it out: at 8 waves their SGPRs are all taken by the
+// traversal, and the few extra uniform values spilled into its loops (c5 +14 %); the host
+// enables heavy-first only with kernels that have it (heavy_kernel).
+template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, bool HEAVY = (MODE & MODE_PACKED) == 0>
 __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
     __shared__ int kpix[SAMPLES ? BLOCK : 1];
@@ -1402,10 +1413,21 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
 #endif
     // the wave's start time goes through LDS (an SGPR pair live across the whole tile spilled)
     __shared__ uint32_t t_start[BLOCK / 64], t_tile[BLOCK / 64];
-    if (P.tile_cost && lane_id() == 0) t_start[threadIdx.x / 64] = (uint32_t)wall_clock64();
+    if (HEAVY && P.tile_cost && lane_id() == 0) t_start[threadIdx.x / 64] = (uint32_t)wall_clock64();
     const int b = (int)blockIdx.x;
-    if (b >= P.tiles_virtual + 8 * NCLASS * P.heavy_cap) return;
     int tile = -1;
+    if constexpr (!HEAVY) {
+        // The cull lists with the cut pass's slot flags.  (The register allocation of these
+        // kernels is at its limits: reading the cut pass's survivor lists here instead moved
+        // SGPR spills into the traversal loops, c5 +18 %.)
+        if (b >= P.tiles_virtual) return;
+        const int q = P.nqueues == 1 ? 0 : (b & 7);
+        const int i = P.nqueues == 1 ? b : (b >> 3);
+        tile = planned_tile(P, list_length(P, q), q, i);
+        if (tile < 0) return;
+        if (P.sc.ncut > 0 && P.cut_flag[(size_t)q * P.queue_cap + i]) return;
+    } else {
+    if (b >= P.tiles_virtual + 8 * NCLASS * P.heavy_cap) return;
     // Virtual index i = b >> 3 of list q = b & 7 (the block's XCD).  Heavy phase: the first
     // NCLASS * heavy_cap indices, list q's heavy entries (its classes in order, heaviest first)
     // and then nothing; then the list's slots.  Dispatch is in block order across the XCDs, so
@@ -1439,10 +1461,11 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
             if (tile < 0) return;
         }
     }
-    if (P.tile_cost && lane_id() == 0) t_tile[threadIdx.x / 64] = (uint32_t)tile;
+    }
+    if (HEAVY && P.tile_cost && lane_id() == 0) t_tile[threadIdx.x / 64] = (uint32_t)tile;
     if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col, kpix, park);
     else pixels_tile<MODE, D1>(P, tile, park);
-    if (P.tile_cost && lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
+    if (HEAVY && P.tile_cost && lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
         asm volatile("" ::: "memory");
         const uint32_t d = (uint32_t)wall_clock64() - t_start[threadIdx.x / 64];
         P.tile_cost[4 * (size_t)t_tile[threadIdx.x / 64] + threadIdx.x / 64] = (uint16_t)(d < 0xffffu ? d : 0xffffu);
@@ -2510,7 +2533,11 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // (0: off).
     double heavy_frac = 0.08;
     if (const char* e = std::getenv("RT_HEAVY_FRAC")) heavy_frac = std::atof(e);
-    const bool costs = P.cull && P.sc.ncut > 0 && P.nqueues == 8 && heavy_frac > 0.0;
+    // the kernel launch() will pick: the big-scene build has no heavy-first support
+    const bool big = big_scene_waves(s);
+    const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
+    const bool heavy_kernel = !(big && o->max_depth == 1 && samples && mode != RT_KERNEL_LANE && !s->deep);
+    const bool costs = heavy_kernel && P.cull && P.sc.ncut > 0 && P.nqueues == 8 && heavy_frac > 0.0;
     int heavy_cap = 512;  // RT_HEAVY_CAP: entries per (class, list) (speed experiments)
     if (const char* e = std::getenv("RT_HEAVY_CAP")) heavy_cap = std::max(1, std::atoi(e));
     P.heavy_cap = costs ? std::min(P.queue_cap, heavy_cap) : 0;
@@ -2519,8 +2546,9 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     constexpr size_t kCounterBytes = COUNTER_SET_U32 * sizeof(uint32_t);
     const size_t list_bytes = size_t(P.nqueues) * size_t(P.queue_cap) * sizeof(int32_t);
     const size_t cut_bytes = P.sc.ncut > 0 ? list_bytes : 0;
+    const size_t flag_bytes = P.sc.ncut > 0 ? (size_t(P.nqueues) * size_t(P.queue_cap) + 255) / 256 * 256 : 0;
     const size_t heavy_bytes = size_t(8 * NCLASS) * size_t(P.heavy_cap) * sizeof(int32_t);
-    const size_t set_bytes = list_bytes + cut_bytes + heavy_bytes;
+    const size_t set_bytes = list_bytes + cut_bytes + heavy_bytes + flag_bytes;
     const size_t work_bytes = rt_scene::kSets * (kCounterBytes + set_bytes);
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint64_t k = s->launches;
@@ -2604,7 +2632,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.live_tiles = reinterpret_cast<int32_t*>(lists);
     P.cut_tiles = reinterpret_cast<int32_t*>(lists + list_bytes);
     P.heavy_tiles = reinterpret_cast<int32_t*>(lists + list_bytes + cut_bytes);
-    const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
+    P.cut_flag = reinterpret_cast<uint8_t*>(lists + list_bytes + cut_bytes + heavy_bytes);
     const int slot = int(k % rt_scene::kRing);
     // From the cull launch on, a failure leaves the counter sets unknown (counters_dirty).
     auto frame = [&]() -> int {
@@ -2632,7 +2660,6 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         const bool sep = std::getenv("RT_EXP_EVENT_RECORD") != nullptr;  // A/B: separate event records
         if (sep) HIP_TRY(hipEventRecord(s->evm[slot], st));
         const Launch L{st, sep ? nullptr : s->evm[slot], sep ? nullptr : s->ev1[slot]};
-        const bool big = big_scene_waves(s);
         if (s->deep) launch<MODE_DEEP>(P, samples, false, L);
         else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, big, L);
         else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, big, L);

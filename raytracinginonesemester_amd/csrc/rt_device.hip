@@ -298,6 +298,14 @@ struct HitState {
 #endif
 };
 
+#ifdef RT_EXP_LDS_TOP
+// Experiment (north_star "LDS-staged BVH-node tiles"): the first RT_EXP_LDS_TOP 4-ary records in
+// BFS order of the 4-ary tree (internal refs renumbered so, rt_scene_create) are staged in LDS
+// by every render block and read from there (ds_read_b128 + v_readfirstlane) instead of through
+// the scalar cache.  Measured slower; see DESIGN.md §4.6.
+__shared__ float4 g_lds_top[8 * RT_EXP_LDS_TOP];
+#endif
+
 // ---- WAVE traversal ---------------------------------------------------------------------
 // Every lane of the wave must call this (uniform control flow); `active` selects the
 // lanes that own a ray.  any_hit_dist > 0: shadow query — a lane stops as soon as its
@@ -390,6 +398,18 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
             // load next to its child's test, one load + wait per child).
             const float4* W = sc.wnode + 8 * (size_t)ref;
             vf4 wq[7];
+#ifdef RT_EXP_LDS_TOP
+            if (ref < RT_EXP_LDS_TOP) {
+#pragma unroll
+                for (int k = 0; k < 7; ++k) {
+                    const float4 v = g_lds_top[8 * ref + k];
+                    wq[k] = (vf4){__builtin_bit_cast(float, uni(__float_as_uint(v.x))),
+                                  __builtin_bit_cast(float, uni(__float_as_uint(v.y))),
+                                  __builtin_bit_cast(float, uni(__float_as_uint(v.z))),
+                                  __builtin_bit_cast(float, uni(__float_as_uint(v.w)))};
+                }
+            } else
+#endif
 #pragma unroll
             for (int k = 0; k < 7; ++k) wq[k] = ldc_v(W + k);
             asm volatile("" ::"s"(wq[0]), "s"(wq[1]), "s"(wq[2]), "s"(wq[3]), "s"(wq[4]), "s"(wq[5]), "s"(wq[6]));
@@ -1463,6 +1483,13 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
     }
     }
     if (HEAVY && P.tile_cost && lane_id() == 0) t_tile[threadIdx.x / 64] = (uint32_t)tile;
+#ifdef RT_EXP_LDS_TOP
+    if (P.sc.wide) {  // stage the top records (every block: LDS is per workgroup)
+        const int n = 8 * min(RT_EXP_LDS_TOP, max(P.sc.num_tris - 1, 1));
+        for (int k = (int)threadIdx.x; k < n; k += BLOCK) g_lds_top[k] = P.sc.wnode[k];
+        __syncthreads();
+    }
+#endif
     if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col, kpix, park);
     else pixels_tile<MODE, D1>(P, tile, park);
     if (HEAVY && P.tile_cost && lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
@@ -2098,6 +2125,28 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
         deep = std::max(1, S[0]) > STACK_CAP;
         if (deep || std::max(1, SW[0]) > STACK_CAP) wide_ok = false;
     }
+#ifdef RT_EXP_LDS_TOP
+    // internal refs in BFS order of the 4-ary records (root, its internal entries, theirs...),
+    // then the internal nodes only the binary records reach, so the top records come first
+    if (wide_ok && n_int > 0 && cid[0] != NO_REF && !(cid[0] & LEAF_BIT)) {
+        std::vector<uint32_t> order;
+        std::vector<uint8_t> seen(NN, 0);
+        order.push_back(0);
+        seen[0] = 1;
+        for (size_t h = 0; h < order.size(); ++h) {
+            uint32_t e[4];
+            const int k = wide_entries(nodes[order[h]], e);
+            for (int i = 0; i < k; ++i)
+                if (!(cid[e[i]] & LEAF_BIT) && !seen[e[i]]) {
+                    seen[e[i]] = 1;
+                    order.push_back(e[i]);
+                }
+        }
+        for (size_t n = 0; n < NN; ++n)
+            if (cid[n] != NO_REF && !(cid[n] & LEAF_BIT) && !seen[n]) order.push_back(uint32_t(n));
+        for (size_t i = 0; i < order.size(); ++i) cid[order[i]] = uint32_t(i);
+    }
+#endif
     std::vector<float4> hin(4 * std::max<size_t>(n_int, 1)), hib(2 * std::max<size_t>(n_int, 1));
     std::vector<float4> hwn(wide_ok ? 8 * std::max<size_t>(n_int, 1) : 0);
     std::vector<float4> hlf(4 * std::max<size_t>(n_leaf, 1)), hnm(3 * P);

@@ -374,6 +374,9 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
         }
         if (leaf) {
             RT_STAT(10 + so, 1);
+#ifdef RT_STATS
+            if (sp > 0 && (rdlane(st_ref, sp - 1) & LEAF_BIT)) RT_STAT(18 + so, 1);  // next pop a leaf too
+#endif
             const uint32_t slot = ref & ~LEAF_BIT;
             const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
             float t, u, v;
@@ -1404,7 +1407,9 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, flo
 }
 
 // One virtual block (planned_tile) per workgroup; a block whose slot holds no live tile leaves
-// at once.  (Looping a block over several slots measured no faster on c3 and, by keeping the
+// at once.  (One-wave blocks, each a quarter of a tile, so that a CU takes new work one wave slot
+// at a time: c3 0.286 vs 0.223 ms, c5 93 vs 84 ms — 4x the workgroups, empty ones included, cost
+// more in dispatch than the freer packing gains.)  (Looping a block over several slots measured no faster on c3 and, by keeping the
 // per-sample invariants live across the loop, spilled 224 B instead of 144 B per lane: c5 -6 %
 // without the loop.)
 // WAVES: waves per SIMD the kernel is compiled for.  With the shading spills removed (8 B of

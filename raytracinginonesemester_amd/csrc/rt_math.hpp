@@ -418,8 +418,8 @@ __host__ __device__ __forceinline__ double asd(uint64_t u) { double f; __builtin
     {                                                                                          \
         constexpr uint64_t b_ = __builtin_bit_cast(uint64_t, (double)(val));                   \
         uint32_t lo_, hi_;                                                                     \
-        asm volatile("s_mov_b32 %0, %1" : "=s"(lo_) : "i"((uint32_t)b_));                      \
-        asm volatile("s_mov_b32 %0, %1" : "=s"(hi_) : "i"((uint32_t)(b_ >> 32)));              \
+        asm volatile("s_mov_b32 %0, %1" : "=s"(lo_) : "i"((int32_t)(uint32_t)b_));             \
+        asm volatile("s_mov_b32 %0, %1" : "=s"(hi_) : "i"((int32_t)(uint32_t)(b_ >> 32)));     \
         name = __builtin_bit_cast(double, ((uint64_t)hi_ << 32) | lo_);                        \
     }
 #else

@@ -28,7 +28,7 @@ L.rt_debug_stats(out, 1)
 v = list(out)
 keys = ["trav_p", "trav_s", "pops_p", "pops_s", "popsm_p", "popsm_s", "retest_p", "retest_s", "inner_p",
         "inner_s", "leaf_p", "leaf_s", "ambig", "lanes_p", "lanes_s", "nohit_trav_p", "nohit_pops_p",
-        "rootmiss_trav_p"]
+        "rootmiss_trav_p", "leafnext_p", "leafnext_s"]
 d = dict(zip(keys, v))
 d["per_trav_p"] = {k: round(d[k + "_p"] / max(1, d["trav_p"]), 2) for k in ("pops", "popsm", "retest", "inner", "leaf")}
 d["per_trav_s"] = {k: round(d[k + "_s"] / max(1, d["trav_s"]), 2) for k in ("pops", "popsm", "retest", "inner", "leaf")}

@@ -102,6 +102,14 @@ constexpr int kTimeRing = 256;
 
 // Bands of rank r (b % world == r) in its strip, in band order, go to image rows b*band_rows.
 // The full bands are one strided 2-D copy; a partial last band (H % band_rows) a plain one.
+// (The runtime moves these bytes with blit kernels, __amd_rocclr_copyBuffer, whatever
+// GPU_BLIT_ENGINE_TYPE / HSA_ENABLE_SDMA say.  A 64-wave copy kernel of ours with 16-byte
+// non-temporal stores into the pinned frame made the render kernel beside it far slower:
+// 0.317 vs 0.251 ms per delivered c3 frame.)
+// (The runtime moves these bytes with blit kernels, __amd_rocclr_copyBuffer, whatever
+// GPU_BLIT_ENGINE_TYPE / HSA_ENABLE_SDMA say.  A 64-wave copy kernel of ours with 16-byte
+// non-temporal stores into the pinned frame made the render kernel beside it far slower:
+// 0.317 vs 0.251 ms per delivered c3 frame.)
 hipError_t scatter_strip(char* dst, const char* strip, int r, int world, int H, int band_rows, size_t rb,
                          hipMemcpyKind kind, hipStream_t st) {
     if (world <= 1) return hipMemcpyAsync(dst, strip, size_t(H) * rb, kind, st);

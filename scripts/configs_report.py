@@ -120,7 +120,17 @@ def gpath(cfg, threads, reps, cpu_rows):
            "total_rays_s": samples * (1 + SHADOW_PER_SAMPLE[cfg]) / t,
            "timing": "rt_render_device per frame (scene resident, stream-ordered), mean of reps",
            "ms": t * 1e3, "kernel_ms": float(kt.mean()),
-           "roofline_frac": samples * B / (float(kt.mean()) / 1e3) / 8.0e12}
+           # SURVEY §8(d) reference-layout byte model: what the reference's per-ray traversal
+           # would fetch, NOT this kernel's traffic (that is profiles/traffic.json / bench.py)
+           "reference_equivalent_frac": samples * B / (float(kt.mean()) / 1e3) / 8.0e12}
+    tr = {}
+    try:
+        tr = json.loads((REPO / "profiles" / "traffic.json").read_text()).get(cfg, {})
+    except Exception:
+        pass
+    if tr.get("bytes_per_launch"):
+        out["hbm_frac_measured"] = tr["bytes_per_launch"] / (float(kt.mean()) / 1e3) / 8.0e12
+        out["hbm_bytes_per_launch"] = tr["bytes_per_launch"]
     rgb_h = rgb.cpu().numpy()
     hit_h = hit.cpu().numpy()
     oc = orc.camera_from_basis(*(cam.basis()[k] for k in ("center", "pixel00_loc", "pixel_delta_u",

@@ -81,7 +81,10 @@ def main():
         child(int(sys.argv[2]))
         return
     steps = 200
-    settings = json.loads(sys.argv[1]) if len(sys.argv) > 1 else SETTINGS
+    arg = sys.argv[1] if len(sys.argv) > 1 else None
+    if arg and arg.startswith("@"):
+        arg = Path(arg[1:]).read_text()
+    settings = json.loads(arg) if arg else SETTINGS
     for name, env in settings.items():
         e = dict(os.environ, **env)
         p = subprocess.run([sys.executable, __file__, "--child", str(steps)], env=e, capture_output=True, text=True,

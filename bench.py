@@ -391,7 +391,9 @@ def main():
         except rt.RTError as e:
             if world == 1 or e.code != -8:
                 raise
-            fallback = f"native RCCL failed ({e}); torch.distributed gather used"
+            # the process group is gloo (the native path's control plane): gather over it, CPU-staged
+            a.backend = "gloo"
+            fallback = f"native RCCL failed ({e}); torch.distributed gather (gloo, CPU-staged) used"
             print(f"bench: {fallback}", file=sys.stderr, flush=True)
             comm = "torch"
     if comm == "torch":

@@ -79,14 +79,19 @@ def issue(c):
 
 def binding(i):
     """Name the resource that bounds the kernel: the largest of the pipe fractions, or latency
-    when no pipe is near saturation and waves spend most cycles waiting."""
+    when no pipe is near saturation and waves spend most cycles waiting.  The scalar unit is one
+    per CU at about one instruction per cycle, and v_readlane / v_writelane run at the same
+    per-CU rate (scripts/micro/issue_mix.hip, profiles/r02/issue_mix.jsonl), so the SALU
+    fraction understates the scalar side of a kernel that keeps its stack in VGPR lanes."""
     pipes = {"VALU issue": i["valu_issue"], "SALU issue": i["salu_issue"]}
     name, frac = max(pipes.items(), key=lambda kv: kv[1])
     if frac >= 0.8:
         return f"{name} ({frac:.2f} of peak)"
-    return (f"latency (dependent scalar node loads in the wave DFS): no pipe saturated "
-            f"(VALU issue {i['valu_issue']:.2f}, SALU {i['salu_issue']:.2f} of peak), waves waiting "
-            f"{i['wait_any']:.2f} of their cycles at {i['waves_per_simd']:.1f} waves/SIMD")
+    return (f"latency and scalar issue: the per-wave chain scalar node load -> box tests -> ballot -> "
+            f"push/pop; the busiest pipe is the per-CU scalar unit (SALU {i['salu_issue']:.2f} of its "
+            f"rate before the stack's v_readlane/v_writelane, which share it), VALU issue "
+            f"{i['valu_issue']:.2f}; waves waiting {i['wait_any']:.2f} of their cycles at "
+            f"{i['waves_per_simd']:.1f} waves/SIMD")
 if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
     fetch = 2 * k["FETCH_SIZE"] * 1024
     write = k["WRITE_SIZE"] * 1024

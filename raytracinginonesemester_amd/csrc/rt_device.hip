@@ -141,6 +141,14 @@ __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+// This lane's bit of a wave-uniform mask, the inverse of ballot: one v_cndmask on the SGPR pair
+// (`(m >> lane_id()) & 1` keeps a 64-bit lane bit live across the traversal loop, which the
+// compiler spills to scratch and reloads at every leaf pop).
+__device__ __forceinline__ bool lane_in(uint64_t m) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(r) : "s"(m));
+    return r != 0;
+}
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
@@ -473,8 +481,6 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
 template <bool WIDE>
 __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const RayPre& r, bool active,
                                                    bool any_hit, float any_hit_dist, HitState& hs) {
-    const uint32_t lane = lane_id();
-    const uint64_t lane_bit = 1ull << lane;
     uint64_t alive = ballot(active);
     hs.bestT = FLT_MAX;
     hs.slot = -1;
@@ -497,8 +503,9 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
 #endif
     uint32_t st_ref = 0, st_mlo = 0, st_mhi = 0;  // lane k holds entry k
     // Entries [0, stale) were pushed before the latest bestT change of some lane: they take the
-    // pop-time re-test.  A hit sets stale = sp (every entry then on the stack); a pop at index sp
-    // lowers it to sp, so what is pushed next (at sp and up) is fresh.  The same entries as a
+    // pop-time re-test.  A hit sets stale = sp (every entry then on the stack); a re-tested pop
+    // at index sp lowers it to sp (a pop at or above it leaves it), so what is pushed next, at sp
+    // and up, is fresh.  The same entries as a
     // per-entry version compared with a wave counter, without a fourth stack lane.
     int sp = 0;
     int stale = 0;
@@ -508,8 +515,6 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
     sp = 1;
     while (sp > 0) {
         --sp;
-        const bool retest = sp < stale;
-        stale = min(stale, sp);
         const uint32_t ref = rdlane(st_ref, sp);
         uint64_t mask = ((uint64_t)rdlane(st_mhi, sp) << 32) | rdlane(st_mlo, sp);
         RT_STAT(2 + so, 1);
@@ -529,7 +534,8 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
         if (ref & LEAF_BIT) {
             const uint32_t slot = ref & ~LEAF_BIT;
             const float4* L = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.leaf) + (slot << 6));
-            if (retest) {
+            if (sp < stale) {  // re-test (and lower the watermark to this slot)
+                stale = sp;
                 RT_STAT(6 + so, 1);
                 const float4 c = ldc(L + 2), d = ldc(L + 3);
                 mask = box_hit_mask<false>(r, BoxP{hi2(c), lo2(d), hi2(d)}, hs.bestT, mask);
@@ -539,7 +545,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
 #ifdef RT_STATS
             if (sp > 0 && (rdlane(st_ref, sp - 1) & LEAF_BIT)) RT_STAT(18 + so, 1);  // next pop a leaf too
 #endif
-            const bool act = (mask & lane_bit) != 0;
+            const bool act = lane_in(mask);
             const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
             float t, u, v;
             const bool h = act && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin,
@@ -555,7 +561,8 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
             }
             continue;
         }
-        if (retest) {
+        if (sp < stale) {  // re-test (and lower the watermark to this slot)
+            stale = sp;
             RT_STAT(6 + so, 1);
             const float4* B = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.ibox) + (ref << 5));
             const float4 p = ldc(B), q = ldc(B + 1);

@@ -539,101 +539,103 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                 RT_STAT(6 + so, 1);
                 const float4 c = ldc(L + 2), d = ldc(L + 3);
                 mask = box_hit_mask<false>(r, BoxP{hi2(c), lo2(d), hi2(d)}, hs.bestT, mask);
-                if (mask == 0) continue;
             }
-            RT_STAT(10 + so, 1);
+            if (mask != 0) {
+                RT_STAT(10 + so, 1);
 #ifdef RT_STATS
-            if (sp > 0 && (rdlane(st_ref, sp - 1) & LEAF_BIT)) RT_STAT(18 + so, 1);  // next pop a leaf too
+                if (sp > 0 && (rdlane(st_ref, sp - 1) & LEAF_BIT)) RT_STAT(18 + so, 1);  // next pop a leaf too
 #endif
-            const bool act = lane_in(mask);
-            const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
-            float t, u, v;
-            const bool h = act && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin,
-                                       hs.bestT, t, u, v);
-            if (h) {
-                hs.bestT = t;
-                hs.slot = (int32_t)slot;
+                const bool act = lane_in(mask);
+                const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
+                float t, u, v;
+                const bool h = act && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin,
+                                           hs.bestT, t, u, v);
+                if (h) {
+                    hs.bestT = t;
+                    hs.slot = (int32_t)slot;
+                }
+                const uint64_t hm = ballot(h);
+                if (hm != 0) {
+                    stale = sp;
+                    if (any_hit) alive &= ~ballot(h && t < any_hit_dist);
+                }
             }
-            const uint64_t hm = ballot(h);
-            if (hm != 0) {
+        } else {
+            if (sp < stale) {  // re-test (and lower the watermark to this slot)
                 stale = sp;
-                if (any_hit) alive &= ~ballot(h && t < any_hit_dist);
+                RT_STAT(6 + so, 1);
+                const float4* B = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.ibox) + (ref << 5));
+                const float4 p = ldc(B), q = ldc(B + 1);
+                mask = box_hit_mask<false>(r, BoxP{lo2(p), hi2(p), lo2(q)}, hs.bestT, mask);
             }
-            continue;
-        }
-        if (sp < stale) {  // re-test (and lower the watermark to this slot)
-            stale = sp;
-            RT_STAT(6 + so, 1);
-            const float4* B = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.ibox) + (ref << 5));
-            const float4 p = ldc(B), q = ldc(B + 1);
-            mask = box_hit_mask<false>(r, BoxP{lo2(p), hi2(p), lo2(q)}, hs.bestT, mask);
-            if (mask == 0) continue;
-        }
-        RT_STAT(8 + so, 1);
-        if constexpr (WIDE) {
-            // 4-ary record: up to four entries in push order, each pushed if some lane passes.
-            // The whole record in one round trip: the seven 16-byte scalar loads are issued
-            // together and waited for once (the empty asm keeps the compiler from sinking each
-            // load next to its child's test, one load + wait per child).
-            // 32-bit byte offset (rt_scene_create keeps the 4-ary array under 4 GiB): the scalar
-            // loads take it as their SGPR offset, no 64-bit address arithmetic per pop
-            const float4* W = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.wnode) + (ref << 7));
-            vf4 wq[7];
+            if (mask != 0) {
+                RT_STAT(8 + so, 1);
+                if constexpr (WIDE) {
+                    // 4-ary record: up to four entries in push order, each pushed if some lane passes.
+                    // The whole record in one round trip: the seven 16-byte scalar loads are issued
+                    // together and waited for once (the empty asm keeps the compiler from sinking each
+                    // load next to its child's test, one load + wait per child).
+                    // 32-bit byte offset (rt_scene_create keeps the 4-ary array under 4 GiB): the scalar
+                    // loads take it as their SGPR offset, no 64-bit address arithmetic per pop
+                    const float4* W = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.wnode) + (ref << 7));
+                    vf4 wq[7];
 #ifdef RT_EXP_LDS_TOP
-            if (ref < RT_EXP_LDS_TOP) {
+                    if (ref < RT_EXP_LDS_TOP) {
 #pragma unroll
-                for (int k = 0; k < 7; ++k) {
-                    const float4 v = g_lds_top[8 * ref + k];
-                    wq[k] = (vf4){__builtin_bit_cast(float, uni(__float_as_uint(v.x))),
-                                  __builtin_bit_cast(float, uni(__float_as_uint(v.y))),
-                                  __builtin_bit_cast(float, uni(__float_as_uint(v.z))),
-                                  __builtin_bit_cast(float, uni(__float_as_uint(v.w)))};
-                }
-            } else
+                        for (int k = 0; k < 7; ++k) {
+                            const float4 v = g_lds_top[8 * ref + k];
+                            wq[k] = (vf4){__builtin_bit_cast(float, uni(__float_as_uint(v.x))),
+                                          __builtin_bit_cast(float, uni(__float_as_uint(v.y))),
+                                          __builtin_bit_cast(float, uni(__float_as_uint(v.z))),
+                                          __builtin_bit_cast(float, uni(__float_as_uint(v.w)))};
+                        }
+                    } else
 #endif
 #pragma unroll
-            for (int k = 0; k < 7; ++k) wq[k] = ldc_v(W + k);
-            asm volatile("" ::"s"(wq[0]), "s"(wq[1]), "s"(wq[2]), "s"(wq[3]), "s"(wq[4]), "s"(wq[5]), "s"(wq[6]));
-            const uint32_t refs[4] = {__float_as_uint(wq[6].x), __float_as_uint(wq[6].y), __float_as_uint(wq[6].z),
-                                      __float_as_uint(wq[6].w)};
-            float4 wv[6];
+                    for (int k = 0; k < 7; ++k) wq[k] = ldc_v(W + k);
+                    asm volatile("" ::"s"(wq[0]), "s"(wq[1]), "s"(wq[2]), "s"(wq[3]), "s"(wq[4]), "s"(wq[5]), "s"(wq[6]));
+                    const uint32_t refs[4] = {__float_as_uint(wq[6].x), __float_as_uint(wq[6].y), __float_as_uint(wq[6].z),
+                                              __float_as_uint(wq[6].w)};
+                    float4 wv[6];
 #pragma unroll
-            for (int k = 0; k < 6; ++k) wv[k] = make_float4(wq[k].x, wq[k].y, wq[k].z, wq[k].w);
+                    for (int k = 0; k < 6; ++k) wv[k] = make_float4(wq[k].x, wq[k].y, wq[k].z, wq[k].w);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (refs[k] == NO_REF) continue;
-                const float4 p = wv[(3 * k) / 2], q = wv[(3 * k) / 2 + 1];
-                const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
-                const uint64_t mk_ = box_hit_mask<false>(r, bk, hs.bestT, mask);
-                if (mk_ != 0) {
-                    st_ref = wrlane(refs[k], sp, st_ref);
-                    st_mlo = wrlane((uint32_t)mk_, sp, st_mlo);
-                    st_mhi = wrlane((uint32_t)(mk_ >> 32), sp, st_mhi);
-                    ++sp;
+                    for (int k = 0; k < 4; ++k) {
+                        if (refs[k] == NO_REF) continue;
+                        const float4 p = wv[(3 * k) / 2], q = wv[(3 * k) / 2 + 1];
+                        const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
+                        const uint64_t mk_ = box_hit_mask<false>(r, bk, hs.bestT, mask);
+                        if (mk_ != 0) {
+                            st_ref = wrlane(refs[k], sp, st_ref);
+                            st_mlo = wrlane((uint32_t)mk_, sp, st_mlo);
+                            st_mhi = wrlane((uint32_t)(mk_ >> 32), sp, st_mhi);
+                            ++sp;
+                        }
+                    }
+                } else {
+                    const float4* N = sc.inode + 4 * (size_t)ref;
+                    const float4 q0 = ldc(N), q1 = ldc(N + 1), q2 = ldc(N + 2);
+                    const uint4 q3 = ldc_u(N + 3);
+                    const uint32_t lref = q3.x, rref = q3.y;
+                    if (lref != NO_REF) {
+                        const uint64_t ml = box_hit_mask<false>(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
+                        if (ml != 0) {
+                            st_ref = wrlane(lref, sp, st_ref);
+                            st_mlo = wrlane((uint32_t)ml, sp, st_mlo);
+                            st_mhi = wrlane((uint32_t)(ml >> 32), sp, st_mhi);
+                            ++sp;
+                        }
+                    }
+                    if (rref != NO_REF) {
+                        const uint64_t mr = box_hit_mask<false>(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
+                        if (mr != 0) {
+                            st_ref = wrlane(rref, sp, st_ref);
+                            st_mlo = wrlane((uint32_t)mr, sp, st_mlo);
+                            st_mhi = wrlane((uint32_t)(mr >> 32), sp, st_mhi);
+                            ++sp;
+                        }
+                    }
                 }
-            }
-            continue;
-        }
-        const float4* N = sc.inode + 4 * (size_t)ref;
-        const float4 q0 = ldc(N), q1 = ldc(N + 1), q2 = ldc(N + 2);
-        const uint4 q3 = ldc_u(N + 3);
-        const uint32_t lref = q3.x, rref = q3.y;
-        if (lref != NO_REF) {
-            const uint64_t ml = box_hit_mask<false>(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
-            if (ml != 0) {
-                st_ref = wrlane(lref, sp, st_ref);
-                st_mlo = wrlane((uint32_t)ml, sp, st_mlo);
-                st_mhi = wrlane((uint32_t)(ml >> 32), sp, st_mhi);
-                ++sp;
-            }
-        }
-        if (rref != NO_REF) {
-            const uint64_t mr = box_hit_mask<false>(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
-            if (mr != 0) {
-                st_ref = wrlane(rref, sp, st_ref);
-                st_mlo = wrlane((uint32_t)mr, sp, st_mlo);
-                st_mhi = wrlane((uint32_t)(mr >> 32), sp, st_mhi);
-                ++sp;
             }
         }
     }

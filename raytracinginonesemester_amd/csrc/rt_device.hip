@@ -478,7 +478,7 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
 // records are addressed by 32-bit byte offsets, which the scalar loads take as their SGPR
 // offset.  (A separate function: folding this form into traverse_wave_impl behind
 // `if constexpr` changed the big-scene kernels' register allocation, c5 89.6 vs 85.9 ms.)
-template <bool WIDE>
+template <bool WIDE, bool PK>
 __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const RayPre& r, bool active,
                                                    bool any_hit, float any_hit_dist, HitState& hs) {
     uint64_t alive = ballot(active);
@@ -493,7 +493,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
     RT_STAT(13 + so, __popcll(alive));
     // The root's pop-time test (SearchBVH tests every popped node, query.h:252-254) is made
     // here with the initial bestT, before the loop, so the loop never needs the root box.
-    const uint64_t root_mask = box_hit_mask<false>(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
+    const uint64_t root_mask = box_hit_mask<PK>(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
     if (root_mask == 0) {
         if (!any_hit) RT_STAT(17, 1);
         return;
@@ -538,7 +538,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                 stale = sp;
                 RT_STAT(6 + so, 1);
                 const float4 c = ldc(L + 2), d = ldc(L + 3);
-                mask = box_hit_mask<false>(r, BoxP{hi2(c), lo2(d), hi2(d)}, hs.bestT, mask);
+                mask = box_hit_mask<PK>(r, BoxP{hi2(c), lo2(d), hi2(d)}, hs.bestT, mask);
             }
             if (mask != 0) {
                 RT_STAT(10 + so, 1);
@@ -566,7 +566,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                 RT_STAT(6 + so, 1);
                 const float4* B = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.ibox) + (ref << 5));
                 const float4 p = ldc(B), q = ldc(B + 1);
-                mask = box_hit_mask<false>(r, BoxP{lo2(p), hi2(p), lo2(q)}, hs.bestT, mask);
+                mask = box_hit_mask<PK>(r, BoxP{lo2(p), hi2(p), lo2(q)}, hs.bestT, mask);
             }
             if (mask != 0) {
                 RT_STAT(8 + so, 1);
@@ -604,7 +604,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                         if (refs[k] == NO_REF) continue;
                         const float4 p = wv[(3 * k) / 2], q = wv[(3 * k) / 2 + 1];
                         const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
-                        const uint64_t mk_ = box_hit_mask<false>(r, bk, hs.bestT, mask);
+                        const uint64_t mk_ = box_hit_mask<PK>(r, bk, hs.bestT, mask);
                         if (mk_ != 0) {
                             st_ref = wrlane(refs[k], sp, st_ref);
                             st_mlo = wrlane((uint32_t)mk_, sp, st_mlo);
@@ -618,7 +618,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                     const uint4 q3 = ldc_u(N + 3);
                     const uint32_t lref = q3.x, rref = q3.y;
                     if (lref != NO_REF) {
-                        const uint64_t ml = box_hit_mask<false>(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
+                        const uint64_t ml = box_hit_mask<PK>(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
                         if (ml != 0) {
                             st_ref = wrlane(lref, sp, st_ref);
                             st_mlo = wrlane((uint32_t)ml, sp, st_mlo);
@@ -627,7 +627,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                         }
                     }
                     if (rref != NO_REF) {
-                        const uint64_t mr = box_hit_mask<false>(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
+                        const uint64_t mr = box_hit_mask<PK>(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
                         if (mr != 0) {
                             st_ref = wrlane(rref, sp, st_ref);
                             st_mlo = wrlane((uint32_t)mr, sp, st_mlo);
@@ -756,9 +756,9 @@ __device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, b
                                          float any_hit_dist, HitState& hs) {
     if constexpr ((MODE & MODE_DEEP) != 0) traverse_deep(sc, r, active, any_hit, any_hit_dist, hs);
     else if constexpr (MODE == RT_KERNEL_LANE) traverse_lane(sc, r, active, any_hit, any_hit_dist, hs);
-    else if constexpr ((MODE & MODE_PACKED) != 0)
+    else if constexpr ((MODE & MODE_PACKED) != 0)  // (traverse_wave_split<W, true>: c5 89.3 vs 86.1 ms)
         traverse_wave_impl<(MODE & MODE_WIDE) != 0, true>(sc, r, active, any_hit, any_hit_dist, hs);
-    else traverse_wave_split<(MODE & MODE_WIDE) != 0>(sc, r, active, any_hit, any_hit_dist, hs);
+    else traverse_wave_split<(MODE & MODE_WIDE) != 0, false>(sc, r, active, any_hit, any_hit_dist, hs);
 }
 
 // Triangle index of a hit (the primary-hit AOV): the leaf's, or (DEEP kernels) the triangle a

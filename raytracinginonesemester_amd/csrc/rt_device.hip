@@ -473,14 +473,23 @@ __device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const Ra
 }
 
 // traverse_wave_impl for the 7-wave (unpacked) kernels, c3's: the same tests in the same order,
-// with fewer scalar instructions per pop (the scalar unit, one per CU, is the kernel's busiest
-// pipe: DESIGN.md §4.2): leaf and internal entries part at the pop with their own re-tests, and
-// records are addressed by 32-bit byte offsets, which the scalar loads take as their SGPR
-// offset.  (A separate function: folding this form into traverse_wave_impl behind
-// `if constexpr` changed the big-scene kernels' register allocation, c5 89.6 vs 85.9 ms.)
+// with fewer scalar instructions per entry (the scalar unit, one per CU, and the v_readlane /
+// v_writelane it shares are the kernel's busiest pipe: DESIGN.md §4.2, §5):
+// - the entry in hand: after an internal record, the last entry it would push (the one the
+//   reference pops next) stays in SGPRs and is processed at once, skipping its push and pop.
+//   Nothing runs between its test and its processing, so it needs no re-test;
+// - a stale watermark instead of a per-entry version lane: entries [0, stale) were pushed
+//   before the latest bestT change of some lane and take the pop-time re-test.  A hit sets
+//   stale = sp, and a re-tested pop at index sp lowers it to sp, so stale <= sp and what is
+//   pushed next is fresh;
+// - records addressed by 32-bit byte offsets, which the scalar loads take as their SGPR offset
+//   (rt_scene_create sends larger trees to MODE_DEEP);
+// - the camera ray's query skips the `alive` AND (only a shadow query's lanes leave early).
+// The packed big-scene kernels keep traverse_wave_impl: every one of these forms measured
+// slower there (their SGPRs are all taken).
 template <bool WIDE, bool PK>
 __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const RayPre& r, bool active,
-                                                   bool any_hit, float any_hit_dist, HitState& hs) {
+                                                  bool any_hit, float any_hit_dist, HitState& hs) {
     uint64_t alive = ballot(active);
     hs.bestT = FLT_MAX;
     hs.slot = -1;
@@ -492,59 +501,29 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
     RT_STAT(0 + so, 1);
     RT_STAT(13 + so, __popcll(alive));
     // The root's pop-time test (SearchBVH tests every popped node, query.h:252-254) is made
-    // here with the initial bestT, before the loop, so the loop never needs the root box.
-    const uint64_t root_mask = box_hit_mask<PK>(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
-    if (root_mask == 0) {
+    // here with the initial bestT; the root is then the first entry in hand.
+    uint64_t mask = box_hit_mask<PK>(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
+    if (mask == 0) {
         if (!any_hit) RT_STAT(17, 1);
         return;
     }
-#ifdef RT_EXP_ROOT_ONLY  // timing experiments only (wrong output): stop after the root test
-    return;
-#endif
+    uint32_t ref = sc.root_ref;
     uint32_t st_ref = 0, st_mlo = 0, st_mhi = 0;  // lane k holds entry k
-    // Entries [0, stale) were pushed before the latest bestT change of some lane: they take the
-    // pop-time re-test.  A hit sets stale = sp (every entry then on the stack); a re-tested pop
-    // at index sp lowers it to sp (a pop at or above it leaves it), so what is pushed next, at sp
-    // and up, is fresh.  The same entries as a
-    // per-entry version compared with a wave counter, without a fourth stack lane.
     int sp = 0;
-    int stale = 0;
-    st_ref = wrlane(sc.root_ref, 0, st_ref);
-    st_mlo = wrlane((uint32_t)root_mask, 0, st_mlo);
-    st_mhi = wrlane((uint32_t)(root_mask >> 32), 0, st_mhi);
-    sp = 1;
-    while (sp > 0) {
-        --sp;
-        const uint32_t ref = rdlane(st_ref, sp);
-        uint64_t mask = ((uint64_t)rdlane(st_mhi, sp) << 32) | rdlane(st_mlo, sp);
+    int stale = 0;  // entries [0, stale) take the pop-time re-test
+    while (true) {
         RT_STAT(2 + so, 1);
 #ifdef RT_STATS
         ++hs.pops;
 #endif
-        // Only a shadow query's lanes leave the traversal early (alive shrinks); a camera ray's
-        // entries are pushed with non-empty masks inside the initial alive, so the and and the
-        // empty test are the shadow query's alone (any_hit is a constant at each inlined call).
-        if (any_hit) {
-            mask &= alive;
-            if (mask == 0) continue;
-        }
-        RT_STAT(4 + so, 1);
-        // Leaf and internal entries part at once, each with its own pop-time re-test (a test of
-        // some lane's changed bestT since the push), so no flag of either outlives the branch.
-        if (ref & LEAF_BIT) {
-            const uint32_t slot = ref & ~LEAF_BIT;
-            const float4* L = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.leaf) + (slot << 6));
-            if (sp < stale) {  // re-test (and lower the watermark to this slot)
-                stale = sp;
-                RT_STAT(6 + so, 1);
-                const float4 c = ldc(L + 2), d = ldc(L + 3);
-                mask = box_hit_mask<PK>(r, BoxP{hi2(c), lo2(d), hi2(d)}, hs.bestT, mask);
-            }
-            if (mask != 0) {
+        uint32_t pref = 0;
+        uint64_t pmask = 0;  // the entry to hold next (0: pop)
+        if (mask != 0) {
+            RT_STAT(4 + so, 1);
+            if (ref & LEAF_BIT) {
                 RT_STAT(10 + so, 1);
-#ifdef RT_STATS
-                if (sp > 0 && (rdlane(st_ref, sp - 1) & LEAF_BIT)) RT_STAT(18 + so, 1);  // next pop a leaf too
-#endif
+                const uint32_t slot = ref & ~LEAF_BIT;
+                const float4* L = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.leaf) + (slot << 6));
                 const bool act = lane_in(mask);
                 const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
                 float t, u, v;
@@ -559,43 +538,17 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                     stale = sp;
                     if (any_hit) alive &= ~ballot(h && t < any_hit_dist);
                 }
-            }
-        } else {
-            if (sp < stale) {  // re-test (and lower the watermark to this slot)
-                stale = sp;
-                RT_STAT(6 + so, 1);
-                const float4* B = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.ibox) + (ref << 5));
-                const float4 p = ldc(B), q = ldc(B + 1);
-                mask = box_hit_mask<PK>(r, BoxP{lo2(p), hi2(p), lo2(q)}, hs.bestT, mask);
-            }
-            if (mask != 0) {
+            } else {
                 RT_STAT(8 + so, 1);
                 if constexpr (WIDE) {
-                    // 4-ary record: up to four entries in push order, each pushed if some lane passes.
-                    // The whole record in one round trip: the seven 16-byte scalar loads are issued
-                    // together and waited for once (the empty asm keeps the compiler from sinking each
-                    // load next to its child's test, one load + wait per child).
-                    // 32-bit byte offset (rt_scene_create keeps the 4-ary array under 4 GiB): the scalar
-                    // loads take it as their SGPR offset, no 64-bit address arithmetic per pop
+                    // 4-ary record in one round trip (see traverse_wave_impl), by 32-bit byte offset
                     const float4* W = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.wnode) + (ref << 7));
                     vf4 wq[7];
-#ifdef RT_EXP_LDS_TOP
-                    if (ref < RT_EXP_LDS_TOP) {
-#pragma unroll
-                        for (int k = 0; k < 7; ++k) {
-                            const float4 v = g_lds_top[8 * ref + k];
-                            wq[k] = (vf4){__builtin_bit_cast(float, uni(__float_as_uint(v.x))),
-                                          __builtin_bit_cast(float, uni(__float_as_uint(v.y))),
-                                          __builtin_bit_cast(float, uni(__float_as_uint(v.z))),
-                                          __builtin_bit_cast(float, uni(__float_as_uint(v.w)))};
-                        }
-                    } else
-#endif
 #pragma unroll
                     for (int k = 0; k < 7; ++k) wq[k] = ldc_v(W + k);
                     asm volatile("" ::"s"(wq[0]), "s"(wq[1]), "s"(wq[2]), "s"(wq[3]), "s"(wq[4]), "s"(wq[5]), "s"(wq[6]));
-                    const uint32_t refs[4] = {__float_as_uint(wq[6].x), __float_as_uint(wq[6].y), __float_as_uint(wq[6].z),
-                                              __float_as_uint(wq[6].w)};
+                    const uint32_t refs[4] = {__float_as_uint(wq[6].x), __float_as_uint(wq[6].y),
+                                              __float_as_uint(wq[6].z), __float_as_uint(wq[6].w)};
                     float4 wv[6];
 #pragma unroll
                     for (int k = 0; k < 6; ++k) wv[k] = make_float4(wq[k].x, wq[k].y, wq[k].z, wq[k].w);
@@ -606,10 +559,14 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                         const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
                         const uint64_t mk_ = box_hit_mask<PK>(r, bk, hs.bestT, mask);
                         if (mk_ != 0) {
-                            st_ref = wrlane(refs[k], sp, st_ref);
-                            st_mlo = wrlane((uint32_t)mk_, sp, st_mlo);
-                            st_mhi = wrlane((uint32_t)(mk_ >> 32), sp, st_mhi);
-                            ++sp;
+                            if (pmask != 0) {  // the previous passing entry goes to the stack
+                                st_ref = wrlane(pref, sp, st_ref);
+                                st_mlo = wrlane((uint32_t)pmask, sp, st_mlo);
+                                st_mhi = wrlane((uint32_t)(pmask >> 32), sp, st_mhi);
+                                ++sp;
+                            }
+                            pref = refs[k];
+                            pmask = mk_;
                         }
                     }
                 } else {
@@ -620,27 +577,56 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                     if (lref != NO_REF) {
                         const uint64_t ml = box_hit_mask<PK>(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
                         if (ml != 0) {
-                            st_ref = wrlane(lref, sp, st_ref);
-                            st_mlo = wrlane((uint32_t)ml, sp, st_mlo);
-                            st_mhi = wrlane((uint32_t)(ml >> 32), sp, st_mhi);
-                            ++sp;
+                            pref = lref;
+                            pmask = ml;
                         }
                     }
                     if (rref != NO_REF) {
                         const uint64_t mr = box_hit_mask<PK>(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
                         if (mr != 0) {
-                            st_ref = wrlane(rref, sp, st_ref);
-                            st_mlo = wrlane((uint32_t)mr, sp, st_mlo);
-                            st_mhi = wrlane((uint32_t)(mr >> 32), sp, st_mhi);
-                            ++sp;
+                            if (pmask != 0) {
+                                st_ref = wrlane(pref, sp, st_ref);
+                                st_mlo = wrlane((uint32_t)pmask, sp, st_mlo);
+                                st_mhi = wrlane((uint32_t)(pmask >> 32), sp, st_mhi);
+                                ++sp;
+                            }
+                            pref = rref;
+                            pmask = mr;
                         }
                     }
                 }
             }
         }
+        if (pmask != 0) {  // hold the last pushed entry: the next one the reference pops
+            ref = pref;
+            mask = pmask;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            ref = rdlane(st_ref, sp);
+            mask = ((uint64_t)rdlane(st_mhi, sp) << 32) | rdlane(st_mlo, sp);
+            // only a shadow query's lanes leave early (alive shrinks); any_hit is a constant at
+            // each inlined call
+            if (any_hit) mask &= alive;
+            if (sp < stale) {  // re-test (and lower the watermark to this slot)
+                stale = sp;
+                RT_STAT(6 + so, 1);
+                BoxP ob;
+                if (ref & LEAF_BIT) {
+                    const float4* L = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.leaf) +
+                                                                      ((ref & ~LEAF_BIT) << 6));
+                    const float4 c = ldc(L + 2), d = ldc(L + 3);
+                    ob = BoxP{hi2(c), lo2(d), hi2(d)};
+                } else {
+                    const float4* B = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.ibox) + (ref << 5));
+                    const float4 p = ldc(B), q = ldc(B + 1);
+                    ob = BoxP{lo2(p), hi2(p), lo2(q)};
+                }
+                mask = box_hit_mask<PK>(r, ob, hs.bestT, mask);
+            }
+        }
     }
 }
-
 
 // ---- LANE traversal (private stack per lane; the reference's shape) ---------------------
 __device__ __forceinline__ void traverse_lane(const SceneView& sc, const RayPre& r, bool active,
@@ -756,7 +742,7 @@ __device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, b
                                          float any_hit_dist, HitState& hs) {
     if constexpr ((MODE & MODE_DEEP) != 0) traverse_deep(sc, r, active, any_hit, any_hit_dist, hs);
     else if constexpr (MODE == RT_KERNEL_LANE) traverse_lane(sc, r, active, any_hit, any_hit_dist, hs);
-    else if constexpr ((MODE & MODE_PACKED) != 0)  // (traverse_wave_split<W, true>: c5 89.3 vs 86.1 ms)
+    else if constexpr ((MODE & MODE_PACKED) != 0)
         traverse_wave_impl<(MODE & MODE_WIDE) != 0, true>(sc, r, active, any_hit, any_hit_dist, hs);
     else traverse_wave_split<(MODE & MODE_WIDE) != 0, false>(sc, r, active, any_hit, any_hit_dist, hs);
 }

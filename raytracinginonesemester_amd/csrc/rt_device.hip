@@ -2609,8 +2609,12 @@ void launch(const RenderParams& P, bool samples, bool big, const Launch& L) {
 
 // Scene data well beyond the eight 4 MB L2s (c5: 345 MB; frog: 6.6 MB): the 7-wave build.
 bool big_scene_waves(const rt_scene* s) {
+    // The 8-wave packed kernels were the big-scene choice (c5 85.5 ms vs 88.0 at 7 waves) until
+    // traverse_wave_split: the 7-wave kernels now render c5 in 76.0 ms vs 84.9.  They stay
+    // selectable for A/B (RT_RENDER_WAVES_BIG=1), scene size no longer picks them.
     if (const char* e = std::getenv("RT_RENDER_WAVES_BIG")) return std::atoi(e) != 0;
-    return s->bytes > (size_t(64) << 20);
+    (void)s;
+    return false;
 }
 
 // Host restatement of a pixel whose spp samples all miss the root: each sample is

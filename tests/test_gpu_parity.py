@@ -137,6 +137,21 @@ def test_heavy_first_dispatch_changes_nothing(env, monkeypatch):
     ds.close()
 
 
+def test_packed_big_scene_kernels_match_reference(monkeypatch):
+    """The 8-wave packed-FMA kernels (traverse_wave_impl), no longer picked by scene size but kept
+    for A/B (RT_RENDER_WAVES_BIG=1): the c3 frame still equals the reference's own outputs."""
+    monkeypatch.setenv("RT_RENDER_WAVES_BIG", "1")
+    meta = golden_meta("c3_full")
+    hs = host_scene("frog.json")
+    cam = hs.camera(1920, 1080)
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    rgb, hi, ht = ds.render(cam, spp=16, max_depth=1, aov=True)
+    assert hashlib.sha256(hi.tobytes()).hexdigest() == meta["sha256"]["hits.i32"]
+    assert hashlib.sha256(ht.tobytes()).hexdigest() == meta["sha256"]["hitt.f32"]
+    _check_fb(rgb, golden_array("c3_full", "fb.f32.gz", np.float32))
+    ds.close()
+
+
 @pytest.mark.parametrize("tiles", [rt.RT_TILES_ROWS, rt.RT_TILES_LINEAR])
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("spp,W,H", [(1, 37, 23), (3, 40, 21), (64, 9, 7), (2, 1, 1), (16, 65, 3)])

@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import argparse
 import gzip
+import hashlib
 import json
 import os
 import platform
@@ -358,6 +359,21 @@ def load_traffic(path: Path, config: str):
         return None
 
 
+def primary_hit_parity(ds, cam, cfg, hs) -> dict:
+    """Primary-hit AOVs of one c3 frame (triangle index and t per sample) against the reference's
+    own full-size outputs (sha256 in tests/golden/scenes/c3_full/meta.json): equal hashes mean
+    0 index mismatches."""
+    meta = json.loads((REPO / "tests" / "golden" / "scenes" / "c3_full" / "meta.json").read_text())
+    _, hi, ht = ds.render(cam, spp=cfg["spp"], max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
+                          aov=True)
+    idx_ok = hashlib.sha256(hi.tobytes()).hexdigest() == meta["sha256"]["hits.i32"]
+    t_ok = hashlib.sha256(ht.tobytes()).hexdigest() == meta["sha256"]["hitt.f32"]
+    return {"vs": "reference hits.i32 / hitt.f32 sha256 (tests/golden/scenes/c3_full)",
+            "hit_index_sha256_equal": idx_ok, "hit_t_sha256_equal": t_ok,
+            "hit_index_mismatches": 0 if idx_ok else "unknown (hash differs)",
+            "samples_hit": int((hi >= 0).sum())}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -469,6 +485,20 @@ def main():
         roof["issue"] = tr["issue"]
         roof["binding"] = tr.get("binding")
     line["roofline"] = roof
+    if not a.no_extras:
+        # total rays/s: the frame's camera + shadow (+ bounce) rays, counted on
+        # the device by rt_count_rays outside the timed region, over the same wall time
+        ds = rt.DeviceScene.from_host(hs, device=local)
+        try:
+            rays = ds.count_rays(cam, spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"])
+            if a.config == "c3" and not a.no_parity:
+                line["parity_primary_hits"] = primary_hit_parity(ds, cam, cfg, hs)
+        finally:
+            ds.close()
+        total = rays["camera"] + rays["shadow"] + rays["bounce"]
+        line["rays_per_frame"] = rays
+        line["total_rays_per_s"] = round(total * a.steps / elapsed / 1e6, 3)
+        line["total_rays_unit"] = "Mrays/s (camera + shadow + bounce rays)"
     extra = {"kernel_ms": round(kernel_ms, 4), "frame_ms": round(frame_ms, 4)}
     for k in ("gather_ms", "deliver_ms", "frame_latency_ms"):
         if k in res:

@@ -245,6 +245,14 @@ int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_render_opts*
 int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt,
               float* rgb_host, int32_t* hit_idx_host, float* hit_t_host);
 
+/* Rays one frame of rt_render traces, in the oracle's classes: counts[0] camera rays
+ * (W*rows*spp when max_depth > 0), counts[1] shadow rays (IsInShadow calls that cast a ray,
+ * shader.h:44-62 behind ShadeDirect's NdotL > 0, shader.h:87-93), counts[2] bounce rays
+ * (TraceRayIterative depths > 0, query.h:156-220).  Renders the frame once more with counting
+ * kernels (not the timed ones) and discards it; synchronous.  For total rays/s
+ * (SURVEY.md §8(d)). */
+int rt_count_rays(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt, uint64_t counts[3]);
+
 /* The reference signature verbatim (query.h:13-29) over host arrays: uploads to device 0,
  * renders on the GPU, writes W*H Vec3 to `output` (host).  Synchronous. */
 int rt_render_reference(size_t num_triangles, int W, int H, const rt_camera* cam, rt_vec3 miss_color,

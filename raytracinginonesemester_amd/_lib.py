@@ -143,6 +143,7 @@ SIGNATURES = {
     "rt_render_device": (I, [P, P, P, P, P, P, P]),
     "rt_render_device_p6": (I, [P, P, P, P, P, P, P, P]),
     "rt_render": (I, [P, P, P, P, P, P]),
+    "rt_count_rays": (I, [P, P, P, P]),
     "rt_render_reference": (I, [SZ, I, I, P, Vec3, I, I, P, P, P, P, P, I, P, I, I, P]),
     "rt_render_reference_gpus": (I, [SZ, I, I, P, Vec3, I, I, P, P, P, P, P, I, P, I, I, I, P]),
     "rt_renderer_opts_default": (None, [P]),

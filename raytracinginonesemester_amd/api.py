@@ -265,6 +265,16 @@ class DeviceScene:
         check(lib().rt_render(self._h, C.byref(camera.c), C.byref(o), ptr(rgb), ptr(hi), ptr(ht)))
         return (rgb, hi, ht) if aov else rgb
 
+    def count_rays(self, camera: Camera, spp: int = 1, max_depth: int = 1, diffuse_bounce: bool = True,
+                   miss_color=(0, 0, 0), band_rows: int = 8, band_index: int = 0, band_count: int = 1) -> dict:
+        """Rays one frame traces (rt_count_rays): camera, shadow and bounce counts, the classes of
+        the oracle's stats["rays"]."""
+        o, _jit = self.make_opts(spp, max_depth, diffuse_bounce, miss_color, None, band_rows, band_index,
+                                 band_count)
+        out = (C.c_uint64 * 3)()
+        check(lib().rt_count_rays(self._h, C.byref(camera.c), C.byref(o), out))
+        return {"camera": int(out[0]), "shadow": int(out[1]), "bounce": int(out[2])}
+
     def render_device(self, camera: Camera, opts, rgb_dev_ptr: int, hit_idx_ptr=None, hit_t_ptr=None,
                       stream: Optional[int] = None, p6_dev_ptr=None) -> None:
         """Render into device memory (rt_render_device); with ``p6_dev_ptr`` the render and cull

@@ -134,6 +134,10 @@ struct RenderParams {
     int32_t* heavy_tiles;
     int32_t heavy_cap;
     uint32_t heavy_ticks[4];  // NCLASS thresholds, descending
+    // rt_count_rays only (LANE and DEEP kernels; null otherwise): [1] shadow rays cast, [2]
+    // bounce rays traced, the classes of the oracle's orc_stats.rays ([0], camera rays, is
+    // W*H*spp by definition and counted on the host)
+    unsigned long long* ray_count;
 };
 
 // ---- wave primitives ------------------------------------------------------------------
@@ -295,6 +299,19 @@ __device__ __forceinline__ uint64_t box_hit_mask(const RayPre& r, const BoxP& b,
     const double tmin_d = (double)kRayTMin, tmax_d = (double)tmax;
 #endif
     return hit | (ballot(box_hit_exact(r, b, tmin_d, tmax_d)) & amb);
+}
+
+// rt_count_rays: one wave-aggregated add of the lanes where `c` holds into ray class `cls`.
+// Compiled into the LANE and DEEP kernels only (the WAVE kernels' code is unchanged); every
+// lane of the wave calls it (converged control flow).
+template <int MODE>
+__device__ __forceinline__ void count_rays(unsigned long long* rc, int cls, bool c) {
+    if constexpr (MODE == RT_KERNEL_LANE || (MODE & MODE_DEEP) != 0) {
+        if (rc != nullptr) {
+            const uint64_t b = ballot(c);
+            if (lane_id() == 0 && b != 0) atomicAdd(rc + cls, (unsigned long long)__popcll(b));
+        }
+    }
 }
 
 // Result of one closest-hit query.
@@ -917,6 +934,7 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, con
         pk.put(10, __int_as_float((valid ? 1 : 0) | (hit ? 2 : 0) | (lit ? 4 : 0)));
         Park::fence();
         HitState shs;
+        count_rays<MODE>(P.ray_count, 1, need);
         traverse<MODE>(sc, sray, need, true, dist, shs);
         const bool occluded = need && shs.slot >= 0 && shs.bestT < dist;
         Park::fence();
@@ -974,6 +992,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
     for (int depth = 0; depth < max_depth; ++depth) {
         if (ballot(alive) == 0) break;
         HitState hs;
+        if (depth > 0) count_rays<MODE>(P.ray_count, 2, alive);
         traverse<MODE>(sc, ray, alive, false, 0.0f, hs);
         const bool hit = alive && hs.slot >= 0;
         SurfHit sh;
@@ -1026,6 +1045,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
                 }
             }
             HitState shs;
+            count_rays<MODE>(P.ray_count, 1, need);
             traverse<MODE>(sc, sray, need, true, dist, shs);
             const bool occluded = need && shs.slot >= 0 && shs.bestT < dist;
             if (lit && !occluded) Lo = add(Lo, contrib);
@@ -2665,6 +2685,9 @@ double root_box_coverage(const float* rb, const rt_camera* cam) {
 }
 }  // namespace
 
+// Set by rt_count_rays around its one render (the calling thread's frame only).
+thread_local unsigned long long* t_ray_count = nullptr;
+
 extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, float* rgb,
                                 int32_t* hit_idx, float* hit_t, void* stream) {
     return rt_render_device_p6(s, cam, o, rgb, hit_idx, hit_t, nullptr, stream);
@@ -2727,6 +2750,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.hit_idx = hit_idx;
     P.hit_t = hit_t;
     P.p6 = p6;
+    P.ray_count = t_ray_count;
     {
         const f3 mp = miss_pixel_value(o);
         P.miss_p6[0] = rtp::p6_default_sample(mp.x);
@@ -3035,6 +3059,39 @@ extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts
         HIP_TRY(hipMemcpy(hit_idx_host, hi.p, npx * size_t(o->spp) * sizeof(int32_t), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(hit_t_host, ht.p, npx * size_t(o->spp) * sizeof(float), hipMemcpyDeviceToHost));
     }
+    return RT_OK;
+}
+
+// Rays one frame traces, by the oracle's classes (orc_stats.rays: camera, shadow, bounce).
+// Camera rays are W*rows*spp whenever max_depth > 0 (TraceRayIterative traces every sample);
+// shadow and bounce rays are counted on the device by one LANE-kernel render of the frame
+// (wave-aggregated atomics; the frame itself is discarded).  Synchronous.
+extern "C" int rt_count_rays(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, uint64_t* counts) {
+    if (!s || !cam || !o || !counts) return set_error(RT_ERR_ARG, "rt_count_rays: null argument");
+    const int rows = rt_shard_rows(cam->pixel_height, o->band_rows, o->band_index, o->band_count);
+    if (rows < 0) return set_error(RT_ERR_ARG, "bad band sharding parameters");
+    if (o->spp < 1) return set_error(RT_ERR_ARG, "spp must be >= 1");
+    if (cam->pixel_width < 1 || cam->pixel_height < 1) return set_error(RT_ERR_ARG, "camera has no pixels");
+    DeviceGuard g(s->device);
+    const size_t npx = size_t(rows) * size_t(cam->pixel_width);
+    DevBuf rgb, cnt;
+    int rc;
+    if ((rc = rgb.alloc(std::max<size_t>(npx * 3 * sizeof(float), 4))) != RT_OK) return rc;
+    if ((rc = cnt.alloc(3 * sizeof(unsigned long long))) != RT_OK) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemset(cnt.p, 0, 3 * sizeof(unsigned long long)));
+    rt_render_opts lo = *o;
+    lo.kernel = RT_KERNEL_LANE;  // deep trees take the DEEP kernels, which count too
+    t_ray_count = static_cast<unsigned long long*>(cnt.p);
+    rc = rt_render_device(s, cam, &lo, static_cast<float*>(rgb.p), nullptr, nullptr, nullptr);
+    t_ray_count = nullptr;
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long h[3] = {0, 0, 0};
+    HIP_TRY(hipMemcpy(h, cnt.p, sizeof(h), hipMemcpyDeviceToHost));
+    counts[0] = o->max_depth > 0 ? uint64_t(npx) * uint64_t(o->spp) : 0;
+    counts[1] = h[1];
+    counts[2] = h[2];
     return RT_OK;
 }
 

@@ -105,6 +105,27 @@ def test_device_deep_tree_matches_reference(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_device_deep_tree_ray_counts_match_oracle(name):
+    """rt_count_rays through the DEEP kernels (overflowing chains included) against the oracle's
+    counters."""
+    import raytracinginonesemester_amd as rt
+
+    c = chain(name)
+    m = c["meta"]
+    ds = rt.DeviceScene(c["P"], c["nodes"], c["aabbs"], c["tris"], c["objids"], c["mats"], c["lights"])
+    try:
+        got = ds.count_rays(_camera(c), spp=c["spp"], max_depth=c["depth"])
+    finally:
+        ds.close()
+    cam = orc.camera_from_basis(hexv(m["center"]), hexv(m["pixel00_loc"]), hexv(m["pixel_delta_u"]),
+                                hexv(m["pixel_delta_v"]), c["W"], c["H"])
+    _, st = orc.render_g(c["P"], cam, c["nodes"], c["aabbs"], c["tris"], c["objids"], c["mats"], c["lights"],
+                         spp=c["spp"], max_depth=c["depth"], stats=True)
+    assert [got["camera"], got["shadow"], got["bounce"]] == list(st["rays"])
+
+
+@pytest.mark.gpu
 def test_reference_signature_deep_tree():
     """The drop-in entry point (query.h:13-29) accepts the deep tree the reference accepts."""
     import raytracinginonesemester_amd as rt

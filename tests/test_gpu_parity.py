@@ -70,6 +70,47 @@ def test_golden_scene_parity(name, kernel, flags):
     _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
 
 
+@pytest.mark.parametrize("name", ["c3_small", "frog_bounce", "sphere_single", "cornell"])
+def test_ray_counts_match_oracle(name):
+    """rt_count_rays (total rays/s): camera, shadow and bounce rays of a frame
+    equal the oracle's counters (orc_stats.rays; shadow = IsInShadow calls that cast a ray,
+    shader.h:44-62; bounce = TraceRayIterative depths > 0, query.h:156-220)."""
+    meta = golden_meta(name)
+    scene = G_SCENES[name]
+    hs = host_scene(scene)
+    cam = hs.camera(meta["width"], meta["height"])
+    kw = dict(spp=meta["spp"], max_depth=meta["max_depth"], diffuse_bounce=bool(meta["diffuse_bounce"]),
+              miss_color=hexv(meta["miss_color"]))
+    got = _device_scene(scene).count_rays(cam, **kw)
+    _, st = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,
+                         hs.tri_object_ids, hs.materials, hs.lights, spp=kw["spp"], max_depth=kw["max_depth"],
+                         diffuse_bounce=kw["diffuse_bounce"], miss=tuple(kw["miss_color"]), stats=True)
+    assert [got["camera"], got["shadow"], got["bounce"]] == list(st["rays"])
+    assert got["shadow"] + got["bounce"] > 0  # cornell's light casts no shadow ray; its bounces count
+    if meta["max_depth"] > 1:
+        assert got["bounce"] > 0
+
+
+def test_ray_counts_c3_full_frame():
+    """c3's full frame: 33,177,600 camera rays and 687,530 shadow rays, the oracle's count (whose
+    frame is the reference's bit for bit; SURVEY.md §8(d) quotes 687,822 from its survey-time
+    restatement); band shards sum to the same counts."""
+    cfg = configs.G_CONFIGS["c3"]
+    hs = host_scene(cfg["scene"])
+    cam = hs.camera(cfg["width"], cfg["height"])
+    ds = _device_scene(cfg["scene"])
+    got = ds.count_rays(cam, spp=cfg["spp"], max_depth=cfg["max_depth"])
+    _, st = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,
+                         hs.tri_object_ids, hs.materials, hs.lights, spp=cfg["spp"], max_depth=cfg["max_depth"],
+                         stats=True)
+    assert [got["camera"], got["shadow"], got["bounce"]] == list(st["rays"])
+    assert got == {"camera": 33_177_600, "shadow": 687_530, "bounce": 0}
+    parts = [ds.count_rays(cam, spp=cfg["spp"], max_depth=cfg["max_depth"], band_index=b, band_count=4)
+             for b in range(4)]
+    assert sum(q["shadow"] for q in parts) == got["shadow"]
+    assert sum(q["camera"] for q in parts) == got["camera"]
+
+
 @pytest.mark.parametrize("name", ["c3_small", "c5_small", "frog_bounce"])
 def test_big_scene_kernel_build_parity(name, monkeypatch):
     """The 7-wave build of the depth-1 sample kernels (picked for scenes far beyond the L2s)

@@ -106,6 +106,7 @@ struct RenderParams {
     int32_t band_rows, band_index, band_count, rows;  // rows = local rows rendered
     int32_t tile_w, tile_h, tiles_x, tiles_total;     // pixel tile per block
     int32_t lane_samples;                             // 1: one sample per lane; else pixel loop
+    int32_t half_waves;                               // samples kernel: lanes 32-63 of each wave idle
     int32_t tile_order;                               // RT_TILES_*
     int32_t spp_log2, tile_w_log2;                    // samples kernel: both powers of two
     int32_t cull;                                     // tile culling against the root box
@@ -1490,9 +1491,14 @@ __device__ __forceinline__ int planned_tile(const RenderParams& P, int len, int 
 template <int MODE, bool D1>
 __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, float* col, int* kpix, float* park) {
     const int t = (int)threadIdx.x;
+    // half_waves (band shards of a multi-GPU frame, spp <= 32): each wave traces 32 samples in
+    // its low lanes, so a tile's longest wave, which bounds a short kernel, has half the rays'
+    // path union; lt is the sample's index in the (half-size) tile
+    const bool on = !P.half_waves || (t & 32) == 0;
+    const int lt = P.half_waves ? (((t >> 6) << 5) | (t & 31)) : t;
     {
-        const int s = t & (P.spp - 1);  // spp and tile_w are powers of two here
-        const int pit = t >> P.spp_log2;
+        const int s = lt & (P.spp - 1);  // spp and tile_w are powers of two here
+        const int pit = lt >> P.spp_log2;
         const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
 #ifndef RT_ROW_PIXELS
         // Pixels in Z order inside a square tile (a wave's pixels form a square: 2x2 at 16 spp,
@@ -1511,7 +1517,7 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
 #endif
         const int x = tx * P.tile_w + px;
         const int r = ty * P.tile_h + py;
-        const bool valid = x < P.W && r < P.rows;
+        const bool valid = on && x < P.W && r < P.rows;
         const int y = valid ? global_row(P, r) : 0;
         const int pix = valid ? r * P.W + x : -1;
         // The pixel's index goes through LDS (read back below), so the compiler does not keep
@@ -2759,7 +2765,16 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         P.miss_p6[3] = 0;
     }
     const bool samples = o->kernel != RT_KERNEL_WAVE_PIXELS && o->spp <= BLOCK && (o->spp & (o->spp - 1)) == 0;
-    int ppb = samples ? BLOCK / o->spp : BLOCK;  // pixels per block
+    // Half waves (32 samples per wave) for the shards of an 8-way split: a shard's kernel is then
+    // bound by its longest waves, and halving their rays shortens them (c3 band shards on one
+    // GPU, max over the 8: kernel 0.101 -> 0.095 ms, frame 0.122 -> 0.116; at 4 and fewer shards
+    // the doubled wave count costs more: N = 4 0.106 -> 0.116, N = 1 0.211 -> 0.373;
+    // scripts/half_waves_ab.py).  RT_HALF_WAVES=0/1 overrides.
+    bool half = o->band_count >= 8;
+    if (const char* e = std::getenv("RT_HALF_WAVES")) half = std::atoi(e) != 0;
+    half = half && samples && o->spp <= 32;
+    P.half_waves = half ? 1 : 0;
+    int ppb = samples ? (half ? BLOCK / 2 : BLOCK) / o->spp : BLOCK;  // pixels per block
     int tw = 1;
     while (tw * tw < ppb) tw <<= 1;                // square-ish power-of-two tile
     int th = ppb / tw;

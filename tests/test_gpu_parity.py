@@ -111,6 +111,24 @@ def test_ray_counts_c3_full_frame():
     assert sum(q["camera"] for q in parts) == got["camera"]
 
 
+@pytest.mark.parametrize("name", ["c3_small", "frog_bounce", "cornell", "c5_small"])
+def test_half_waves_parity(name, monkeypatch):
+    """Half waves (32 samples per wave, the default for 8-way band shards) forced on whole
+    frames: the reference's outputs bit for bit, AOVs included."""
+    monkeypatch.setenv("RT_HALF_WAVES", "1")
+    meta = golden_meta(name)
+    scene = G_SCENES[name]
+    hs = host_scene(scene)
+    cam = hs.camera(meta["width"], meta["height"])
+    rgb, hi, ht = _device_scene(scene).render(cam, spp=meta["spp"], max_depth=meta["max_depth"],
+                                              diffuse_bounce=bool(meta["diffuse_bounce"]),
+                                              miss_color=hexv(meta["miss_color"]), aov=True)
+    assert np.array_equal(hi.reshape(-1), golden_array(name, "hits.i32.gz", np.int32))
+    assert np.array_equal(ht.reshape(-1).view(np.uint32),
+                          golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
+    _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
+
+
 @pytest.mark.parametrize("name", ["c3_small", "c5_small", "frog_bounce"])
 def test_big_scene_kernel_build_parity(name, monkeypatch):
     """The 7-wave build of the depth-1 sample kernels (picked for scenes far beyond the L2s)

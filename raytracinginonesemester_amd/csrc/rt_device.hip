@@ -106,7 +106,7 @@ struct RenderParams {
     int32_t band_rows, band_index, band_count, rows;  // rows = local rows rendered
     int32_t tile_w, tile_h, tiles_x, tiles_total;     // pixel tile per block
     int32_t lane_samples;                             // 1: one sample per lane; else pixel loop
-    int32_t half_waves;                               // samples kernel: lanes 32-63 of each wave idle
+    int32_t half_waves;                               // samples kernel: lanes >= 64 >> half_waves idle
     int32_t tile_order;                               // RT_TILES_*
     int32_t spp_log2, tile_w_log2;                    // samples kernel: both powers of two
     int32_t cull;                                     // tile culling against the root box
@@ -1494,8 +1494,9 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
     // half_waves (band shards of a multi-GPU frame, spp <= 32): each wave traces 32 samples in
     // its low lanes, so a tile's longest wave, which bounds a short kernel, has half the rays'
     // path union; lt is the sample's index in the (half-size) tile
-    const bool on = !P.half_waves || (t & 32) == 0;
-    const int lt = P.half_waves ? (((t >> 6) << 5) | (t & 31)) : t;
+    const int wl = 64 >> P.half_waves;  // lanes that trace (64, 32 or 16)
+    const bool on = (t & 63) < wl;
+    const int lt = ((t >> 6) * wl) | (t & (wl - 1));
     {
         const int s = lt & (P.spp - 1);  // spp and tile_w are powers of two here
         const int pit = lt >> P.spp_log2;
@@ -2770,11 +2771,12 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // GPU, max over the 8: kernel 0.101 -> 0.095 ms, frame 0.122 -> 0.116; at 4 and fewer shards
     // the doubled wave count costs more: N = 4 0.106 -> 0.116, N = 1 0.211 -> 0.373;
     // scripts/half_waves_ab.py).  RT_HALF_WAVES=0/1 overrides.
-    bool half = o->band_count >= 8;
-    if (const char* e = std::getenv("RT_HALF_WAVES")) half = std::atoi(e) != 0;
-    half = half && samples && o->spp <= 32;
-    P.half_waves = half ? 1 : 0;
-    int ppb = samples ? (half ? BLOCK / 2 : BLOCK) / o->spp : BLOCK;  // pixels per block
+    // (RT_HALF_WAVES=2: 16 samples per wave, experiments.)
+    int half = o->band_count >= 8 ? 1 : 0;
+    if (const char* e = std::getenv("RT_HALF_WAVES")) half = std::clamp(std::atoi(e), 0, 2);
+    if (!samples || o->spp > (64 >> half)) half = 0;
+    P.half_waves = half;
+    int ppb = samples ? (BLOCK >> half) / o->spp : BLOCK;  // pixels per block
     int tw = 1;
     while (tw * tw < ppb) tw <<= 1;                // square-ish power-of-two tile
     int th = ppb / tw;

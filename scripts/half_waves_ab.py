@@ -25,6 +25,7 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--counts", default="1,2,4,8")
+ap.add_argument("--settings", default="0,1")
 a = ap.parse_args()
 
 cfg = configs.G_CONFIGS[a.config]
@@ -38,11 +39,12 @@ p6 = torch.zeros((H * W * 3,), dtype=torch.uint8, device=dev)
 rgb = torch.zeros((H * W * 3,), dtype=torch.float32, device=dev)
 res = {}
 for n in [int(x) for x in a.counts.split(",")]:
-    acc = {h: [[] for _ in range(n)] for h in ("0", "1")}
-    facc = {h: [[] for _ in range(n)] for h in ("0", "1")}
+    S = a.settings.split(",")
+    acc = {h: [[] for _ in range(n)] for h in S}
+    facc = {h: [[] for _ in range(n)] for h in S}
     outs = {}
     for _ in range(a.rounds):
-        for h in ("0", "1"):
+        for h in S:
             os.environ["RT_HALF_WAVES"] = h
             for r in range(n):
                 o, _j = ds.make_opts(spp=cfg["spp"], max_depth=cfg["max_depth"],
@@ -59,7 +61,7 @@ for n in [int(x) for x in a.counts.split(",")]:
                 else:
                     outs[r] = got
     line = {"N": n}
-    for h in ("0", "1"):
+    for h in S:
         k = [float(np.median(v)) for v in acc[h]]
         f = [float(np.median(v)) for v in facc[h]]
         line[f"half{h}"] = {"kernel_max": round(max(k), 4), "kernel_mean": round(sum(k) / n, 4),

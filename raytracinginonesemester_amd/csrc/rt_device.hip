@@ -1488,13 +1488,14 @@ __device__ __forceinline__ int planned_tile(const RenderParams& P, int len, int 
 
 // One sample per lane: a block covers a tile_w x tile_h pixel tile x spp samples (spp a power
 // of two <= 256, tile_w*tile_h*spp == BLOCK); per-pixel sums run in sample order from LDS.
-template <int MODE, bool D1>
+template <int MODE, bool D1, int LS = 0>
 __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, float* col, int* kpix, float* park) {
     const int t = (int)threadIdx.x;
-    // half_waves (band shards of a multi-GPU frame, spp <= 32): each wave traces 32 samples in
-    // its low lanes, so a tile's longest wave, which bounds a short kernel, has half the rays'
-    // path union; lt is the sample's index in the (half-size) tile
-    const int wl = 64 >> P.half_waves;  // lanes that trace (64, 32 or 16)
+    // LS = 1, half waves (band shards of a multi-GPU frame, spp <= 32): each wave traces 32
+    // samples in its low lanes, so a tile's longest wave, which bounds a short kernel, has half
+    // the rays' path union; lt is the sample's index in the (half-size) tile.  A template
+    // parameter: a run-time flag here cost the full-wave c3 kernel 0.8 % (register allocation).
+    constexpr int wl = 64 >> LS;  // lanes that trace
     const bool on = (t & 63) < wl;
     const int lt = ((t >> 6) * wl) | (t & (wl - 1));
     {
@@ -1620,7 +1621,8 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, flo
 // big-scene (MODE_PACKED) kernels leave it out: at 8 waves their SGPRs are all taken by the
 // traversal, and the few extra uniform values spilled into its loops (c5 +14 %); the host
 // enables heavy-first only with kernels that have it (heavy_kernel).
-template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, bool HEAVY = (MODE & MODE_PACKED) == 0>
+template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, bool HEAVY = (MODE & MODE_PACKED) == 0,
+          int LS = 0>
 __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
     __shared__ int kpix[SAMPLES ? BLOCK : 1];
@@ -1689,7 +1691,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
         __syncthreads();
     }
 #endif
-    if constexpr (SAMPLES) samples_tile<MODE, D1>(P, tile, col, kpix, park);
+    if constexpr (SAMPLES) samples_tile<MODE, D1, LS>(P, tile, col, kpix, park);
     else pixels_tile<MODE, D1>(P, tile, park);
     if (HEAVY && P.tile_cost && lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
         asm volatile("" ::: "memory");
@@ -2622,8 +2624,22 @@ void launch_mode(const RenderParams& P, bool big, const Launch& L) {
                 return;
             }
         }
+        if constexpr (SAMPLES) {
+            if (P.half_waves) {
+                launch_render(render_tiles_kernel<MODE, SAMPLES, true, RT_RENDER_WAVES, (MODE & MODE_PACKED) == 0, 1>,
+                              grid, P, L);
+                return;
+            }
+        }
         launch_render(render_tiles_kernel<MODE, SAMPLES, true>, grid, P, L);
     } else {
+        if constexpr (SAMPLES) {
+            if (P.half_waves) {
+                launch_render(render_tiles_kernel<MODE, SAMPLES, false, RT_RENDER_WAVES, (MODE & MODE_PACKED) == 0, 1>,
+                              grid, P, L);
+                return;
+            }
+        }
         launch_render(render_tiles_kernel<MODE, SAMPLES, false>, grid, P, L);
     }
 }
@@ -2770,11 +2786,13 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // bound by its longest waves, and halving their rays shortens them (c3 band shards on one
     // GPU, max over the 8: kernel 0.101 -> 0.095 ms, frame 0.122 -> 0.116; at 4 and fewer shards
     // the doubled wave count costs more: N = 4 0.106 -> 0.116, N = 1 0.211 -> 0.373;
-    // scripts/half_waves_ab.py).  RT_HALF_WAVES=0/1 overrides.
-    // (RT_HALF_WAVES=2: 16 samples per wave, experiments.)
+    // scripts/half_waves_ab.py).  RT_HALF_WAVES=0/1 overrides.  (Quarter waves,
+    // 16 samples, measured slower at N = 8 and were dropped.)  The big-scene kernels have no
+    // half-wave form.
     int half = o->band_count >= 8 ? 1 : 0;
-    if (const char* e = std::getenv("RT_HALF_WAVES")) half = std::clamp(std::atoi(e), 0, 2);
-    if (!samples || o->spp > (64 >> half)) half = 0;
+    if (const char* e = std::getenv("RT_HALF_WAVES")) half = std::clamp(std::atoi(e), 0, 1);
+    const bool big_path = big_scene_waves(s) && o->max_depth == 1 && o->kernel != RT_KERNEL_LANE && !s->deep;
+    if (!samples || o->spp > (64 >> half) || big_path) half = 0;
     P.half_waves = half;
     int ppb = samples ? (BLOCK >> half) / o->spp : BLOCK;  // pixels per block
     int tw = 1;

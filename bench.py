@@ -3,7 +3,7 @@
 1920x1080x16 spp on the frog scene (BASELINE.json configs[2]; c4 when N > 1), counting frames
 that reached host memory.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c5] [--deliver p6|f32]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c3b|c5] [--deliver p6|f32]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N ...
 
@@ -11,15 +11,21 @@ A step = one full frame delivered to rank 0's host memory, as the reference's ti
 is render() plus the device-to-host copy of the frame (G/src/main.cu:369-376).  The native
 frame renderer (rt_renderer, include/rt_mi355x.h) does it: every rank renders its 8-row bands
 (band b -> rank b % N) with the HIP kernels, which write the strip's P6 samples themselves
-(write_p6, fused epilogue); the strips reach rank 0 over RCCL (grouped ncclSend/ncclRecv,
-xGMI) and rank 0 copies them into a pinned host frame with 2-D copies that place each band at
-its rows.  Frames are pipelined 3 deep: frame k+1 renders while frame k is gathered and
-copied.  Every timed frame is waited for in host memory before the clock stops.
+(write_p6, fused epilogue), and copies them over its own PCIe link into their rows of the
+host frame: pinned memory of the one process (--gpus N without a launcher: this process
+drives GPUs 0..N-1), or, one process per GPU under torchrun, a host frame shared by the
+processes (POSIX shm pinned in each, per-rank completion words; rank 0's wait returns when
+every rank has published the frame).  Frames are pipelined 2 deep on one GPU, 3 over N.
+Every timed frame is waited for in host memory before the clock stops.  At N > 1 the RCCL
+strip gather over xGMI (rank 0 assembles the frame in its HBM, then copies it) is measured
+after the headline and reported beside it (rccl_gather).
 --deliver f32 delivers the float framebuffer (the reference's own payload, 4x the bytes).
 --comm torch keeps the older torch.distributed gather (nccl or gloo) as an alternate launcher.
+A failed native multi-GPU path exits non-zero; --allow-fallback permits the gloo gather.
 
 Scene upload and BVH build are outside the timed region (as G/src/main.cu:362-378 times only
-render() + copy).  Rank 0 prints one JSON line.
+render() + copy); the LBVH build times are reported beside (lbvh_build).  Rank 0 prints one
+JSON line.
 """
 from __future__ import annotations
 
@@ -52,19 +58,28 @@ METRIC = "Mrays/s at 1920x1080x16spp (1/2/4/8 GPU) + PPM max-abs pixel diff"
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs: under torchrun one process per GPU (WORLD_SIZE must match); without a "
+                         "launcher this process drives GPUs 0..N-1 itself")
     ap.add_argument("--steps", type=int, default=100)  # ~35 ms of frames: a steadier average
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(configs.G_CONFIGS))
     ap.add_argument("--kernel", default="auto", choices=["auto", "wave", "lane"])
     ap.add_argument("--deliver", default="p6", choices=["p6", "f32"])
-    ap.add_argument("--gather", default="auto", choices=["auto", "rccl", "direct"])
+    ap.add_argument("--gather", default="auto", choices=["auto", "rccl", "direct", "shm"],
+                    help="auto: direct (one process) / shm (one process per GPU); rccl: the strip gather "
+                         "to rank 0's GPU over RCCL, then rank 0's host copy")
+    ap.add_argument("--allow-fallback", action="store_true",
+                    help="if the native multi-GPU path fails, fall back to the torch.distributed gather "
+                         "over gloo (CPU-staged; named in config.fallback).  Off: the failure exits non-zero")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal only: more ranks / band shards than visible GPUs, sharing them")
+    ap.add_argument("--no-rccl-leg", action="store_true", help="N > 1: skip the secondary RCCL-gather measurement")
     # frames in flight: 2 on one GPU (render k+1 while frame k's P6 is copied: 0.2170 vs 0.2233
-    # ms per frame at 3, 0.328 at 6); 3 over N GPUs, where rank 0's gather of
-    # frame k+1 can then overlap its host copy of frame k
+    # ms per frame at 3, 0.328 at 6); 3 over N GPUs
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--comm", default="native", choices=["native", "torch"],
-                    help="native: rt_renderer (RCCL inside librt_mi355x); torch: torch.distributed gather")
+                    help="native: rt_renderer (librt_mi355x); torch: torch.distributed gather (alternate launcher)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="--comm torch only. gloo: CPU-staged gather (lets N ranks share one GPU)")
     ap.add_argument("--gather-payload", default="p6", choices=["p6", "f32"], help="--comm torch only")
@@ -111,12 +126,12 @@ def cpu_baseline(hs, cam, cfg) -> dict:
     oc = orc.camera_from_basis(b["center"], b["pixel00_loc"], b["pixel_delta_u"], b["pixel_delta_v"],
                                cam.pixel_width, cam.pixel_height)
     H, W, spp = cam.pixel_height, cam.pixel_width, cfg["spp"]
-    rows = (0, H) if cfg is configs.G_CONFIGS["c3"] else (H // 2 - 32, H // 2 + 32)
+    rows = (0, H) if cfg["scene"] == "frog.json" else (H // 2 - 32, H // 2 + 32)
     reps, t0 = 0, time.perf_counter()
     while True:  # repeat the sample until ~10 s of CPU work (at least once)
         orc.render_g(hs.num_triangles, oc, hs.nodes, hs.aabbs, hs.triangles, hs.tri_object_ids, hs.materials,
                      hs.lights, spp=spp, max_depth=cfg["max_depth"], miss=hs.settings["miss_color"], rows=rows,
-                     threads=threads)
+                     diffuse_bounce=hs.settings["diffuse_bounce"], threads=threads)
         reps += 1
         if time.perf_counter() - t0 >= 10.0:
             break
@@ -149,7 +164,7 @@ def cpu_baseline(hs, cam, cfg) -> dict:
     except Exception as e:  # pragma: no cover - reported, not fatal
         out["hw1_c1"] = {"error": repr(e)}
     ref = REPO / "oracle" / "_ref" / "ref_g"
-    if ref.exists() and cfg is configs.G_CONFIGS["c3"]:
+    if ref.exists() and cfg["scene"] == "frog.json":
         with tempfile.TemporaryDirectory() as td:
             r = subprocess.run([str(ref), "scene", str(configs.SCENES / cfg["scene"]), str(REPO), td, str(W), str(H),
                                 str(spp), str(cfg["max_depth"]), "-1", "0"], capture_output=True, text=True,
@@ -171,13 +186,6 @@ def sync_all(dev, world):
     torch.cuda.synchronize(dev)
 
 
-def max_over_ranks(vals, world):
-    t = torch.tensor(vals, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return [float(x) for x in t.tolist()]
-
-
 def run_frames(r, cam, opts, n, depth):
     """Submit n frames, waiting for every one of them (host memory on rank 0)."""
     pend = []
@@ -191,67 +199,177 @@ def run_frames(r, cam, opts, n, depth):
     return last
 
 
-def timed_native(r, cam, opts, steps, warmup, depth, dev, world):
+def timed_native(r, cam, opts, steps, warmup, depth, ctx):
     run_frames(r, cam, opts, warmup, depth)
-    sync_all(dev, world)
+    ctx.sync()
     t0 = time.perf_counter()
     last = run_frames(r, cam, opts, steps, depth)
-    sync_all(dev, world)
+    ctx.sync()
     t1 = time.perf_counter()
     return t1 - t0, last
 
 
-def native(a, hs, cam, cfg, world, rank, local, dev):
+GATHERS = {"rccl": rt.RT_GATHER_RCCL, "direct": rt.RT_GATHER_DIRECT, "shm": rt.RT_GATHER_HOST_SHARED}
+GATHER_NAMES = {rt.RT_GATHER_RCCL: "rccl", rt.RT_GATHER_DIRECT: "direct", rt.RT_GATHER_HOST_SHARED: "shm"}
+COMM_TEXT = {
+    "direct": "each GPU copies its own bands into the pinned host frame over its own PCIe link (one process)",
+    "shm": "each rank copies its own bands over its own PCIe link into one host frame shared by the "
+           "ranks' processes (POSIX shm pinned with hipHostRegister, per-rank completion words); no RCCL",
+    "rccl": "strips to rank 0's GPU over RCCL (grouped ncclSend/ncclRecv, xGMI), then rank 0's host copy",
+}
+
+
+class Ctx:
+    """Where this process's ranks live: one process per GPU (torchrun: WORLD_SIZE > 1) or one
+    process driving every GPU (--gpus N without a launcher)."""
+
+    def __init__(self, a):
+        env_world = int(os.environ.get("WORLD_SIZE", "1"))
+        ndev = torch.cuda.device_count()
+        self.multiproc = env_world > 1
+        if self.multiproc:
+            if a.gpus != env_world:
+                raise SystemExit(f"bench: --gpus {a.gpus} but WORLD_SIZE {env_world}")
+            self.world = env_world
+            self.rank = int(os.environ.get("RANK", "0"))
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            if local >= ndev and not a.share_gpu:
+                raise SystemExit(f"bench: local rank {local} but only {ndev} GPU(s) visible "
+                                 "(--share-gpu rehearses several ranks per GPU)")
+            self.devices = (local % max(ndev, 1),)
+        else:
+            self.world, self.rank = a.gpus, 0
+            if a.gpus < 1:
+                raise SystemExit("bench: --gpus must be >= 1")
+            if ndev < a.gpus and not a.share_gpu:
+                raise SystemExit(f"bench: --gpus {a.gpus} but only {ndev} GPU(s) visible "
+                                 "(--share-gpu rehearses several band shards per GPU)")
+            self.devices = tuple(d % max(ndev, 1) for d in range(a.gpus))
+        self.distinct = len(set(self.devices)) == len(self.devices) and not (self.multiproc and a.share_gpu)
+        self.dev = torch.device("cuda", self.devices[0])
+        torch.cuda.set_device(self.dev)
+        if self.multiproc:
+            # control plane (barriers, max over ranks, ids) over gloo; frames move over the
+            # renderer's own paths (or torch's nccl group with --comm torch)
+            if a.comm == "torch" and a.backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist.init_process_group("gloo")
+
+    def sync(self):
+        for d in sorted(set(self.devices)):
+            torch.cuda.synchronize(d)
+        if self.multiproc:
+            dist.barrier()
+        for d in sorted(set(self.devices)):
+            torch.cuda.synchronize(d)
+
+    def bcast(self, obj):
+        if not self.multiproc:
+            return obj
+        box = [obj if self.rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    def max(self, vals):
+        t = torch.tensor(vals, dtype=torch.float64)
+        if self.multiproc:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(x) for x in t.tolist()]
+
+
+def make_renderer(hs, ctx, a, deliver, gather, depth):
+    kw = dict(band_rows=BAND_ROWS, deliver=deliver, gather=gather, depth=depth, devices=ctx.devices)
+    if ctx.multiproc:
+        kw.update(world_size=ctx.world, rank0=ctx.rank)
+        if gather == rt.RT_GATHER_RCCL:
+            kw["unique_id"] = ctx.bcast(rt.comm_unique_id() if ctx.rank == 0 else None)
+        if gather == rt.RT_GATHER_HOST_SHARED:
+            kw["host_frame_name"] = ctx.bcast(f"/rt_bench_{os.getpid()}_{os.urandom(6).hex()}"
+                                              if ctx.rank == 0 else None)
+    return rt.Renderer.from_host(hs, **kw)
+
+
+def native(a, hs, cam, cfg, ctx):
     spp = cfg["spp"]
     kernel = {"auto": rt.RT_KERNEL_AUTO, "wave": rt.RT_KERNEL_WAVE, "lane": rt.RT_KERNEL_LANE}[a.kernel]
     opts, _jit = rt.DeviceScene.make_opts(spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
-                                          kernel=kernel)
-    gather = {"auto": rt.RT_GATHER_AUTO, "rccl": rt.RT_GATHER_RCCL, "direct": rt.RT_GATHER_DIRECT}[a.gather]
-
-    def make(deliver, depth=a.depth):
-        uid = None
-        if world > 1:
-            obj = [rt.comm_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            uid = obj[0]
-        return rt.Renderer.from_host(hs, devices=(local,), world_size=world, rank0=rank, unique_id=uid,
-                                     band_rows=BAND_ROWS, deliver=deliver, gather=gather, depth=depth)
-
+                                          diffuse_bounce=hs.settings["diffuse_bounce"], kernel=kernel)
+    if a.gather == "auto":
+        gather = rt.RT_GATHER_HOST_SHARED if ctx.multiproc else rt.RT_GATHER_DIRECT
+    else:
+        gather = GATHERS[a.gather]
     deliver = rt.RT_DELIVER_F32 if a.deliver == "f32" else rt.RT_DELIVER_P6
-    r = make(deliver)
-    elapsed, last = timed_native(r, cam, opts, a.steps, a.warmup, a.depth, dev, world)
+    r = make_renderer(hs, ctx, a, deliver, gather, a.depth)
+    elapsed, last = timed_native(r, cam, opts, a.steps, a.warmup, a.depth, ctx)
+    kts, fts, pts = [], [], []
+    for i in range(r.local_ranks):
+        sc = r.scene(i)
+        kts.append(float(sc.kernel_times(a.steps).mean()))
+        fts.append(float(sc.frame_times(a.steps).mean()))
+        pts.append(float(sc.prepass_times(a.steps).mean()))
     sc = r.scene(0)
-    kt, ft, pt = sc.kernel_times(a.steps), sc.frame_times(a.steps), sc.prepass_times(a.steps)
-    res = {"elapsed": elapsed,
-           "kernel_ms": float(kt.mean()) if len(kt) else float("nan"),
-           "frame_ms": float(ft.mean()) if len(ft) else float("nan"),
-           "prepass_ms": float(pt.mean()) if len(pt) else float("nan"),
-           "live_tiles": list(sc.live_tiles()), "heavy_tiles": sc.heavy_tiles()}
-    if rank == 0:
+    res = {"elapsed": elapsed, "kernel_ms": max(kts), "frame_ms": max(fts), "prepass_ms": max(pts),
+           "kernel_ms_local": kts, "live_tiles": list(sc.live_tiles()), "heavy_tiles": sc.heavy_tiles(),
+           "gather_path": GATHER_NAMES[gather]}
+    if ctx.rank == 0:
         g, d, f = (r.times(k, a.steps) for k in (rt.RT_TIME_GATHER, rt.RT_TIME_DELIVER, rt.RT_TIME_FRAME))
         res.update(gather_ms=float(g.mean()), deliver_ms=float(d.mean()), frame_latency_ms=float(f.mean()))
         addr, n = last
         res["frame_bytes"] = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_uint8 * n).from_address(addr)).tobytes()
-    res["gather_path"] = "rccl" if (world > 1 and a.gather != "direct") else "direct (own strip to host)"
     r.close()
     if a.no_extras:
         return res
     # secondary: render only (strips stay in HBM), the rate the round-1 bench reported
-    rn = make(rt.RT_DELIVER_NONE)
-    el, _ = timed_native(rn, cam, opts, a.steps, a.warmup, a.depth, dev, world)
-    res["render_only_s"] = el
+    rn = make_renderer(hs, ctx, a, rt.RT_DELIVER_NONE, gather, a.depth)
+    res["render_only_s"], _ = timed_native(rn, cam, opts, a.steps, a.warmup, a.depth, ctx)
     rn.close()
     # secondary: the other payload (f32 = the reference's Vec3 framebuffer), also the float parity
     other = rt.RT_DELIVER_P6 if deliver == rt.RT_DELIVER_F32 else rt.RT_DELIVER_F32
-    ro = make(other)
-    el, last_o = timed_native(ro, cam, opts, max(10, a.steps // 4), 2, a.depth, dev, world)
-    res["other_payload"] = {"deliver": "p6" if other == rt.RT_DELIVER_P6 else "f32", "s": el,
-                            "steps": max(10, a.steps // 4)}
-    if rank == 0:
+    ro = make_renderer(hs, ctx, a, other, gather, a.depth)
+    n_other = max(10, a.steps // 4)
+    el, last_o = timed_native(ro, cam, opts, n_other, 2, a.depth, ctx)
+    res["other_payload"] = {"deliver": "p6" if other == rt.RT_DELIVER_P6 else "f32", "s": el, "steps": n_other}
+    if ctx.rank == 0:
         addr, n = last_o
         res["other_bytes"] = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_uint8 * n).from_address(addr)).tobytes()
     ro.close()
     return res
+
+
+def rccl_leg(a, hs, cam, cfg, ctx) -> dict:
+    """Secondary at N > 1 on distinct GPUs: the RCCL strip gather (north_star's xGMI gather), the
+    frame assembled in rank 0's HBM (RT_DELIVER_DEVICE) and, second, also copied to rank 0's host
+    memory.  Reported beside the headline, never substituted for it: an RCCL error is recorded."""
+    opts, _jit = rt.DeviceScene.make_opts(spp=cfg["spp"], max_depth=cfg["max_depth"],
+                                          miss_color=hs.settings["miss_color"],
+                                          diffuse_bounce=hs.settings["diffuse_bounce"])
+    out = {}
+    for name, dl in (("device", rt.RT_DELIVER_DEVICE), ("host_p6", rt.RT_DELIVER_P6)):
+        rr, err = None, ""
+        try:
+            rr = make_renderer(hs, ctx, a, dl, rt.RT_GATHER_RCCL, 3)
+        except rt.RTError as e:
+            err = str(e)
+        if ctx.max([1.0 if err else 0.0])[0] > 0:  # some rank failed: no rank runs the leg
+            out[name] = {"error": err or "RCCL renderer failed on another rank"}
+            if rr is not None:
+                rr.close()
+            continue
+        el, last = timed_native(rr, cam, opts, a.steps, a.warmup, 3, ctx)
+        el = ctx.max([el])[0]
+        d = {"value": round(cfg["spp"] * cam.pixel_width * cam.pixel_height * a.steps / el / 1e6, 3),
+             "ms_per_step": round(el / a.steps * 1e3, 4)}
+        if ctx.rank == 0:
+            d["gather_ms"] = round(float(rr.times(rt.RT_TIME_GATHER, a.steps).mean()), 4)
+            d["deliver_ms"] = round(float(rr.times(rt.RT_TIME_DELIVER, a.steps).mean()), 4)
+            if dl == rt.RT_DELIVER_P6 and a.config in GOLDEN_FULL:
+                addr, n = last
+                body = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_uint8 * n).from_address(addr)).tobytes()
+                d["ppm_identical"] = rt.p6_header(cam.pixel_width, cam.pixel_height) + body == golden_ppm(a.config)
+        rr.close()
+        out[name] = d
+    return out
 
 
 def band_shards(hs, cam, cfg, local, steps=20):
@@ -362,40 +480,60 @@ def load_traffic(path: Path, config: str):
         return None
 
 
-def primary_hit_parity(ds, cam, cfg, hs) -> dict:
-    """Primary-hit AOVs of one c3 frame (triangle index and t per sample) against the reference's
-    own full-size outputs (sha256 in tests/golden/scenes/c3_full/meta.json): equal hashes mean
+def primary_hit_parity(ds, cam, cfg, hs, golden: str) -> dict:
+    """Primary-hit AOVs of one frame (triangle index and t per sample) against the reference's
+    own full-size outputs (sha256 in tests/golden/scenes/<golden>/meta.json): equal hashes mean
     0 index mismatches."""
-    meta = json.loads((REPO / "tests" / "golden" / "scenes" / "c3_full" / "meta.json").read_text())
+    meta = json.loads((REPO / "tests" / "golden" / "scenes" / golden / "meta.json").read_text())
     _, hi, ht = ds.render(cam, spp=cfg["spp"], max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
-                          aov=True)
+                          diffuse_bounce=hs.settings["diffuse_bounce"], aov=True)
     idx_ok = hashlib.sha256(hi.tobytes()).hexdigest() == meta["sha256"]["hits.i32"]
     t_ok = hashlib.sha256(ht.tobytes()).hexdigest() == meta["sha256"]["hitt.f32"]
-    return {"vs": "reference hits.i32 / hitt.f32 sha256 (tests/golden/scenes/c3_full)",
+    return {"vs": f"reference hits.i32 / hitt.f32 sha256 (tests/golden/scenes/{golden})",
             "hit_index_sha256_equal": idx_ok, "hit_t_sha256_equal": t_ok,
             "hit_index_mismatches": 0 if idx_ok else "unknown (hash differs)",
             "samples_hit": int((hi >= 0).sum())}
 
 
+GOLDEN_FULL = {"c3": "c3_full", "c3b": "c3b_full"}  # reference outputs of the full bench frame
+
+
+def golden_ppm(config: str) -> bytes:
+    return gzip.open(REPO / "tests" / "golden" / "scenes" / GOLDEN_FULL[config] / "image.ppm.gz").read()
+
+
+def lbvh_times(hs, device: int, reps: int = 5) -> dict:
+    """The LBVH build the reference times (G/src/main.cu:281-293 GPU, :306-317 CPU): the host
+    build (rt_build_bvh, the reference CPU algorithm) and the GPU build (rt_build_bvh_device,
+    mesh resident in HBM), wall clock around each call as the reference measures; arrays compared."""
+    hn, ha = rt.build_bvh(hs.positions, hs.indices)  # warm (page-in)
+    th = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        hn, ha = rt.build_bvh(hs.positions, hs.indices)
+        th.append(time.perf_counter() - t0)
+    pos = torch.from_numpy(hs.positions).to(torch.device("cuda", device))
+    idx = torch.from_numpy(hs.indices.view(np.int32)).to(torch.device("cuda", device))
+    gn, ga = rt.build_bvh_device(pos, idx, device=device, tensors=True)  # warm (code objects, rocPRIM)
+    tg = []
+    for _ in range(reps):
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        gn, ga = rt.build_bvh_device(pos, idx, device=device, tensors=True)  # synchronises its stream
+        tg.append(time.perf_counter() - t0)
+    same = (np.array_equal(gn.cpu().numpy().view(np.uint32), hn)
+            and np.array_equal(ga.cpu().numpy().view(np.uint32), ha.view(np.uint32)))
+    return {"triangles": hs.num_triangles, "host_ms": round(float(np.median(th)) * 1e3, 3),
+            "gpu_ms": round(float(np.median(tg)) * 1e3, 3), "gpu_ms_min": round(min(tg) * 1e3, 3),
+            "arrays_identical": bool(same),
+            "note": "median wall ms of the call (host: rt_build_bvh, 1 thread; GPU: rt_build_bvh_device incl. "
+                    "its stream sync), outside the timed region; the reference prints both (G/src/main.cu:293,317)"}
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and world > 1:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
-    ndev = torch.cuda.device_count()
-    local = local % max(ndev, 1)  # gloo rehearsal: several ranks may share one GPU
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        # control plane (barriers, max over ranks, the RCCL id) over gloo; the frame data moves
-        # over the renderer's own RCCL communicator (or torch's nccl group with --comm torch)
-        if a.comm == "torch" and a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
-
+    ctx = Ctx(a)
+    world, rank = ctx.world, ctx.rank
     cfg = configs.G_CONFIGS[a.config]
     sp = configs.scene_path(cfg["scene"])
     hs = rt.HostScene.load_json(sp, REPO if sp.parent == configs.SCENES else sp.parent)
@@ -406,36 +544,35 @@ def main():
 
     comm = a.comm
     fallback = None
+    if comm == "torch" and not ctx.multiproc and world > 1:
+        raise SystemExit("bench: --comm torch needs one process per GPU (torchrun)")
     if comm == "native":
         try:
-            res = native(a, hs, cam, cfg, world, rank, local, dev)
+            res = native(a, hs, cam, cfg, ctx)
         except rt.RTError as e:
-            if world == 1 or e.code != -8:
-                raise
-            # the process group is gloo (the native path's control plane): gather over it, CPU-staged
+            if world == 1 or not ctx.multiproc or not a.allow_fallback:
+                print(f"bench: native {world}-GPU path failed: {e}", file=sys.stderr, flush=True)
+                raise SystemExit(2)
+            # --allow-fallback: the process group is gloo (the native path's control plane)
             a.backend = "gloo"
-            fallback = f"native RCCL failed ({e}); torch.distributed gather (gloo, CPU-staged) used"
+            fallback = f"native path failed ({e}); torch.distributed gather (gloo, CPU-staged) used (--allow-fallback)"
             print(f"bench: {fallback}", file=sys.stderr, flush=True)
             comm = "torch"
     if comm == "torch":
         a.deliver = a.gather_payload
-        res = torch_path(a, hs, cam, cfg, world, rank, local, dev)
+        res = torch_path(a, hs, cam, cfg, world, rank, ctx.devices[0], ctx.dev)
 
     elapsed = res["elapsed"]
     vals = [elapsed, res["kernel_ms"], res["frame_ms"]]
     if "render_only_s" in res:
         vals.append(res["render_only_s"])
         vals.append(res["other_payload"]["s"])
-    m = max_over_ranks(vals, world)
+    m = ctx.max(vals)
     elapsed, kernel_ms, frame_ms = m[0], m[1], m[2]
-    shards = None
+    shards = lbvh = None
     if world == 1 and not a.no_extras and comm == "native":
-        shards = band_shards(hs, cam, cfg, local)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    if rank != 0:
-        return
+        shards = band_shards(hs, cam, cfg, ctx.devices[0])
+        lbvh = lbvh_times(hs, ctx.devices[0])
 
     samples = W * H * spp
     value = samples * a.steps / elapsed / 1e6
@@ -452,24 +589,28 @@ def main():
         "vs_baseline": None,
         "dtype": "f32+f64",
         "data": "synthetic=false: frog.obj scene (reference asset), camera/light from frog.json"
-                if a.config == "c3" else "synthetic seeded 1,048,576-triangle heightfield",
-        "config": {"workload": f"{a.config if world == 1 else 'c4'}: {cfg['scene']} {W}x{H}x{spp}spp "
-                               f"max_bounces={cfg['max_depth']}, Lambert/Blinn-Phong + 1 hard shadow ray per light",
-                   "triangles": hs.num_triangles, "bands": f"{BAND_ROWS}-row bands round-robin over {world} GPU(s)",
-                   "step_delivers": (f"the frame's {'P6 samples (PPM body)' if a.deliver == 'p6' else 'float framebuffer'}"
-                                     " in rank 0's host memory (pinned), every timed frame waited for"),
-                   "comm": ("native rt_renderer: " + res["gather_path"]) if comm == "native" else res["gather_path"],
-                   "pipeline_depth": a.depth if comm == "native" else 2, "kernel": a.kernel},
+                if a.config in ("c3", "c3b") else "synthetic seeded 1,048,576-triangle heightfield",
     }
+    gpath = res["gather_path"]
+    line["config"] = {
+        "workload": f"{a.config if world == 1 or a.config != 'c3' else 'c4'}: {cfg['scene']} {W}x{H}x{spp}spp "
+                    f"max_bounces={cfg['max_depth']}" + (", diffuse bounces" if cfg["max_depth"] > 1 else "")
+                    + ", Lambert/Blinn-Phong + 1 hard shadow ray per light",
+        "triangles": hs.num_triangles, "bands": f"{BAND_ROWS}-row bands round-robin over {world} GPU(s)",
+        "processes": world if ctx.multiproc else 1,
+        "devices": "one per process" if ctx.multiproc else list(ctx.devices),
+        "step_delivers": (f"the frame's {'P6 samples (PPM body)' if a.deliver == 'p6' else 'float framebuffer'}"
+                          " in rank 0's host memory, every timed frame waited for"),
+        "comm": (f"native rt_renderer, gather={gpath}: {COMM_TEXT[gpath]}" if comm == "native" else gpath),
+        "pipeline_depth": a.depth if comm == "native" else 2, "kernel": a.kernel}
+    if a.share_gpu and world > 1:
+        line["config"]["rehearsal"] = "--share-gpu: ranks share GPUs (not a multi-GPU measurement)"
     if fallback:
         line["config"]["fallback"] = fallback
     per_gpu_samples = samples / world
-    ref_eq = configs.BYTES_PER_SAMPLE[a.config] * per_gpu_samples / (kernel_ms / 1e3) / 1e9
+    bps = configs.BYTES_PER_SAMPLE.get(a.config)
     tr = load_traffic(Path(a.traffic_file), a.config) if world == 1 else None
     traffic = tr.get("bytes_per_launch") if tr else None
-    compulsory = None
-    if tr and tr.get("compulsory_bytes_per_launch"):
-        compulsory = tr["compulsory_bytes_per_launch"]
     roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": traffic,
             "kernel": "render_tiles_kernel", "kernel_ms": round(kernel_ms, 4), "frame_ms": round(frame_ms, 4)}
     if traffic:
@@ -477,37 +618,47 @@ def main():
         roof.update(achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
                     achieved_from="measured HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
                                   f"{tr.get('source', '?')}) / live kernel_ms")
+        if tr.get("compulsory_bytes_per_launch"):
+            roof["compulsory_bytes_per_launch"] = tr["compulsory_bytes_per_launch"]
+            roof["compulsory_GBps"] = round(tr["compulsory_bytes_per_launch"] / (kernel_ms / 1e3) / 1e9, 2)
     else:
         roof.update(achieved=None, frac=None, achieved_from="no PMC traffic for this launch shape")
-    if compulsory:
-        roof["compulsory_bytes_per_launch"] = compulsory
-        roof["compulsory_GBps"] = round(compulsory / (kernel_ms / 1e3) / 1e9, 2)
-    roof["reference_equivalent_GBps"] = round(ref_eq, 2)
-    roof["reference_equivalent_note"] = ("SURVEY.md §8(d) reference-layout model, "
-                                         f"{configs.BYTES_PER_SAMPLE[a.config]:.2f} B/sample: the bytes the "
-                                         "reference's per-ray traversal would fetch, not this kernel's traffic")
+    if bps:
+        roof["reference_equivalent_GBps"] = round(bps * per_gpu_samples / (kernel_ms / 1e3) / 1e9, 2)
+        roof["reference_equivalent_note"] = (f"SURVEY.md §8(d) reference-layout model, {bps:.2f} B/sample: the "
+                                             "bytes the reference's per-ray traversal would fetch, not this "
+                                             "kernel's traffic")
     if tr and tr.get("issue"):
         roof["issue"] = tr["issue"]
         roof["binding"] = tr.get("binding")
     line["roofline"] = roof
-    if not a.no_extras:
-        # total rays/s: the frame's camera + shadow (+ bounce) rays, counted on
-        # the device by rt_count_rays outside the timed region, over the same wall time
-        ds = rt.DeviceScene.from_host(hs, device=local)
+    if not a.no_extras and rank == 0:
+        # rays: camera + shadow (+ bounce) rays of one frame, counted on the
+        # device by rt_count_rays_ex outside the timed region, over the same wall time; the
+        # traced rate counts only camera rays that are traversed (the culling passes prove the
+        # others miss: their samples are written without a traversal)
+        ds = rt.DeviceScene.from_host(hs, device=ctx.devices[0])
         try:
-            rays = ds.count_rays(cam, spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"])
-            if a.config == "c3" and not a.no_parity:
-                line["parity_primary_hits"] = primary_hit_parity(ds, cam, cfg, hs)
+            rays = ds.count_rays(cam, spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
+                                 diffuse_bounce=hs.settings["diffuse_bounce"])
+            if a.config in GOLDEN_FULL and not a.no_parity:
+                line["parity_primary_hits"] = primary_hit_parity(ds, cam, cfg, hs, GOLDEN_FULL[a.config])
         finally:
             ds.close()
         total = rays["camera"] + rays["shadow"] + rays["bounce"]
+        traced = rays["camera_traced"] + rays["shadow"] + rays["bounce"]
         line["rays_per_frame"] = rays
         line["total_rays_per_s"] = round(total * a.steps / elapsed / 1e6, 3)
-        line["total_rays_unit"] = "Mrays/s (camera + shadow + bounce rays)"
+        line["traced_rays_per_s"] = round(traced * a.steps / elapsed / 1e6, 3)
+        line["culled_sample_frac"] = round(1.0 - rays["camera_traced"] / max(rays["camera"], 1), 5)
+        line["rays_unit"] = ("Mrays/s: total = camera + shadow + bounce rays; traced = the same with only the "
+                             "camera rays of tiles the exact culling passes leave to the render kernel")
     extra = {"kernel_ms": round(kernel_ms, 4), "frame_ms": round(frame_ms, 4)}
     for k in ("gather_ms", "deliver_ms", "frame_latency_ms"):
         if k in res:
             extra[k] = round(res[k], 4)
+    if len(res.get("kernel_ms_local", [])) > 1:
+        extra["kernel_ms_per_local_rank"] = [round(x, 4) for x in res["kernel_ms_local"]]
     if "render_only_s" in res:
         extra["render_only_value"] = round(samples * a.steps / m[3] / 1e6, 3)
         op = res["other_payload"]
@@ -521,12 +672,14 @@ def main():
     if shards:
         extra["band_shards_one_gpu"] = shards
     line["timing"] = extra
+    if lbvh:
+        line["lbvh_build"] = lbvh
 
-    if not a.no_parity and a.config == "c3":
-        ref = np.frombuffer(gzip.open(REPO / "tests" / "golden" / "scenes" / "c3_full" / "fb.f32.gz").read(),
-                            np.float32).reshape(H, W, 3)
-        ppm_ref = gzip.open(REPO / "tests" / "golden" / "scenes" / "c3_full" / "image.ppm.gz").read()
-        par = {"vs": "reference CPU render() output (tests/golden/scenes/c3_full)"}
+    if not a.no_parity and a.config in GOLDEN_FULL and rank == 0:
+        gdir = REPO / "tests" / "golden" / "scenes" / GOLDEN_FULL[a.config]
+        ref = np.frombuffer(gzip.open(gdir / "fb.f32.gz").read(), np.float32).reshape(H, W, 3)
+        ppm_ref = golden_ppm(a.config)
+        par = {"vs": f"reference CPU render() output (tests/golden/scenes/{GOLDEN_FULL[a.config]})"}
 
         def p6_check(body: bytes, tag: str):
             got = np.frombuffer(body, np.uint8).astype(int)
@@ -551,7 +704,27 @@ def main():
     if world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(hs, cam, cfg)
         line["speedup_vs_cpu_baseline"] = round(value / line["cpu_baseline"]["value"], 2)
-    print(json.dumps(line), flush=True)
+    if world > 1 and comm == "native" and ctx.distinct and not a.no_extras and not a.no_rccl_leg \
+            and res["gather_path"] != "rccl":
+        # last, under a watchdog: a collective that never completes must not cost the line
+        import threading
+
+        def _expire():
+            if rank == 0:
+                line["rccl_gather"] = {"error": "timed out after 180 s (RCCL leg abandoned)"}
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+
+        wd = threading.Timer(180.0, _expire)
+        wd.daemon = True
+        wd.start()
+        line["rccl_gather"] = rccl_leg(a, hs, cam, cfg, ctx)
+        wd.cancel()
+    if ctx.multiproc:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

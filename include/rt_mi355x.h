@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2  /* 2: rt_renderer_opts.host_frame_name, RT_GATHER_HOST_SHARED */
 
 enum {
     RT_OK = 0,
@@ -224,11 +224,12 @@ int rt_shard_rows(int height, int band_rows, int band_index, int band_count);
 /* Render into device memory on `hip_stream` (hipStream_t; NULL = the null stream), no
  * host sync.  rgb_dev: rows*W*3 floats.  hit_idx_dev / hit_t_dev (optional, rows*W*spp):
  * primary-ray triangle index (-1 = miss) and t per (pixel, sample).
- * Frames of one scene are ordered: a call on another stream than the scene's previous frame
- * makes its stream wait for that frame first.  A frame's tile pre-passes (which write the culled
- * tiles' pixels) run on the scene's own stream, overlapping the previous frame's render kernel
- * unless the two frames' output buffers overlap; hip_stream waits for them before the render
- * kernel, so the frame is complete when hip_stream reaches the end of this call's work. */
+ * Stream-ordered: the frame's work starts after everything queued on hip_stream before the
+ * call and is complete when hip_stream reaches the end of this call's work.  (A frame's tile
+ * pre-passes, which write the culled tiles' pixels, run on the scene's own stream after an
+ * event wait on hip_stream; rt_renderer, which orders its buffer reuse on the host, lets them
+ * overlap the previous frame's render kernel instead.)  Frames of one scene are ordered: a
+ * call on another stream than the scene's previous frame makes its stream wait for that frame. */
 int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt,
                      float* rgb_dev, int32_t* hit_idx_dev, float* hit_t_dev, void* hip_stream);
 
@@ -252,6 +253,10 @@ int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt,
  * kernels (not the timed ones) and discards it; synchronous.  For total rays/s
  * (SURVEY.md §8(d)). */
 int rt_count_rays(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt, uint64_t counts[3]);
+/* rt_count_rays + counts[3]: the camera rays that are traversed, i.e. those of the pixel tiles
+ * the culling pre-passes leave to the render kernel (the others provably miss every box of the
+ * tree, their samples are written as misses without a traversal). */
+int rt_count_rays_ex(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt, uint64_t counts[4]);
 
 /* The reference signature verbatim (query.h:13-29) over host arrays: uploads to device 0,
  * renders on the GPU, writes W*H Vec3 to `output` (host).  Synchronous. */
@@ -286,7 +291,16 @@ int rt_render_reference_gpus(size_t num_triangles, int W, int H, const rt_camera
  * process per GPU under torchrun); every process passes the same 128-byte unique_id, made by
  * rt_comm_unique_id on the process holding rank 0 and shared by the caller.
  * A device id may repeat (several band shards on one GPU, for tests): then gather must be
- * RT_GATHER_DIRECT, each rank copying its bands straight into the host frame. */
+ * RT_GATHER_DIRECT (one process) or RT_GATHER_HOST_SHARED (several), each rank copying its
+ * bands straight into the host frame.
+ *
+ * RT_GATHER_HOST_SHARED (one process per GPU, e.g. under torchrun): the depth host frames are
+ * one POSIX shared-memory segment (host_frame_name, the same on every process; rank 0's
+ * process creates it, the others attach, each pins it with hipHostRegister).  Every rank
+ * copies its own bands over its own PCIe link into their image rows, then publishes the frame
+ * in the segment's per-rank completion word; rank 0's rt_renderer_wait returns once every rank
+ * has published.  A rank copies frame t into a slot only after rank 0 has submitted frame t
+ * (rank 0's caller then no longer holds frame t-depth).  RCCL is not used on this path. */
 typedef struct rt_renderer rt_renderer;
 
 enum {
@@ -296,10 +310,12 @@ enum {
     RT_DELIVER_NONE = 3    /* render only (strips stay on each rank): measurement */
 };
 enum {
-    RT_GATHER_AUTO = 0,    /* RCCL when world_size > 1 and the devices differ, else DIRECT */
+    RT_GATHER_AUTO = 0,    /* one process: DIRECT; several: HOST_SHARED with host_frame_name, else RCCL */
     RT_GATHER_RCCL = 1,    /* strips -> rank 0's GPU over RCCL, then one host copy stream */
-    RT_GATHER_DIRECT = 2   /* each local rank copies its own bands into the host frame (its own
+    RT_GATHER_DIRECT = 2,  /* each local rank copies its own bands into the host frame (its own
                               PCIe link); single process only */
+    RT_GATHER_HOST_SHARED = 3 /* each rank of a multi-process job copies its own bands into one
+                                 host frame shared by the processes (host_frame_name); no RCCL */
 };
 enum { RT_RENDERER_SELF_SEND = 1 /* rank 0's own strip also goes through RCCL (tests at world 1) */ };
 
@@ -314,6 +330,9 @@ typedef struct {
     int32_t gather;           /* RT_GATHER_* */
     int32_t depth;            /* frames in flight, 1..8 (default 3) */
     int32_t flags;            /* RT_RENDERER_* */
+    const char* host_frame_name; /* RT_GATHER_HOST_SHARED: shared-memory name ("/..."), same on every
+                                    process; RT_GATHER_AUTO picks HOST_SHARED for a multi-process
+                                    renderer when it is set (RCCL otherwise) */
 } rt_renderer_opts;
 void rt_renderer_opts_default(rt_renderer_opts* o);
 
@@ -331,7 +350,8 @@ void rt_renderer_destroy(rt_renderer* r);
 /* Enqueue one frame (opts: its band fields are the renderer's).  Blocks only to reuse the
  * buffers of frame ticket-depth, which must then be complete.  *ticket numbers the frames. */
 int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt_render_opts* opts, uint64_t* ticket);
-/* Wait for frame `ticket` (one of the last `depth` submitted).  On the process holding rank 0,
+/* Wait for frame `ticket` (one of the last `depth` submitted, and not from before a change of
+ * the frame size, which reallocates the buffers).  On the process holding rank 0,
  * *frame / *bytes give the delivered frame: pinned host memory (RT_DELIVER_P6/F32) or rank 0's
  * device memory (RT_DELIVER_DEVICE), valid until the submit of frame ticket+depth; elsewhere
  * NULL / 0.  Either pointer may be NULL. */

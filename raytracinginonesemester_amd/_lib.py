@@ -22,7 +22,7 @@ RT_TILES_AUTO, RT_TILES_LINEAR, RT_TILES_XCD_CHUNK, RT_TILES_ROWS = 0, 1, 2, 3
 RT_FLAG_NO_CULL = 1
 RT_FLAG_BINARY = 4
 RT_DELIVER_P6, RT_DELIVER_F32, RT_DELIVER_DEVICE, RT_DELIVER_NONE = 0, 1, 2, 3
-RT_GATHER_AUTO, RT_GATHER_RCCL, RT_GATHER_DIRECT = 0, 1, 2
+RT_GATHER_AUTO, RT_GATHER_RCCL, RT_GATHER_DIRECT, RT_GATHER_HOST_SHARED = 0, 1, 2, 3
 RT_RENDERER_SELF_SEND = 1
 RT_TIME_GATHER, RT_TIME_DELIVER, RT_TIME_FRAME = 0, 1, 2
 
@@ -104,7 +104,8 @@ class RenderOpts(C.Structure):
 class RendererOpts(C.Structure):
     _fields_ = [("n_devices", C.c_int32), ("devices", C.c_void_p), ("world_size", C.c_int32),
                 ("rank0", C.c_int32), ("unique_id", C.c_void_p), ("band_rows", C.c_int32),
-                ("deliver", C.c_int32), ("gather", C.c_int32), ("depth", C.c_int32), ("flags", C.c_int32)]
+                ("deliver", C.c_int32), ("gather", C.c_int32), ("depth", C.c_int32), ("flags", C.c_int32),
+                ("host_frame_name", C.c_void_p)]
 
 
 P = C.c_void_p
@@ -144,6 +145,7 @@ SIGNATURES = {
     "rt_render_device_p6": (I, [P, P, P, P, P, P, P, P]),
     "rt_render": (I, [P, P, P, P, P, P]),
     "rt_count_rays": (I, [P, P, P, P]),
+    "rt_count_rays_ex": (I, [P, P, P, P]),
     "rt_render_reference": (I, [SZ, I, I, P, Vec3, I, I, P, P, P, P, P, I, P, I, I, P]),
     "rt_render_reference_gpus": (I, [SZ, I, I, P, Vec3, I, I, P, P, P, P, P, I, P, I, I, I, P]),
     "rt_renderer_opts_default": (None, [P]),

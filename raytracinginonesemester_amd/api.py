@@ -206,7 +206,8 @@ class DeviceScene:
 
     @classmethod
     def _borrow(cls, handle, num_triangles: int, owner) -> "DeviceScene":
-        """A scene owned by a Renderer (its timing queries; destroyed with the renderer)."""
+        """A scene owned by a Renderer (its timing queries; destroyed with the renderer, which
+        then invalidates this view: later calls raise instead of touching freed memory)."""
         self = cls.__new__(cls)
         self._h = C.c_void_p(handle)
         self._owned = False
@@ -215,6 +216,11 @@ class DeviceScene:
         self.num_triangles = num_triangles
         self.device = int(lib().rt_scene_device(self._h))
         return self
+
+    def _handle(self) -> C.c_void_p:
+        if not self._h:
+            raise L.RTError(-1, "scene is closed (or its Renderer was closed)")
+        return self._h
 
     @classmethod
     def from_host(cls, hs: HostScene, device: int = 0) -> "DeviceScene":
@@ -227,7 +233,7 @@ class DeviceScene:
 
     @property
     def device_bytes(self) -> int:
-        return int(lib().rt_scene_device_bytes(self._h))
+        return int(lib().rt_scene_device_bytes(self._handle()))
 
     @staticmethod
     def make_opts(spp: int = 1, max_depth: int = 1, diffuse_bounce: bool = True, miss_color=(0, 0, 0),
@@ -262,57 +268,58 @@ class DeviceScene:
         if aov:
             hi = np.zeros((rows, W, spp), np.int32)
             ht = np.zeros((rows, W, spp), np.float32)
-        check(lib().rt_render(self._h, C.byref(camera.c), C.byref(o), ptr(rgb), ptr(hi), ptr(ht)))
+        check(lib().rt_render(self._handle(), C.byref(camera.c), C.byref(o), ptr(rgb), ptr(hi), ptr(ht)))
         return (rgb, hi, ht) if aov else rgb
 
     def count_rays(self, camera: Camera, spp: int = 1, max_depth: int = 1, diffuse_bounce: bool = True,
                    miss_color=(0, 0, 0), band_rows: int = 8, band_index: int = 0, band_count: int = 1) -> dict:
-        """Rays one frame traces (rt_count_rays): camera, shadow and bounce counts, the classes of
-        the oracle's stats["rays"]."""
+        """Rays one frame traces (rt_count_rays_ex): camera, shadow and bounce counts, the classes
+        of the oracle's stats["rays"], and camera_traced, the camera rays of the tiles the culling
+        passes leave to the render kernel (the rest provably miss and are not traversed)."""
         o, _jit = self.make_opts(spp, max_depth, diffuse_bounce, miss_color, None, band_rows, band_index,
                                  band_count)
-        out = (C.c_uint64 * 3)()
-        check(lib().rt_count_rays(self._h, C.byref(camera.c), C.byref(o), out))
-        return {"camera": int(out[0]), "shadow": int(out[1]), "bounce": int(out[2])}
+        out = (C.c_uint64 * 4)()
+        check(lib().rt_count_rays_ex(self._handle(), C.byref(camera.c), C.byref(o), out))
+        return {"camera": int(out[0]), "shadow": int(out[1]), "bounce": int(out[2]), "camera_traced": int(out[3])}
 
     def render_device(self, camera: Camera, opts, rgb_dev_ptr: int, hit_idx_ptr=None, hit_t_ptr=None,
                       stream: Optional[int] = None, p6_dev_ptr=None) -> None:
         """Render into device memory (rt_render_device); with ``p6_dev_ptr`` the render and cull
         kernels also write the pixels' P6 samples (write_p6 defaults), rt_render_device_p6."""
-        check(lib().rt_render_device_p6(self._h, C.byref(camera.c), C.byref(opts), rgb_dev_ptr, hit_idx_ptr,
+        check(lib().rt_render_device_p6(self._handle(), C.byref(camera.c), C.byref(opts), rgb_dev_ptr, hit_idx_ptr,
                                         hit_t_ptr, p6_dev_ptr, stream))
 
     def kernel_times(self, max_launches: int = 256) -> np.ndarray:
         """ms of the render kernel for the most recent launches (HIP events on its stream)."""
         out = np.zeros(max_launches, np.float32)
         n = C.c_int()
-        check(lib().rt_kernel_times(self._h, ptr(out), max_launches, C.byref(n)))
+        check(lib().rt_kernel_times(self._handle(), ptr(out), max_launches, C.byref(n)))
         return out[:n.value]
 
     def live_tiles(self) -> tuple:
         """(traced tiles, all tiles) of the most recent render."""
         live, total = C.c_int64(), C.c_int64()
-        check(lib().rt_live_tiles(self._h, C.byref(live), C.byref(total)))
+        check(lib().rt_live_tiles(self._handle(), C.byref(live), C.byref(total)))
         return live.value, total.value
 
     def heavy_tiles(self) -> int:
         """Tiles the most recent render dispatched first (heavy-first order, speed only)."""
         n = C.c_int64()
-        check(lib().rt_heavy_tiles(self._h, C.byref(n)))
+        check(lib().rt_heavy_tiles(self._handle(), C.byref(n)))
         return n.value
 
     def frame_times(self, max_launches: int = 256) -> np.ndarray:
         """ms of the frame's device work (cull pre-passes + render kernel)."""
         out = np.zeros(max_launches, np.float32)
         n = C.c_int()
-        check(lib().rt_frame_times(self._h, ptr(out), max_launches, C.byref(n)))
+        check(lib().rt_frame_times(self._handle(), ptr(out), max_launches, C.byref(n)))
         return out[:n.value]
 
     def prepass_times(self, max_launches: int = 256) -> np.ndarray:
         """ms of the cull pre-passes (root-box cull + tree-cut cull) alone."""
         out = np.zeros(max_launches, np.float32)
         n = C.c_int()
-        check(lib().rt_prepass_times(self._h, ptr(out), max_launches, C.byref(n)))
+        check(lib().rt_prepass_times(self._handle(), ptr(out), max_launches, C.byref(n)))
         return out[:n.value]
 
     def close(self) -> None:
@@ -331,16 +338,18 @@ class Renderer:
     """render(scene, camera) -> frame in host memory on 1..N GPUs (rt_renderer, include/rt_mi355x.h).
 
     Every rank renders its 8-row bands (band b -> rank b % world) into a device strip with the
-    fused P6 epilogue; the strips reach rank 0 over RCCL and are copied band by band into a
-    pinned host frame, pipelined `depth` frames deep.  ``devices``: the GPUs this process
-    drives; ``world_size``/``rank0``/``unique_id`` join a multi-process job (one process per
-    GPU): rank 0's process makes the id with :func:`comm_unique_id` and shares it.
+    fused P6 epilogue; the strips reach the host frame band by band, pipelined `depth` frames
+    deep: each GPU over its own PCIe link (RT_GATHER_DIRECT in one process; RT_GATHER_HOST_SHARED
+    across processes, into the shared-memory frame ``host_frame_name``), or over RCCL to rank 0
+    first (RT_GATHER_RCCL).  ``devices``: the GPUs this process drives;
+    ``world_size``/``rank0``/``unique_id`` join a multi-process job (one process per GPU): rank
+    0's process makes the RCCL id with :func:`comm_unique_id` and shares it.
     """
 
     def __init__(self, num_triangles: int, nodes, aabbs, triangles, tri_object_ids=None, materials=None,
                  lights=None, devices=(0,), world_size: int = 0, rank0: int = 0, unique_id: bytes = None,
                  band_rows: int = 8, deliver: int = L.RT_DELIVER_P6, gather: int = L.RT_GATHER_AUTO,
-                 depth: int = 3, flags: int = 0):
+                 depth: int = 3, flags: int = 0, host_frame_name: Optional[str] = None):
         P = int(num_triangles)
         keep = [_c(nodes, np.uint32), _c(aabbs, np.float32), _c(triangles, np.float32)]
         objs = None if tri_object_ids is None else _c(tri_object_ids, np.int32)
@@ -356,11 +365,17 @@ class Renderer:
             uid = C.create_string_buffer(bytes(unique_id), 128)
             o.unique_id = C.addressof(uid)
         o.band_rows, o.deliver, o.gather, o.depth, o.flags = int(band_rows), int(deliver), int(gather), int(depth), int(flags)
+        name = None
+        if host_frame_name:
+            name = C.create_string_buffer(str(host_frame_name).encode())
+            o.host_frame_name = C.addressof(name)
         h = C.c_void_p()
         check(lib().rt_renderer_create(P, ptr(keep[0]), ptr(keep[1]), ptr(keep[2]), ptr(objs), ptr(mats),
                                        0 if mats is None else mats.shape[0], ptr(lts),
                                        0 if lts is None else lts.shape[0], C.byref(o), C.byref(h)))
         self._h = h
+        self._name = name
+        self._borrowed = []  # DeviceScene views of this renderer's scenes (invalidated by close)
         self.num_triangles = P
         self.deliver = int(deliver)
         self.world = int(world_size) or len(devs)
@@ -380,7 +395,9 @@ class Renderer:
         h = lib().rt_renderer_scene(self._h, int(i))
         if not h:
             raise L.RTError(-1, f"no local rank {i}")
-        return DeviceScene._borrow(h, self.num_triangles, self)
+        v = DeviceScene._borrow(h, self.num_triangles, self)
+        self._borrowed.append(v)
+        return v
 
     def submit(self, camera: Camera, opts) -> int:
         t = C.c_uint64()
@@ -410,6 +427,9 @@ class Renderer:
         return out[:n.value]
 
     def close(self) -> None:
+        for v in getattr(self, "_borrowed", []):
+            v._h = C.c_void_p()
+        self._borrowed = []
         if self._h:
             lib().rt_renderer_destroy(self._h)
             self._h = C.c_void_p()

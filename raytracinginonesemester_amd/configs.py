@@ -7,6 +7,7 @@ The five configurations are BASELINE.json's ``configs`` made concrete (SURVEY.md
 * ``c2`` — HW1 path on frog.obj, 640x480, 1 spp, primary rays + HW1 ``shade`` only.
 * ``c3`` — G/ path, frog.json (HW2/HW2/GPUandCPU/assets/json_files/frog.json), 1920x1080,
   16 spp, max_bounces overridden to 1: Lambert/Blinn-Phong + one hard shadow ray.
+* ``c3b`` — c3 with frog.json's own max_bounces 8 (diffuse bounces), the reference default.
 * ``c4`` — c3 split over N GPUs (image bands) + RCCL gather.
 * ``c5`` — seeded 1,048,576-triangle heightfield, 3840x2160, 64 spp (HBM stress).
 """
@@ -36,6 +37,9 @@ HW1_CONFIGS = {
 # G/ scene configurations: scene JSON + overrides (None keeps the JSON's value).
 G_CONFIGS = {
     "c3": dict(scene="frog.json", width=1920, height=1080, spp=16, max_depth=1),
+    # frog.json as shipped (max_bounces 8, diffuse bounce on) at 1080p x 16 spp: the reference's
+    # default workload (G/assets/json_files/frog.json:3, G/include/scene.h:15-19)
+    "c3b": dict(scene="frog.json", width=1920, height=1080, spp=16, max_depth=8),
     "c5": dict(scene="heightfield_c5.json", width=3840, height=2160, spp=64, max_depth=1),
 }
 

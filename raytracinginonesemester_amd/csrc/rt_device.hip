@@ -137,7 +137,8 @@ struct RenderParams {
     uint32_t heavy_ticks[4];  // NCLASS thresholds, descending
     // rt_count_rays only (LANE and DEEP kernels; null otherwise): [1] shadow rays cast, [2]
     // bounce rays traced, the classes of the oracle's orc_stats.rays ([0], camera rays, is
-    // W*H*spp by definition and counted on the host)
+    // W*H*spp by definition and counted on the host), [3] camera rays of the tiles the culling
+    // passes left to the render kernel (the camera rays that are actually traversed)
     unsigned long long* ray_count;
 };
 
@@ -961,6 +962,7 @@ template <int MODE, bool D1>
 __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int64_t aov, float* park) {
     const SceneView& sc = P.sc;
     RayPre ray = camera_ray(P, valid, x, y, s);
+    count_rays<MODE>(P.ray_count, 3, valid && P.max_depth > 0);  // camera rays that reach traversal
     if constexpr (D1) {
         HitState hs;
         traverse<MODE>(sc, ray, valid, false, 0.0f, hs);
@@ -2183,6 +2185,12 @@ struct rt_scene {
     // so frame k's pre-passes overlap frame k-1's render kernel (its tail leaves CUs idle).
     static constexpr int kRing = 256;
     hipEvent_t ev0[kRing] = {}, evm[kRing] = {}, ev1[kRing] = {}, pdone[kRing] = {};
+    // evq: recorded on the caller's stream at the start of a frame; the prep stream waits for it
+    // so the pre-passes (which write the culled tiles' pixels into the caller's buffers) come
+    // after everything the caller queued on that stream before the call.  A caller that orders
+    // its buffer reuse itself on the host (rt_renderer) sets caller_ordered and skips it.
+    hipEvent_t evq[kRing] = {};
+    bool caller_ordered = false;
     hipStream_t prep = nullptr;
     uint64_t launches = 0;
     size_t bytes = 0;
@@ -2204,6 +2212,7 @@ struct rt_scene {
             if (evm[i]) (void)hipEventDestroy(evm[i]);
             if (ev1[i]) (void)hipEventDestroy(ev1[i]);
             if (pdone[i]) (void)hipEventDestroy(pdone[i]);
+            if (evq[i]) (void)hipEventDestroy(evq[i]);
         }
         if (prep) (void)hipStreamDestroy(prep);
     }
@@ -2216,6 +2225,7 @@ struct rt_scene {
             HIP_TRY(hipEventCreate(&evm[i]));
             HIP_TRY(hipEventCreate(&ev1[i]));
             HIP_TRY(hipEventCreate(&pdone[i]));
+            HIP_TRY(hipEventCreateWithFlags(&evq[i], hipEventDisableTiming));
         }
         return RT_OK;
     }
@@ -2928,6 +2938,10 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         // set k was last read by frame k-3, set k+1 (zeroed by this cull pass) by frame k-2
         if (k >= 2) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 2), 0));
         if (k >= 1 && overlap) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 1), 0));
+        if (!s->caller_ordered) {  // stream order for the caller's buffers (see rt_scene::evq)
+            HIP_TRY(hipEventRecord(s->evq[slot], st));
+            HIP_TRY(hipStreamWaitEvent(pp, s->evq[slot], 0));
+        }
         if (s->counters_dirty) {
             HIP_TRY(hipMemsetAsync(base, 0, rt_scene::kSets * kCounterBytes, pp));
             s->counters_dirty = false;
@@ -2962,6 +2976,10 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     s->launches++;  // the events of this slot belong to this frame even when it failed
     if (rc != RT_OK) s->counters_dirty = true;
     return rc;
+}
+
+void rt::scene_set_caller_ordered(rt_scene* s, bool on) {
+    if (s) s->caller_ordered = on;
 }
 
 void rt::scene_frame_events(const rt_scene* s, hipEvent_t* first, hipEvent_t* last) {
@@ -3102,6 +3120,14 @@ extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts
 // shadow and bounce rays are counted on the device by one LANE-kernel render of the frame
 // (wave-aggregated atomics; the frame itself is discarded).  Synchronous.
 extern "C" int rt_count_rays(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, uint64_t* counts) {
+    if (!counts) return set_error(RT_ERR_ARG, "rt_count_rays: null argument");
+    uint64_t c4[4];
+    const int rc = rt_count_rays_ex(s, cam, o, c4);
+    if (rc == RT_OK) std::memcpy(counts, c4, 3 * sizeof(uint64_t));
+    return rc;
+}
+
+extern "C" int rt_count_rays_ex(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, uint64_t* counts) {
     if (!s || !cam || !o || !counts) return set_error(RT_ERR_ARG, "rt_count_rays: null argument");
     const int rows = rt_shard_rows(cam->pixel_height, o->band_rows, o->band_index, o->band_count);
     if (rows < 0) return set_error(RT_ERR_ARG, "bad band sharding parameters");
@@ -3112,9 +3138,9 @@ extern "C" int rt_count_rays(rt_scene* s, const rt_camera* cam, const rt_render_
     DevBuf rgb, cnt;
     int rc;
     if ((rc = rgb.alloc(std::max<size_t>(npx * 3 * sizeof(float), 4))) != RT_OK) return rc;
-    if ((rc = cnt.alloc(3 * sizeof(unsigned long long))) != RT_OK) return rc;
+    if ((rc = cnt.alloc(4 * sizeof(unsigned long long))) != RT_OK) return rc;
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemset(cnt.p, 0, 3 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(cnt.p, 0, 4 * sizeof(unsigned long long)));
     rt_render_opts lo = *o;
     lo.kernel = RT_KERNEL_LANE;  // deep trees take the DEEP kernels, which count too
     t_ray_count = static_cast<unsigned long long*>(cnt.p);
@@ -3122,11 +3148,12 @@ extern "C" int rt_count_rays(rt_scene* s, const rt_camera* cam, const rt_render_
     t_ray_count = nullptr;
     if (rc != RT_OK) return rc;
     HIP_TRY(hipDeviceSynchronize());
-    unsigned long long h[3] = {0, 0, 0};
+    unsigned long long h[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpy(h, cnt.p, sizeof(h), hipMemcpyDeviceToHost));
     counts[0] = o->max_depth > 0 ? uint64_t(npx) * uint64_t(o->spp) : 0;
     counts[1] = h[1];
     counts[2] = h[2];
+    counts[3] = h[3];
     return RT_OK;
 }
 

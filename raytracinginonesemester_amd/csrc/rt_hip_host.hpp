@@ -68,5 +68,9 @@ struct DeviceGuard {
 // by the scene (valid for the scene's next 255 frames); nullptr before the first frame.
 // rt_renderer synchronises on these instead of recording events of its own on that stream.
 void scene_frame_events(const rt_scene* s, hipEvent_t* first, hipEvent_t* last);
+// A caller that orders the reuse of its output buffers itself (rt_renderer: host waits per
+// frame slot) lets a scene's frame pre-passes skip the wait for the work queued before the
+// frame on its stream, so they overlap the previous frame's render kernel (rt_device.hip).
+void scene_set_caller_ordered(rt_scene* s, bool on);
 
 }  // namespace rt

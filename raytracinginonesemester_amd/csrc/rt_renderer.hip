@@ -4,11 +4,17 @@
 // inside its timed region (G/src/main.cu:362-378; render() is G/include/query.h:13-29).  Here
 // a frame is sharded over ranks as 8-row bands dealt round-robin (rank r renders bands
 // b % world == r); each rank renders its bands into a contiguous device strip
-// with the fused P6 epilogue (rt_render_device_p6), the strips reach rank 0's GPU with one
-// grouped ncclSend/ncclRecv per rank (RCCL over xGMI), and rank 0 copies every strip into a
-// pinned host frame with 2-D copies that put each band at its image rows, so no un-permute
-// pass runs.  Per rank three streams (compute, comm, copy) and per frame slot a strip buffer:
-// frame k+1 renders while frame k is gathered and copied to the host.
+// with the fused P6 epilogue (rt_render_device_p6).  The strips then reach the host frame by
+// one of three paths, all with 2-D copies that put each band at its image rows (no un-permute
+// pass):
+//  * RCCL: one grouped ncclSend/ncclRecv per rank to rank 0's GPU (xGMI), then rank 0 copies
+//    the assembled frame over its PCIe link (or keeps it in HBM, RT_DELIVER_DEVICE);
+//  * DIRECT (one process driving every GPU): each GPU copies its own bands into the pinned
+//    frame over its own PCIe link;
+//  * HOST_SHARED (one process per GPU): the same per-rank copies into a host frame shared by
+//    the processes (POSIX shared memory pinned in each), with per-rank completion words.
+// Per rank three streams (compute, comm, copy) and per frame slot a strip buffer: frame k+1
+// renders while frame k is gathered and copied to the host.
 //
 // RCCL is loaded at run time (dlopen "librccl.so.1"): in a process that has imported torch
 // this is torch's own RCCL (same soname, already loaded), otherwise the image's.
@@ -16,15 +22,23 @@
 #include <rccl/rccl.h>
 
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
+#include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
 #include <new>
 #include <set>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -98,14 +112,11 @@ int nccl_error(ncclResult_t e, const char* what) {
         if (e_ != ncclSuccess) return nccl_error(e_, #expr); \
     } while (0)
 
+
 constexpr int kTimeRing = 256;
 
 // Bands of rank r (b % world == r) in its strip, in band order, go to image rows b*band_rows.
 // The full bands are one strided 2-D copy; a partial last band (H % band_rows) a plain one.
-// (The runtime moves these bytes with blit kernels, __amd_rocclr_copyBuffer, whatever
-// GPU_BLIT_ENGINE_TYPE / HSA_ENABLE_SDMA say.  A 64-wave copy kernel of ours with 16-byte
-// non-temporal stores into the pinned frame made the render kernel beside it far slower:
-// 0.317 vs 0.251 ms per delivered c3 frame.)
 // (The runtime moves these bytes with blit kernels, __amd_rocclr_copyBuffer, whatever
 // GPU_BLIT_ENGINE_TYPE / HSA_ENABLE_SDMA say.  A 64-wave copy kernel of ours with 16-byte
 // non-temporal stores into the pinned frame made the render kernel beside it far slower:
@@ -126,6 +137,76 @@ hipError_t scatter_strip(char* dst, const char* strip, int r, int world, int H, 
         return hipMemcpyAsync(dst + size_t(full) * band, strip + size_t(nfull) * band, rows * rb, kind, st);
     }
     return hipSuccess;
+}
+
+// ---- host frames shared by the processes of a job (RT_GATHER_HOST_SHARED) --------------
+// One POSIX shared-memory segment per frame geometry: a header page of control words, then
+// `depth` frame slots.  Rank 0's process creates it; every process maps it and pins the
+// mapping with hipHostRegister, so each rank's device-to-host copy lands in the one frame.
+// Control words (64-bit, one cache line each, accessed with __atomic builtins):
+//   magic     written last by the creator: the header is complete
+//   attached  local ranks of all processes that have pinned the segment (rank 0's process
+//             unlinks the name once every rank has attached: nothing is left in /dev/shm)
+//   released  frames [0, released) are no longer held by rank 0's caller (published at rank
+//             0's submit of frame t: t - depth + 1); a rank copies frame t into its slot only
+//             when released >= t - depth + 1
+//   done[r]   frames [0, done[r]) of rank r are in the host frame (its copy finished)
+constexpr uint64_t kShmMagic = 0x31564d4652544d52ull;  // "RMTRFMV1"
+constexpr size_t kShmHeader = 8192;
+constexpr size_t kOffMagic = 0, kOffGeom = 8, kOffAttached = 64, kOffReleased = 128, kOffDone = 192;
+static_assert(kOffDone + 64 * 64 <= kShmHeader, "64 ranks of done words fit the header");
+
+struct SharedFrames {
+    std::string name;
+    char* base = nullptr;
+    size_t bytes = 0, slot_bytes = 0;
+    bool registered = false, creator = false, unlinked = false;
+
+    uint64_t* word(size_t off) const { return reinterpret_cast<uint64_t*>(base + off); }
+    uint64_t* done(int r) const { return word(kOffDone + 64 * size_t(r)); }
+    char* slot(int s) const { return base + kShmHeader + size_t(s) * slot_bytes; }
+    static uint64_t load(const uint64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+    static void raise_to(uint64_t* p, uint64_t v) {  // monotone publish (one writer per word)
+        if (__atomic_load_n(p, __ATOMIC_RELAXED) < v) __atomic_store_n(p, v, __ATOMIC_RELEASE);
+    }
+    void unlink_name() {
+        if (creator && !unlinked && !name.empty()) (void)shm_unlink(name.c_str());
+        unlinked = true;
+    }
+    void close() {
+        if (registered) (void)hipHostUnregister(base);
+        registered = false;
+        if (base) (void)munmap(base, bytes);
+        base = nullptr;
+        unlink_name();
+    }
+    ~SharedFrames() { close(); }
+};
+
+double peer_timeout_s() {
+    if (const char* e = std::getenv("RT_PEER_TIMEOUT_S")) return std::max(0.1, std::atof(e));
+    return 120.0;
+}
+
+// Spin (then yield, then sleep) until pred() holds; false on timeout.
+template <typename F>
+bool spin_until(F pred) {
+    if (pred()) return true;
+    const auto t0 = std::chrono::steady_clock::now();
+    const double limit = peer_timeout_s();
+    for (uint64_t i = 0;; ++i) {
+        if (pred()) return true;
+        if (i < 2000) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+            __builtin_ia32_pause();
+#endif
+        } else if (i < 4000) {
+            std::this_thread::yield();
+        } else {
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) return pred();
+        }
+    }
 }
 
 struct LocalRank {
@@ -161,11 +242,16 @@ struct rt_renderer {
     // rank 0's side, per slot
     std::vector<DevBuf> gathered;       // RCCL: world strips of strip_cap bytes
     std::vector<DevBuf> dev_frame;      // RT_DELIVER_DEVICE
-    std::vector<void*> host;            // pinned host frames
+    std::vector<void*> host;            // host frames: pinned (hipHostMalloc) or slots of `shared`
     std::vector<hipEvent_t> delivered;  // per slot: delivered_ev[s], or rank 0's `rendered` (deliver none)
     std::vector<hipEvent_t> delivered_ev;  // owned, on ranks[0].copy
     std::vector<uint64_t> slot_ticket;  // frame held by each slot (+1; 0 = none)
     uint64_t next = 0;
+    uint64_t first_valid = 0;           // tickets before the latest geometry change are gone
+    // RT_GATHER_HOST_SHARED: the segment of the current geometry (every process)
+    std::string shm_base;               // host_frame_name
+    uint64_t shm_gen = 0;               // geometry generation (same sequence on every process)
+    std::unique_ptr<SharedFrames> shared;
     // timing ring (rank 0's process): owned events on the comm / copy streams (gather start/end,
     // delivery start/end), and per frame and RT_TIME_* kind the (start, end) pair to read
     // (nullptr: the step did not run, 0 ms).  The frame's start is the scene's own first event.
@@ -175,9 +261,12 @@ struct rt_renderer {
 
     ~rt_renderer() { release(); }
     void release_buffers() {
-        for (void* h : host)
-            if (h) (void)hipHostFree(h);
+        if (!shared) {
+            for (void* h : host)
+                if (h) (void)hipHostFree(h);
+        }
         host.clear();
+        shared.reset();
         gathered.clear();
         dev_frame.clear();
         for (LocalRank& L : ranks) {
@@ -220,6 +309,7 @@ struct rt_renderer {
         ranks.clear();
     }
     bool uses_rccl() const { return gather == RT_GATHER_RCCL && deliver != RT_DELIVER_NONE; }
+    bool host_shared() const { return gather == RT_GATHER_HOST_SHARED && deliver != RT_DELIVER_NONE; }
     size_t elem() const { return deliver == RT_DELIVER_F32 ? sizeof(float) : 1; }
 };
 
@@ -273,7 +363,83 @@ int init_comms(rt_renderer* r, const rt_renderer_opts* o) {
     return RT_OK;
 }
 
-// (Re)size every buffer for a W x H frame.  Waits for the frames in flight first.
+// Create (rank 0's process) or attach to (the others) the shared frames of the current
+// geometry, pinned for device-to-host copies.
+int open_shared(rt_renderer* r) {
+    auto sf = std::make_unique<SharedFrames>();
+    sf->name = r->shm_base + ".g" + std::to_string(r->shm_gen);
+    sf->slot_bytes = (std::max<size_t>(r->frame_bytes, 1) + 4095) / 4096 * 4096;
+    sf->bytes = kShmHeader + size_t(r->depth) * sf->slot_bytes;
+    sf->creator = r->rank0_local;
+    const uint64_t geom = (uint64_t(r->frame_bytes) << 16) ^ (uint64_t(r->depth) << 8) ^ uint64_t(r->world);
+    if (sf->creator) {
+        (void)shm_unlink(sf->name.c_str());  // a segment left by a crashed job of the same name
+        const int fd = shm_open(sf->name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0) return set_error(RT_ERR_IO, "shm_open " + sf->name + ": " + std::strerror(errno));
+        if (ftruncate(fd, off_t(sf->bytes)) != 0) {
+            const int e = errno;
+            ::close(fd);
+            (void)shm_unlink(sf->name.c_str());
+            return set_error(RT_ERR_NOMEM, "ftruncate " + sf->name + ": " + std::strerror(e));
+        }
+        void* p = mmap(nullptr, sf->bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        ::close(fd);
+        if (p == MAP_FAILED) {
+            (void)shm_unlink(sf->name.c_str());
+            return set_error(RT_ERR_NOMEM, "mmap " + sf->name + ": " + std::strerror(errno));
+        }
+        sf->base = static_cast<char*>(p);
+        *sf->word(kOffGeom) = geom;
+        __atomic_store_n(sf->word(kOffMagic), kShmMagic, __ATOMIC_RELEASE);
+    } else {
+        int err = 0;
+        const bool ok = spin_until([&] {
+            const int fd = shm_open(sf->name.c_str(), O_RDWR, 0600);
+            if (fd < 0) return false;
+            struct stat st;
+            if (fstat(fd, &st) != 0 || size_t(st.st_size) < sf->bytes) {
+                ::close(fd);
+                return false;
+            }
+            void* p = mmap(nullptr, sf->bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            ::close(fd);
+            if (p == MAP_FAILED) {
+                err = errno;
+                return false;
+            }
+            char* b = static_cast<char*>(p);
+            if (__atomic_load_n(reinterpret_cast<uint64_t*>(b + kOffMagic), __ATOMIC_ACQUIRE) != kShmMagic) {
+                (void)munmap(p, sf->bytes);
+                return false;
+            }
+            sf->base = b;
+            return true;
+        });
+        if (!ok)
+            return set_error(RT_ERR_COMM, "rank " + std::to_string(r->ranks[0].rank) + ": shared frame " + sf->name +
+                                              " not created by rank 0's process" +
+                                              (err ? std::string(" (mmap: ") + std::strerror(err) + ")" : ""));
+        if (*sf->word(kOffGeom) != geom)
+            return set_error(RT_ERR_ARG, "shared frame " + sf->name + ": processes disagree on frame size / depth / world");
+    }
+    HIP_TRY(hipHostRegister(sf->base, sf->bytes, hipHostRegisterPortable));
+    sf->registered = true;
+    __atomic_fetch_add(sf->word(kOffAttached), uint64_t(r->ranks.size()), __ATOMIC_ACQ_REL);
+    r->host.assign(r->depth, nullptr);
+    for (int s = 0; s < r->depth; ++s) r->host[s] = sf->slot(s);
+    r->shared = std::move(sf);
+    return RT_OK;
+}
+
+// Rank 0's process: remove the segment's name once every rank has pinned it.
+void maybe_unlink(rt_renderer* r) {
+    SharedFrames* sf = r->shared.get();
+    if (sf && sf->creator && !sf->unlinked && SharedFrames::load(sf->word(kOffAttached)) >= uint64_t(r->world))
+        sf->unlink_name();
+}
+
+// (Re)size every buffer for a W x H frame.  Waits for the frames in flight first; tickets
+// submitted before the change can no longer be waited for.
 int ensure_geometry(rt_renderer* r, int W, int H) {
     if (r->W == W && r->H == H && !r->ranks[0].strip.empty()) return RT_OK;
     for (LocalRank& L : r->ranks) {
@@ -283,6 +449,7 @@ int ensure_geometry(rt_renderer* r, int W, int H) {
         HIP_TRY(hipStreamSynchronize(L.copy));
     }
     r->release_buffers();
+    r->first_valid = r->next;
     r->W = W;
     r->H = H;
     r->row_bytes = size_t(W) * 3 * r->elem();
@@ -300,6 +467,12 @@ int ensure_geometry(rt_renderer* r, int W, int H) {
         std::fill(L.released.begin(), L.released.end(), nullptr);
     }
     std::fill(r->delivered.begin(), r->delivered.end(), nullptr);
+    std::fill(r->slot_ticket.begin(), r->slot_ticket.end(), 0);
+    if (r->host_shared()) {
+        ++r->shm_gen;
+        DeviceGuard g(r->ranks[0].device);
+        if ((rc = open_shared(r)) != RT_OK) return rc;
+    }
     if (r->rank0_local) {
         DeviceGuard g(r->ranks[0].device);
         if (r->uses_rccl()) {
@@ -311,14 +484,20 @@ int ensure_geometry(rt_renderer* r, int W, int H) {
             r->dev_frame.resize(r->depth);
             for (DevBuf& b : r->dev_frame)
                 if ((rc = b.alloc(std::max<size_t>(r->frame_bytes, 1))) != RT_OK) return rc;
-        } else if (r->deliver != RT_DELIVER_NONE) {
+        } else if (r->deliver != RT_DELIVER_NONE && !r->host_shared()) {
             r->host.assign(r->depth, nullptr);
             for (void*& h : r->host)
                 HIP_TRY(hipHostMalloc(&h, std::max<size_t>(r->frame_bytes, 1), hipHostMallocPortable));
         }
     }
-    std::fill(r->slot_ticket.begin(), r->slot_ticket.end(), 0);
     return RT_OK;
+}
+
+// HOST_SHARED: this process's ranks have frame `ticket` in the host frame (their copies are
+// complete: the caller synchronised on them).
+void publish_done(rt_renderer* r, uint64_t ticket) {
+    if (!r->shared) return;
+    for (const LocalRank& L : r->ranks) SharedFrames::raise_to(r->shared->done(L.rank), ticket + 1);
 }
 
 // Host wait until slot s may be reused (its previous frame fully delivered / released).
@@ -332,6 +511,7 @@ int wait_slot(rt_renderer* r, int s) {
         DeviceGuard g(r->ranks[0].device);
         HIP_TRY(hipEventSynchronize(r->delivered[s]));
     }
+    publish_done(r, r->slot_ticket[s] - 1);
     return RT_OK;
 }
 
@@ -348,24 +528,34 @@ extern "C" int rt_renderer_create(size_t P, const rt_bvh_node* nodes, const rt_a
     const int n = o->n_devices;
     if (n < 1 || n > 64) return set_error(RT_ERR_ARG, "n_devices must be in 1..64");
     const int world = o->world_size > 0 ? o->world_size : n;
-    if (world < n || o->rank0 < 0 || o->rank0 + n > world)
-        return set_error(RT_ERR_ARG, "bad world_size / rank0 for n_devices");
-    if (world > n && !o->unique_id) return set_error(RT_ERR_ARG, "a multi-process renderer needs unique_id");
+    if (world < n || world > 64 || o->rank0 < 0 || o->rank0 + n > world)
+        return set_error(RT_ERR_ARG, "bad world_size / rank0 for n_devices (world_size <= 64)");
     if (o->band_rows < 1) return set_error(RT_ERR_ARG, "band_rows must be >= 1");
     if (o->deliver < RT_DELIVER_P6 || o->deliver > RT_DELIVER_NONE) return set_error(RT_ERR_ARG, "bad deliver");
-    if (o->gather < RT_GATHER_AUTO || o->gather > RT_GATHER_DIRECT) return set_error(RT_ERR_ARG, "bad gather");
+    if (o->gather < RT_GATHER_AUTO || o->gather > RT_GATHER_HOST_SHARED) return set_error(RT_ERR_ARG, "bad gather");
     const int depth = o->depth == 0 ? 3 : o->depth;
     if (depth < 1 || depth > 8) return set_error(RT_ERR_ARG, "depth must be in 1..8");
     std::vector<int> devs(n);
     for (int i = 0; i < n; ++i) devs[i] = o->devices ? o->devices[i] : i;
     const bool distinct = std::set<int>(devs.begin(), devs.end()).size() == size_t(n);
+    const bool named = o->host_frame_name && o->host_frame_name[0];
     int gather = o->gather;
-    if (gather == RT_GATHER_AUTO) gather = (world > 1 && distinct) ? RT_GATHER_RCCL : RT_GATHER_DIRECT;
+    if (gather == RT_GATHER_AUTO) {
+        if (world == n) gather = RT_GATHER_DIRECT;
+        else gather = named ? RT_GATHER_HOST_SHARED : RT_GATHER_RCCL;
+    }
     if ((o->flags & RT_RENDERER_SELF_SEND) && o->gather == RT_GATHER_AUTO) gather = RT_GATHER_RCCL;
     if (gather == RT_GATHER_DIRECT && world > n)
         return set_error(RT_ERR_UNSUPPORTED, "RT_GATHER_DIRECT needs every rank in this process");
     if (gather == RT_GATHER_RCCL && !distinct)
         return set_error(RT_ERR_UNSUPPORTED, "RCCL needs one rank per device; use RT_GATHER_DIRECT for repeated ids");
+    if (gather == RT_GATHER_HOST_SHARED) {
+        if (!named || o->host_frame_name[0] != '/' || std::strchr(o->host_frame_name + 1, '/') ||
+            std::strlen(o->host_frame_name) > 200)
+            return set_error(RT_ERR_ARG, "RT_GATHER_HOST_SHARED needs host_frame_name \"/name\" (no other '/')");
+        if (o->deliver == RT_DELIVER_DEVICE)
+            return set_error(RT_ERR_UNSUPPORTED, "RT_DELIVER_DEVICE needs RCCL (the frame is assembled on rank 0's GPU)");
+    }
     for (int i = 0; i < n; ++i) {
         int rc = check_device(devs[i]);
         if (rc != RT_OK) return rc;
@@ -379,6 +569,7 @@ extern "C" int rt_renderer_create(size_t P, const rt_bvh_node* nodes, const rt_a
     r->depth = depth;
     r->flags = o->flags;
     r->rank0_local = o->rank0 == 0;
+    if (named) r->shm_base = o->host_frame_name;
     r->ranks.resize(n);
     r->slot_ticket.assign(depth, 0);
     int rc;
@@ -391,6 +582,9 @@ extern "C" int rt_renderer_create(size_t P, const rt_bvh_node* nodes, const rt_a
         if (i == 0) rc = rt_scene_create(L.device, P, nodes, aabbs, tris, objids, mats, nmat, lights, nlights, &L.scene);
         else rc = rt_scene_clone(r->ranks[0].scene, L.device, &L.scene);
         if (rc != RT_OK) return rc;
+        // the renderer waits for buffer reuse on the host: its frames skip the scene's wait for
+        // work queued before them on the compute stream (there is none but its own frames)
+        rt::scene_set_caller_ordered(L.scene, true);
         HIP_TRY(hipStreamCreateWithFlags(&L.compute, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&L.comm, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking));
@@ -434,7 +628,11 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
     const bool f32 = r->deliver == RT_DELIVER_F32;
     const bool rccl_mode = r->uses_rccl();
     const bool self_send = rccl_mode && (r->flags & RT_RENDERER_SELF_SEND);
+    const bool shared = r->host_shared();
     LocalRank& R0 = r->ranks[0];
+    // HOST_SHARED: rank 0's caller gives up frame t - depth with this submit
+    if (shared && r->rank0_local && t + 1 >= uint64_t(r->depth))
+        SharedFrames::raise_to(r->shared->word(kOffReleased), t + 1 - uint64_t(r->depth));
     for (int k = 0; k < 3; ++k) r->ta[k][ring] = r->tb[k][ring] = nullptr;
     // 1. every local rank renders its bands into strip[s]: the scene's frame and nothing else
     for (LocalRank& L : r->ranks) {
@@ -464,7 +662,7 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
     }
     const hipMemcpyKind kind = r->deliver == RT_DELIVER_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     char* dst = nullptr;
-    if (r->rank0_local)
+    if (r->rank0_local || shared)
         dst = static_cast<char*>(r->deliver == RT_DELIVER_DEVICE ? r->dev_frame[s].p : r->host[s]);
     if (rccl_mode) {
         // 2. strips -> rank 0 (one group: every send and receive of this process)
@@ -529,8 +727,16 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
         }
         return RT_OK;
     }
-    // 2'. DIRECT: every local rank copies its own bands into the frame (all ranks are local)
-    {
+    // 2'. DIRECT / HOST_SHARED: every local rank copies its own bands into the frame.  With a
+    // frame shared by the job's processes, a rank other than 0's first waits for rank 0's caller
+    // to give up this slot's previous frame (rank 0 publishes that at its submit of frame t).
+    if (shared && !r->rank0_local && t + 1 >= uint64_t(r->depth)) {
+        const uint64_t need = t + 1 - uint64_t(r->depth);
+        if (!spin_until([&] { return SharedFrames::load(r->shared->word(kOffReleased)) >= need; }))
+            return set_error(RT_ERR_COMM, "rank " + std::to_string(R0.rank) + ": rank 0 did not release frame " +
+                                              std::to_string(t - uint64_t(r->depth)) + " within RT_PEER_TIMEOUT_S");
+    }
+    if (r->rank0_local) {
         DeviceGuard g(R0.device);
         if (R0.rendered[s]) HIP_TRY(hipStreamWaitEvent(R0.copy, R0.rendered[s], 0));
         HIP_TRY(hipEventRecord(r->td0[ring], R0.copy));
@@ -538,17 +744,18 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
     for (LocalRank& L : r->ranks) {
         if (!L.rendered[s]) continue;
         DeviceGuard g(L.device);
-        if (&L != &R0) HIP_TRY(hipStreamWaitEvent(L.copy, L.rendered[s], 0));
+        const bool own = &L == &R0 && r->rank0_local;  // rank 0's copy: delivered_ev below
+        if (!own) HIP_TRY(hipStreamWaitEvent(L.copy, L.rendered[s], 0));
         HIP_TRY(scatter_strip(dst, static_cast<const char*>(L.strip[s].p), L.rank, r->world, r->H, r->band_rows,
                               r->row_bytes, kind, L.copy));
-        if (&L != &R0) {
+        if (!own) {
             HIP_TRY(hipEventRecord(L.released_ev[s], L.copy));
             L.released[s] = L.released_ev[s];
         }
     }
-    {
+    if (r->rank0_local) {
         DeviceGuard g(R0.device);
-        for (size_t i = 1; i < r->ranks.size(); ++i)  // the frame is complete when every copy is
+        for (size_t i = 1; i < r->ranks.size(); ++i)  // the frame is complete when every local copy is
             if (r->ranks[i].released[s]) HIP_TRY(hipStreamWaitEvent(R0.copy, r->ranks[i].released[s], 0));
         HIP_TRY(hipEventRecord(r->td1[ring], R0.copy));
         HIP_TRY(hipEventRecord(r->delivered_ev[s], R0.copy));
@@ -556,6 +763,12 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
         if (R0.rendered[s]) R0.released[s] = r->delivered_ev[s];
         r->ta[RT_TIME_DELIVER][ring] = r->td0[ring];
         r->tb[RT_TIME_DELIVER][ring] = r->tb[RT_TIME_FRAME][ring] = r->td1[ring];
+    }
+    if (shared) {
+        maybe_unlink(r);
+        // ranks with no rows have nothing to copy: their share of frame t is complete
+        for (const LocalRank& L : r->ranks)
+            if (!L.rendered[s]) SharedFrames::raise_to(r->shared->done(L.rank), t + 1);
     }
     return RT_OK;
 }
@@ -566,6 +779,8 @@ extern "C" int rt_renderer_wait(rt_renderer* r, uint64_t ticket, const void** fr
     if (!r) return set_error(RT_ERR_ARG, "rt_renderer_wait: null renderer");
     if (ticket >= r->next || ticket + uint64_t(r->depth) < r->next)
         return set_error(RT_ERR_ARG, "rt_renderer_wait: frame not submitted or no longer held");
+    if (ticket < r->first_valid)
+        return set_error(RT_ERR_ARG, "rt_renderer_wait: frame submitted before a change of the frame size");
     const int s = int(ticket % uint64_t(r->depth));
     for (LocalRank& L : r->ranks) {
         DeviceGuard g(L.device);
@@ -575,6 +790,20 @@ extern "C" int rt_renderer_wait(rt_renderer* r, uint64_t ticket, const void** fr
     if (r->rank0_local) {
         DeviceGuard g(r->ranks[0].device);
         if (r->delivered[s]) HIP_TRY(hipEventSynchronize(r->delivered[s]));
+    }
+    if (r->host_shared()) {
+        publish_done(r, ticket);
+        maybe_unlink(r);
+        if (r->rank0_local) {  // every rank's bands are in the frame
+            for (int q = 0; q < r->world; ++q) {
+                const uint64_t* w = r->shared->done(q);
+                if (!spin_until([&] { return SharedFrames::load(w) >= ticket + 1; }))
+                    return set_error(RT_ERR_COMM, "rank " + std::to_string(q) + " did not deliver frame " +
+                                                      std::to_string(ticket) + " within RT_PEER_TIMEOUT_S");
+            }
+        }
+    }
+    if (r->rank0_local) {
         if (r->deliver == RT_DELIVER_DEVICE) {
             if (frame) *frame = r->dev_frame[s].p;
             if (bytes) *bytes = r->frame_bytes;
@@ -637,6 +866,7 @@ extern "C" int rt_render_reference_gpus(size_t P, int W, int H, const rt_camera*
     rt_renderer_opts_default(&ro);
     ro.n_devices = n_gpus;
     ro.deliver = RT_DELIVER_F32;
+    ro.gather = n_gpus > 1 ? RT_GATHER_RCCL : RT_GATHER_DIRECT;  // float strips gathered to device 0
     ro.depth = 1;
     rt_renderer* r = nullptr;
     int rc = rt_renderer_create(P, nodes, aabbs, tris, objids, mats, nmat, lights, nlights, &ro, &r);

@@ -54,6 +54,7 @@ G_SCENES = {
     "sphere_single": "sphere_single.json",
     "cornell": "cornell.json",
     "c5_small": "heightfield_c5.json",
+    "c3b_small": "frog.json",
 }
 
 

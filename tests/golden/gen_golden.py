@@ -36,6 +36,9 @@ G_FIXTURES = {
     "sphere_single": ("sphere_single.json", 160, 90, 4, 0, True),
     "cornell": ("cornell.json", 160, 120, 4, 0, True),
     "c5_small": ("heightfield_c5.json", 384, 216, 4, 1, True),
+    # c3b: frog.json's own max_bounces 8 (diffuse bounce), 16 spp (bench config c3b)
+    "c3b_small": ("frog.json", 192, 108, 16, 0, True),
+    "c3b_full": ("frog.json", 1920, 1080, 16, 0, False),
 }
 # HW1 fixtures: name -> (config, W, H)
 HW1_FIXTURES = {
@@ -43,7 +46,7 @@ HW1_FIXTURES = {
     "c2_small": ("c2", 160, 120),
     "c2_full": ("c2", 640, 480),
 }
-PPM_OF = {"c1_full", "c2_full", "c3_full", "c3_small"}
+PPM_OF = {"c1_full", "c2_full", "c3_full", "c3_small", "c3b_full"}
 
 
 def sha256(p: Path) -> str:

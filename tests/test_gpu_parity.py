@@ -54,7 +54,7 @@ def _check_fb(rgb, ref, exact_frac=1.0):
 
 @pytest.mark.parametrize("flags", [0, rt._lib.RT_FLAG_BINARY])
 @pytest.mark.parametrize("kernel", KERNELS)
-@pytest.mark.parametrize("name", ["c3_small", "frog_bounce", "sphere_single", "cornell", "c5_small"])
+@pytest.mark.parametrize("name", ["c3_small", "frog_bounce", "sphere_single", "cornell", "c5_small", "c3b_small"])
 def test_golden_scene_parity(name, kernel, flags):
     meta = golden_meta(name)
     scene = G_SCENES[name]
@@ -70,7 +70,7 @@ def test_golden_scene_parity(name, kernel, flags):
     _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
 
 
-@pytest.mark.parametrize("name", ["c3_small", "frog_bounce", "sphere_single", "cornell"])
+@pytest.mark.parametrize("name", ["c3_small", "frog_bounce", "sphere_single", "cornell", "c3b_small"])
 def test_ray_counts_match_oracle(name):
     """rt_count_rays (total rays/s): camera, shadow and bounce rays of a frame
     equal the oracle's counters (orc_stats.rays; shadow = IsInShadow calls that cast a ray,
@@ -104,7 +104,11 @@ def test_ray_counts_c3_full_frame():
                          hs.tri_object_ids, hs.materials, hs.lights, spp=cfg["spp"], max_depth=cfg["max_depth"],
                          stats=True)
     assert [got["camera"], got["shadow"], got["bounce"]] == list(st["rays"])
-    assert got == {"camera": 33_177_600, "shadow": 687_530, "bounce": 0}
+    assert {k: got[k] for k in ("camera", "shadow", "bounce")} == {"camera": 33_177_600, "shadow": 687_530,
+                                                                  "bounce": 0}
+    # camera rays actually traversed (the tiles culling leaves): at least every primary hit
+    # (1,064,872 samples hit, tests/golden/scenes/c3_full), whole 4x4x16 tiles
+    assert 1_064_872 <= got["camera_traced"] < got["camera"] and got["camera_traced"] % 256 == 0
     parts = [ds.count_rays(cam, spp=cfg["spp"], max_depth=cfg["max_depth"], band_index=b, band_count=4)
              for b in range(4)]
     assert sum(q["shadow"] for q in parts) == got["shadow"]
@@ -166,6 +170,20 @@ def test_c3_full_frame_matches_reference(flags, tiles):
     assert len(mine) == len(ppm) and mine[:17] == ppm[:17]
     diff = np.abs(np.frombuffer(mine[17:], np.uint8).astype(int) - np.frombuffer(ppm[17:], np.uint8).astype(int))
     assert diff.max() <= 1
+
+
+def test_c3b_full_frame_matches_reference():
+    """c3b: frog.json as shipped (max_bounces 8, diffuse bounces) at 1920x1080x16 against the
+    reference's own full-size outputs (hit AOVs by sha256, float frame, P6 file)."""
+    meta = golden_meta("c3b_full")
+    assert meta["max_depth"] == 8 and meta["diffuse_bounce"] == 1
+    hs = host_scene("frog.json")
+    cam = hs.camera(1920, 1080)
+    rgb, hi, ht = _device_scene("frog.json").render(cam, spp=16, max_depth=8, aov=True)
+    assert hashlib.sha256(hi.tobytes()).hexdigest() == meta["sha256"]["hits.i32"]
+    assert hashlib.sha256(ht.tobytes()).hexdigest() == meta["sha256"]["hitt.f32"]
+    _check_fb(rgb, golden_array("c3b_full", "fb.f32.gz", np.float32))
+    assert rt.encode_p6(rgb) == gzip.open(GOLDEN / "scenes" / "c3b_full" / "image.ppm.gz").read()
 
 
 @pytest.mark.parametrize("env", [{}, {"RT_HEAVY_CAP": "8"}, {"RT_HEAVY_FRAC": "0.0001"}])

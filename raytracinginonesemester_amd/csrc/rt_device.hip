@@ -57,7 +57,6 @@ constexpr int BLOCK = 256;
 // Kernel instantiation flag on top of RT_KERNEL_WAVE: traverse the 4-ary records (SceneView::wide).
 // A compile-time choice, so each kernel holds one traversal loop per ray kind.
 constexpr int MODE_WIDE = 16;
-constexpr int MODE_PACKED = 32;  // box tests with packed FMAs (box_ends_pk): the big-scene kernels
 // Trees whose DFS needs more than STACK_CAP entries: SearchBVH literally, per lane, with the
 // reference's 512-entry stack, its overflow rule and brute-force completion (traverse_deep).
 constexpr int MODE_DEEP = 64;
@@ -114,7 +113,6 @@ struct RenderParams {
     uint32_t* live_count;                             // [k * COUNTER_STRIDE], tile_cull_kernel
     int32_t* live_tiles;                              // nqueues lists of queue_cap entries
     int32_t* cut_tiles;   // tile_cut_kernel's survivors (not culled, not heavy), per list (sc.ncut > 0)
-    uint8_t* cut_flag;    // per cull-list slot: 1 = culled by tile_cut_kernel (the big-scene kernels' form)
     uint32_t* next_count; // the other counter set, zeroed by tile_cull_kernel for the next frame
     int32_t cut_force;    // test every candidate in tile_cut_kernel (no pass-through)
     int32_t nqueues;
@@ -278,11 +276,8 @@ __device__ __forceinline__ BoxP leaf_box(const NodeRec& r) {
 // box_hit for the lanes in `act` (a wave mask; all lanes call it), as the mask of lanes that
 // pass: the float pre-classification for everyone, the exact double test only behind a
 // wave-uniform branch taken when some lane is ambiguous.
-template <bool PK = false>
 __device__ __forceinline__ uint64_t box_hit_mask(const RayPre& r, const BoxP& b, float tmax, uint64_t act) {
-    AxisEnds e;
-    if constexpr (PK) e = box_ends_pk(r, b);
-    else e = box_ends(r, b);
+    const AxisEnds e = box_ends(r, b);
     const BoxEnds c = box_lc_hc(e, kRayTMin, tmax);
     uint64_t hit = ballot(box_sure_hit1(r, c)) & act;
     uint64_t amb = act & ~(hit | ballot(box_miss(c)));
@@ -293,13 +288,9 @@ __device__ __forceinline__ uint64_t box_hit_mask(const RayPre& r, const BoxP& b,
     if (amb == 0) return hit;
     RT_STAT(12, 1);
     // double(tmin), double(FLT_MAX): made here (RT_KF64), not hoisted into spilled VGPR pairs
-#ifndef RT_EXP_NO_KF64
     RT_KF64(tmin_d, (double)kRayTMin)
     RT_KF64(fltmax_d, (double)FLT_MAX)
     const double tmax_d = tmax == FLT_MAX ? fltmax_d : (double)tmax;
-#else
-    const double tmin_d = (double)kRayTMin, tmax_d = (double)tmax;
-#endif
     return hit | (ballot(box_hit_exact(r, b, tmin_d, tmax_d)) & amb);
 }
 
@@ -325,188 +316,28 @@ struct HitState {
 #endif
 };
 
-#ifdef RT_EXP_LDS_TOP
-// Experiment (north_star "LDS-staged BVH-node tiles"): the first RT_EXP_LDS_TOP 4-ary records in
-// BFS order of the 4-ary tree (internal refs renumbered so, rt_scene_create) are staged in LDS
-// by every render block and read from there (ds_read_b128 + v_readfirstlane) instead of through
-// the scalar cache.  Measured slower; see DESIGN.md §4.6.
-__shared__ float4 g_lds_top[8 * RT_EXP_LDS_TOP];
-#endif
-
 // ---- WAVE traversal ---------------------------------------------------------------------
-// Every lane of the wave must call this (uniform control flow); `active` selects the
-// lanes that own a ray.  any_hit_dist > 0: shadow query — a lane stops as soon as its
-// bestT < dist (bestT only decreases, so the reference's final `hit && t < dist` is then
-// already true); the traversal order up to that point is the reference's.
-template <bool WIDE, bool PK>
-__device__ __forceinline__ void traverse_wave_impl(const SceneView& sc, const RayPre& r, bool active,
-                                                   bool any_hit, float any_hit_dist, HitState& hs) {
-    const uint32_t lane = lane_id();
-    const uint64_t lane_bit = 1ull << lane;
-    uint64_t alive = ballot(active);
-    hs.bestT = FLT_MAX;
-    hs.slot = -1;
-#ifdef RT_STATS
-    hs.pops = 0;
-#endif
-    if (alive == 0) return;
-    [[maybe_unused]] const int so = any_hit ? 1 : 0;
-    RT_STAT(0 + so, 1);
-    RT_STAT(13 + so, __popcll(alive));
-    // The root's pop-time test (SearchBVH tests every popped node, query.h:252-254) is made
-    // here with the initial bestT, before the loop, so the loop never needs the root box.
-    const uint64_t root_mask = box_hit_mask<PK>(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
-    if (root_mask == 0) {
-        if (!any_hit) RT_STAT(17, 1);
-        return;
-    }
-#ifdef RT_EXP_ROOT_ONLY  // timing experiments only (wrong output): stop after the root test
-    return;
-#endif
-    uint32_t st_ref = 0, st_mlo = 0, st_mhi = 0, st_ver = 0;  // lane k holds entry k
-    int sp = 0;
-    uint32_t wave_ver = 0;
-    st_ref = wrlane(sc.root_ref, 0, st_ref);
-    st_mlo = wrlane((uint32_t)root_mask, 0, st_mlo);
-    st_mhi = wrlane((uint32_t)(root_mask >> 32), 0, st_mhi);
-    st_ver = wrlane(wave_ver, 0, st_ver);
-    sp = 1;
-    while (sp > 0) {
-        --sp;
-        const uint32_t ref = rdlane(st_ref, sp);
-        uint64_t mask = ((uint64_t)rdlane(st_mhi, sp) << 32) | rdlane(st_mlo, sp);
-        const uint32_t ver = rdlane(st_ver, sp);
-        mask &= alive;
-        RT_STAT(2 + so, 1);
-#ifdef RT_STATS
-        ++hs.pops;
-#endif
-        if (mask == 0) continue;
-        RT_STAT(4 + so, 1);
-        bool act = (mask & lane_bit) != 0;
-        const bool leaf = (ref & LEAF_BIT) != 0;
-        const float4* L = sc.leaf + 4 * (size_t)(ref & ~LEAF_BIT);
-        if (ver != wave_ver) {  // some lane's bestT changed since the push: pop-time re-test
-            RT_STAT(6 + so, 1);
-            BoxP ob;
-            if (leaf) {
-                const float4 c = ldc(L + 2), d = ldc(L + 3);
-                ob = BoxP{hi2(c), lo2(d), hi2(d)};
-            } else {
-                ob = own_box(sc, ref, false);
-            }
-            mask = box_hit_mask<PK>(r, ob, hs.bestT, mask);
-            if (mask == 0) continue;
-            act = (mask & lane_bit) != 0;
-        }
-        if (leaf) {
-            RT_STAT(10 + so, 1);
-#ifdef RT_STATS
-            if (sp > 0 && (rdlane(st_ref, sp - 1) & LEAF_BIT)) RT_STAT(18 + so, 1);  // next pop a leaf too
-#endif
-            const uint32_t slot = ref & ~LEAF_BIT;
-            const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
-            float t, u, v;
-            const bool h = act && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin,
-                                       hs.bestT, t, u, v);
-            if (h) {
-                hs.bestT = t;
-                hs.slot = (int32_t)slot;
-            }
-            const uint64_t hm = ballot(h);
-            if (hm != 0) {
-                ++wave_ver;
-                if (any_hit) alive &= ~ballot(h && t < any_hit_dist);
-            }
-            continue;
-        }
-        RT_STAT(8 + so, 1);
-        if constexpr (WIDE) {
-            // 4-ary record: up to four entries in push order, each pushed if some lane passes.
-            // The whole record in one round trip: the seven 16-byte scalar loads are issued
-            // together and waited for once (the empty asm keeps the compiler from sinking each
-            // load next to its child's test, one load + wait per child).
-            const float4* W = sc.wnode + 8 * (size_t)ref;
-            vf4 wq[7];
-#ifdef RT_EXP_LDS_TOP
-            if (ref < RT_EXP_LDS_TOP) {
-#pragma unroll
-                for (int k = 0; k < 7; ++k) {
-                    const float4 v = g_lds_top[8 * ref + k];
-                    wq[k] = (vf4){__builtin_bit_cast(float, uni(__float_as_uint(v.x))),
-                                  __builtin_bit_cast(float, uni(__float_as_uint(v.y))),
-                                  __builtin_bit_cast(float, uni(__float_as_uint(v.z))),
-                                  __builtin_bit_cast(float, uni(__float_as_uint(v.w)))};
-                }
-            } else
-#endif
-#pragma unroll
-            for (int k = 0; k < 7; ++k) wq[k] = ldc_v(W + k);
-            asm volatile("" ::"s"(wq[0]), "s"(wq[1]), "s"(wq[2]), "s"(wq[3]), "s"(wq[4]), "s"(wq[5]), "s"(wq[6]));
-            const uint32_t refs[4] = {__float_as_uint(wq[6].x), __float_as_uint(wq[6].y), __float_as_uint(wq[6].z),
-                                      __float_as_uint(wq[6].w)};
-            float4 wv[6];
-#pragma unroll
-            for (int k = 0; k < 6; ++k) wv[k] = make_float4(wq[k].x, wq[k].y, wq[k].z, wq[k].w);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (refs[k] == NO_REF) continue;
-                const float4 p = wv[(3 * k) / 2], q = wv[(3 * k) / 2 + 1];
-                const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
-                const uint64_t mk_ = box_hit_mask<PK>(r, bk, hs.bestT, mask);
-                if (mk_ != 0) {
-                    st_ref = wrlane(refs[k], sp, st_ref);
-                    st_mlo = wrlane((uint32_t)mk_, sp, st_mlo);
-                    st_mhi = wrlane((uint32_t)(mk_ >> 32), sp, st_mhi);
-                    st_ver = wrlane(wave_ver, sp, st_ver);
-                    ++sp;
-                }
-            }
-            continue;
-        }
-        const float4* N = sc.inode + 4 * (size_t)ref;
-        const float4 q0 = ldc(N), q1 = ldc(N + 1), q2 = ldc(N + 2);
-        const uint4 q3 = ldc_u(N + 3);
-        const uint32_t lref = q3.x, rref = q3.y;
-        if (lref != NO_REF) {
-            const uint64_t ml = box_hit_mask<PK>(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
-            if (ml != 0) {
-                st_ref = wrlane(lref, sp, st_ref);
-                st_mlo = wrlane((uint32_t)ml, sp, st_mlo);
-                st_mhi = wrlane((uint32_t)(ml >> 32), sp, st_mhi);
-                st_ver = wrlane(wave_ver, sp, st_ver);
-                ++sp;
-            }
-        }
-        if (rref != NO_REF) {
-            const uint64_t mr = box_hit_mask<PK>(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
-            if (mr != 0) {
-                st_ref = wrlane(rref, sp, st_ref);
-                st_mlo = wrlane((uint32_t)mr, sp, st_mlo);
-                st_mhi = wrlane((uint32_t)(mr >> 32), sp, st_mhi);
-                st_ver = wrlane(wave_ver, sp, st_ver);
-                ++sp;
-            }
-        }
-    }
-}
-
-// traverse_wave_impl for the 7-wave (unpacked) kernels, c3's: the same tests in the same order,
-// with fewer scalar instructions per entry (the scalar unit, one per CU, and the v_readlane /
-// v_writelane it shares are the kernel's busiest pipe: DESIGN.md §4.2, §5):
+// One DFS per wavefront over a shared stack held in three VGPRs (entry k in lane k: node ref
+// and the 64-bit mask of the lanes that pushed it; push = v_writelane, pop = v_readlane).  The
+// reference's order (push left then right, pop right first) does not depend on the ray, so
+// every lane's sequence of tests is a subsequence of the wave's, made with exactly the bestT the
+// reference would hold.  Every lane of the wave must call this (uniform control flow); `active`
+// selects the lanes that own a ray.  any_hit: shadow query, a lane stops as soon as its bestT <
+// any_hit_dist (bestT only decreases, so the reference's final `hit && t < dist` is decided).
+// The per-CU scalar unit (which also issues v_readlane / v_writelane) is the kernel's busiest
+// pipe, so the loop is written for few scalar instructions per entry:
 // - the entry in hand: after an internal record, the last entry it would push (the one the
 //   reference pops next) stays in SGPRs and is processed at once, skipping its push and pop.
 //   Nothing runs between its test and its processing, so it needs no re-test;
 // - a stale watermark instead of a per-entry version lane: entries [0, stale) were pushed
 //   before the latest bestT change of some lane and take the pop-time re-test.  A hit sets
 //   stale = sp, and a re-tested pop at index sp lowers it to sp, so stale <= sp and what is
-//   pushed next is fresh;
+//   pushed next is fresh (pop-time re-tests are skipped while no lane's bestT has changed
+//   since the push: the re-test would repeat the push-time computation with the same inputs);
 // - records addressed by 32-bit byte offsets, which the scalar loads take as their SGPR offset
 //   (rt_scene_create sends larger trees to MODE_DEEP);
 // - the camera ray's query skips the `alive` AND (only a shadow query's lanes leave early).
-// The packed big-scene kernels keep traverse_wave_impl: every one of these forms measured
-// slower there (their SGPRs are all taken).
-template <bool WIDE, bool PK>
+template <bool WIDE>
 __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const RayPre& r, bool active,
                                                   bool any_hit, float any_hit_dist, HitState& hs) {
     uint64_t alive = ballot(active);
@@ -521,7 +352,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
     RT_STAT(13 + so, __popcll(alive));
     // The root's pop-time test (SearchBVH tests every popped node, query.h:252-254) is made
     // here with the initial bestT; the root is then the first entry in hand.
-    uint64_t mask = box_hit_mask<PK>(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
+    uint64_t mask = box_hit_mask(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
     if (mask == 0) {
         if (!any_hit) RT_STAT(17, 1);
         return;
@@ -560,7 +391,9 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
             } else {
                 RT_STAT(8 + so, 1);
                 if constexpr (WIDE) {
-                    // 4-ary record in one round trip (see traverse_wave_impl), by 32-bit byte offset
+                    // 4-ary record in one round trip: the seven 16-byte scalar loads are issued
+                    // together and waited for once (the empty asm keeps the compiler from sinking
+                    // each load next to its entry's test), addressed by 32-bit byte offset
                     const float4* W = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.wnode) + (ref << 7));
                     vf4 wq[7];
 #pragma unroll
@@ -576,7 +409,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                         if (refs[k] == NO_REF) continue;
                         const float4 p = wv[(3 * k) / 2], q = wv[(3 * k) / 2 + 1];
                         const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
-                        const uint64_t mk_ = box_hit_mask<PK>(r, bk, hs.bestT, mask);
+                        const uint64_t mk_ = box_hit_mask(r, bk, hs.bestT, mask);
                         if (mk_ != 0) {
                             if (pmask != 0) {  // the previous passing entry goes to the stack
                                 st_ref = wrlane(pref, sp, st_ref);
@@ -594,14 +427,14 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                     const uint4 q3 = ldc_u(N + 3);
                     const uint32_t lref = q3.x, rref = q3.y;
                     if (lref != NO_REF) {
-                        const uint64_t ml = box_hit_mask<PK>(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
+                        const uint64_t ml = box_hit_mask(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
                         if (ml != 0) {
                             pref = lref;
                             pmask = ml;
                         }
                     }
                     if (rref != NO_REF) {
-                        const uint64_t mr = box_hit_mask<PK>(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
+                        const uint64_t mr = box_hit_mask(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
                         if (mr != 0) {
                             if (pmask != 0) {
                                 st_ref = wrlane(pref, sp, st_ref);
@@ -641,7 +474,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                     const float4 p = ldc(B), q = ldc(B + 1);
                     ob = BoxP{lo2(p), hi2(p), lo2(q)};
                 }
-                mask = box_hit_mask<PK>(r, ob, hs.bestT, mask);
+                mask = box_hit_mask(r, ob, hs.bestT, mask);
             }
         }
     }
@@ -761,9 +594,7 @@ __device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, b
                                          float any_hit_dist, HitState& hs) {
     if constexpr ((MODE & MODE_DEEP) != 0) traverse_deep(sc, r, active, any_hit, any_hit_dist, hs);
     else if constexpr (MODE == RT_KERNEL_LANE) traverse_lane(sc, r, active, any_hit, any_hit_dist, hs);
-    else if constexpr ((MODE & MODE_PACKED) != 0)
-        traverse_wave_impl<(MODE & MODE_WIDE) != 0, true>(sc, r, active, any_hit, any_hit_dist, hs);
-    else traverse_wave_split<(MODE & MODE_WIDE) != 0, false>(sc, r, active, any_hit, any_hit_dist, hs);
+    else traverse_wave_split<(MODE & MODE_WIDE) != 0>(sc, r, active, any_hit, any_hit_dist, hs);
 }
 
 // Triangle index of a hit (the primary-hit AOV): the leaf's, or (DEEP kernels) the triangle a
@@ -852,11 +683,7 @@ struct Park {
     __device__ __forceinline__ float get(int k) const { return p[k * BLOCK]; }
     // The traversal between put and get writes no LDS, so without this the compiler would
     // forward the stored values and keep them in registers after all.
-    __device__ __forceinline__ static void fence() {
-#ifndef RT_EXP_NO_PARK  // experiment: let the compiler forward the parked values (registers)
-        asm volatile("" ::: "memory");
-#endif
-    }
+    __device__ __forceinline__ static void fence() { asm volatile("" ::: "memory"); }
 };
 
 template <int MODE>
@@ -920,9 +747,6 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, con
                 }
             }
         }
-#ifdef RT_EXP_NO_SHADOW  // timing experiments only (wrong output): skip the shadow traversal
-        need = false;
-#endif
         pk.put(0, cray.d.x);
         pk.put(1, cray.d.y);
         pk.put(2, cray.d.z);
@@ -981,9 +805,6 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
                 P.hit_t[aov] = hs.slot >= 0 ? hs.bestT : -1.0f;
             }
         }
-#ifdef RT_EXP_NO_SHADE  // timing experiments only (wrong output): primary traversal only
-        return mk(hs.bestT, 0.f, 0.f);
-#endif
         return shade_d1<MODE>(P, valid, ray, hs, park);
     }
     uint32_t rng = make_rng_seed(x, y, s);
@@ -1455,9 +1276,7 @@ __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
                 }
             }
         }
-        // the rest go to list q's survivor list (the render kernel's normal phase); the slot flags
-        // serve the big-scene kernels, which read the cull lists
-        if ((int)lane < m) P.cut_flag[slot0 + lane] = (uint8_t)((culled >> lane) & 1ull);
+        // the rest go to list q's survivor list (the render kernel's normal phase)
         const bool keep = (int)lane < m && !((culled >> lane) & 1ull) && !heavy;
         const uint64_t km = ballot(keep);
         if (km != 0) {
@@ -1607,24 +1426,15 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, flo
 // more in dispatch than the freer packing gains.)  (Looping a block over several slots measured no faster on c3 and, by keeping the
 // per-sample invariants live across the loop, spilled 224 B instead of 144 B per lane: c5 -6 %
 // without the loop.)
-// WAVES: waves per SIMD the kernel is compiled for.  With the shading spills removed (8 B of
-// scratch per lane left at 80 VGPRs, 28 B at 72) 7 waves (72 VGPRs) is fastest for scenes whose
-// nodes stay in L2: c3 7 waves 0.267 ms < 6 waves 0.273 < 5 waves 0.294 (one box, interleaved;
-// before the spill fixes 6 waves 0.290).  Scenes far larger than the L2s (c5, 345 MB) gain from
-// 8 waves of latency hiding with packed box tests despite 60 B of spills (c5: 8 waves 85.5 ms <
-// 7 waves 88.0 < 6 waves 89.2; launch picks by scene size, big_scene_waves).
+// WAVES: waves per SIMD the kernel is compiled for.  With the shading spills removed 7 waves
+// (72 VGPRs) is fastest: c3 7 waves 0.267 ms < 6 waves 0.273 < 5 waves 0.294 (one box,
+// interleaved), and with traverse_wave_split c5 too (76.0 ms vs 84.9 for the 8-wave packed-FMA
+// build that was the big-scene choice before).
 #ifndef RT_RENDER_WAVES
 #define RT_RENDER_WAVES 7
 #endif
-#ifndef RT_BIG_WAVES
-#define RT_BIG_WAVES 8
-#endif
-// HEAVY: the kernel takes heavy lists and records tile costs (heavy-first dispatch).  The
-// big-scene (MODE_PACKED) kernels leave it out: at 8 waves their SGPRs are all taken by the
-// traversal, and the few extra uniform values spilled into its loops (c5 +14 %); the host
-// enables heavy-first only with kernels that have it (heavy_kernel).
-template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, bool HEAVY = (MODE & MODE_PACKED) == 0,
-          int LS = 0>
+// Heavy-first dispatch: the kernel takes the heavy lists and records its tiles' costs.
+template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0>
 __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
     __shared__ int kpix[SAMPLES ? BLOCK : 1];
@@ -1634,20 +1444,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
 #endif
     // the wave's start time goes through LDS (an SGPR pair live across the whole tile spilled)
     __shared__ uint32_t t_start[BLOCK / 64], t_tile[BLOCK / 64];
-    if (HEAVY && P.tile_cost && lane_id() == 0) t_start[threadIdx.x / 64] = (uint32_t)wall_clock64();
+    if (P.tile_cost && lane_id() == 0) t_start[threadIdx.x / 64] = (uint32_t)wall_clock64();
     const int b = (int)blockIdx.x;
     int tile = -1;
-    if constexpr (!HEAVY) {
-        // The cull lists with the cut pass's slot flags.  (The register allocation of these
-        // kernels is at its limits: reading the cut pass's survivor lists here instead moved
-        // SGPR spills into the traversal loops, c5 +18 %.)
-        if (b >= P.tiles_virtual) return;
-        const int q = P.nqueues == 1 ? 0 : (b & 7);
-        const int i = P.nqueues == 1 ? b : (b >> 3);
-        tile = planned_tile(P, list_length(P, q), q, i);
-        if (tile < 0) return;
-        if (P.sc.ncut > 0 && P.cut_flag[(size_t)q * P.queue_cap + i]) return;
-    } else {
     if (b >= P.tiles_virtual + 8 * NCLASS * P.heavy_cap) return;
     // Virtual index i = b >> 3 of list q = b & 7 (the block's XCD).  Heavy phase: the first
     // NCLASS * heavy_cap indices, list q's heavy entries (its classes in order, heaviest first)
@@ -1684,18 +1483,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
             if (tile < 0) return;
         }
     }
-    }
-    if (HEAVY && P.tile_cost && lane_id() == 0) t_tile[threadIdx.x / 64] = (uint32_t)tile;
-#ifdef RT_EXP_LDS_TOP
-    if (P.sc.wide) {  // stage the top records (every block: LDS is per workgroup)
-        const int n = 8 * min(RT_EXP_LDS_TOP, max(P.sc.num_tris - 1, 1));
-        for (int k = (int)threadIdx.x; k < n; k += BLOCK) g_lds_top[k] = P.sc.wnode[k];
-        __syncthreads();
-    }
-#endif
+    if (P.tile_cost && lane_id() == 0) t_tile[threadIdx.x / 64] = (uint32_t)tile;
     if constexpr (SAMPLES) samples_tile<MODE, D1, LS>(P, tile, col, kpix, park);
     else pixels_tile<MODE, D1>(P, tile, park);
-    if (HEAVY && P.tile_cost && lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
+    if (P.tile_cost && lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
         asm volatile("" ::: "memory");
         const uint32_t d = (uint32_t)wall_clock64() - t_start[threadIdx.x / 64];
         P.tile_cost[4 * (size_t)t_tile[threadIdx.x / 64] + threadIdx.x / 64] = (uint16_t)(d < 0xffffu ? d : 0xffffu);
@@ -2167,7 +1958,7 @@ struct rt_scene {
     bool deep = false;  // the DFS may need more than STACK_CAP entries: MODE_DEEP kernels
     DevBuf tri;         // deep: triangles by index (brute-force completion)
     bool wide = false;
-    DevBuf work;  // kSets x (counter set | live lists | cut flags)
+    DevBuf work;  // kSets counter sets, then kSets x (live lists | cut survivor lists | heavy lists)
     int64_t last_tiles_total = 0;
     int cus = 256;
     // heavy-first dispatch: per-tile wave durations of the last frames (4 x u16 per tile) for
@@ -2340,28 +2131,6 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
         if (n_int >= (size_t(1) << 25) || n_leaf >= (size_t(1) << 26)) deep = true;
         if (deep || std::max(1, SW[0]) > STACK_CAP) wide_ok = false;
     }
-#ifdef RT_EXP_LDS_TOP
-    // internal refs in BFS order of the 4-ary records (root, its internal entries, theirs...),
-    // then the internal nodes only the binary records reach, so the top records come first
-    if (wide_ok && n_int > 0 && cid[0] != NO_REF && !(cid[0] & LEAF_BIT)) {
-        std::vector<uint32_t> order;
-        std::vector<uint8_t> seen(NN, 0);
-        order.push_back(0);
-        seen[0] = 1;
-        for (size_t h = 0; h < order.size(); ++h) {
-            uint32_t e[4];
-            const int k = wide_entries(nodes[order[h]], e);
-            for (int i = 0; i < k; ++i)
-                if (!(cid[e[i]] & LEAF_BIT) && !seen[e[i]]) {
-                    seen[e[i]] = 1;
-                    order.push_back(e[i]);
-                }
-        }
-        for (size_t n = 0; n < NN; ++n)
-            if (cid[n] != NO_REF && !(cid[n] & LEAF_BIT) && !seen[n]) order.push_back(uint32_t(n));
-        for (size_t i = 0; i < order.size(); ++i) cid[order[i]] = uint32_t(i);
-    }
-#endif
     std::vector<float4> hin(4 * std::max<size_t>(n_int, 1)), hib(2 * std::max<size_t>(n_int, 1));
     std::vector<float4> hwn(wide_ok ? 8 * std::max<size_t>(n_int, 1) : 0);
     std::vector<float4> hlf(4 * std::max<size_t>(n_leaf, 1)), hnm(3 * P);
@@ -2625,19 +2394,12 @@ void launch_render(K kernel, const dim3& grid, const RenderParams& P, const Laun
 }
 
 template <int MODE, bool SAMPLES>
-void launch_mode(const RenderParams& P, bool big, const Launch& L) {
+void launch_mode(const RenderParams& P, const Launch& L) {
     const dim3 grid((P.tiles_virtual + 7) / 8 * 8 + 8 * NCLASS * P.heavy_cap);
     if (P.max_depth == 1) {
-        if constexpr (SAMPLES && MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0) {
-            if (big) {  // more waves and packed box tests (c5 faster with each; both slower on c3)
-                launch_render(render_tiles_kernel<MODE | MODE_PACKED, SAMPLES, true, RT_BIG_WAVES>, grid, P, L);
-                return;
-            }
-        }
         if constexpr (SAMPLES) {
             if (P.half_waves) {
-                launch_render(render_tiles_kernel<MODE, SAMPLES, true, RT_RENDER_WAVES, (MODE & MODE_PACKED) == 0, 1>,
-                              grid, P, L);
+                launch_render(render_tiles_kernel<MODE, SAMPLES, true, RT_RENDER_WAVES, 1>, grid, P, L);
                 return;
             }
         }
@@ -2645,8 +2407,7 @@ void launch_mode(const RenderParams& P, bool big, const Launch& L) {
     } else {
         if constexpr (SAMPLES) {
             if (P.half_waves) {
-                launch_render(render_tiles_kernel<MODE, SAMPLES, false, RT_RENDER_WAVES, (MODE & MODE_PACKED) == 0, 1>,
-                              grid, P, L);
+                launch_render(render_tiles_kernel<MODE, SAMPLES, false, RT_RENDER_WAVES, 1>, grid, P, L);
                 return;
             }
         }
@@ -2655,19 +2416,9 @@ void launch_mode(const RenderParams& P, bool big, const Launch& L) {
 }
 
 template <int MODE>
-void launch(const RenderParams& P, bool samples, bool big, const Launch& L) {
-    if (samples) launch_mode<MODE, true>(P, big, L);
-    else launch_mode<MODE, false>(P, big, L);
-}
-
-// Scene data well beyond the eight 4 MB L2s (c5: 345 MB; frog: 6.6 MB): the 7-wave build.
-bool big_scene_waves(const rt_scene* s) {
-    // The 8-wave packed kernels were the big-scene choice (c5 85.5 ms vs 88.0 at 7 waves) until
-    // traverse_wave_split: the 7-wave kernels now render c5 in 76.0 ms vs 84.9.  They stay
-    // selectable for A/B (RT_RENDER_WAVES_BIG=1), scene size no longer picks them.
-    if (const char* e = std::getenv("RT_RENDER_WAVES_BIG")) return std::atoi(e) != 0;
-    (void)s;
-    return false;
+void launch(const RenderParams& P, bool samples, const Launch& L) {
+    if (samples) launch_mode<MODE, true>(P, L);
+    else launch_mode<MODE, false>(P, L);
 }
 
 // Host restatement of a pixel whose spp samples all miss the root: each sample is
@@ -2797,12 +2548,10 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // GPU, max over the 8: kernel 0.101 -> 0.095 ms, frame 0.122 -> 0.116; at 4 and fewer shards
     // the doubled wave count costs more: N = 4 0.106 -> 0.116, N = 1 0.211 -> 0.373;
     // scripts/half_waves_ab.py).  RT_HALF_WAVES=0/1 overrides.  (Quarter waves,
-    // 16 samples, measured slower at N = 8 and were dropped.)  The big-scene kernels have no
-    // half-wave form.
+    // 16 samples, measured slower at N = 8 and were dropped.)
     int half = o->band_count >= 8 ? 1 : 0;
     if (const char* e = std::getenv("RT_HALF_WAVES")) half = std::clamp(std::atoi(e), 0, 1);
-    const bool big_path = big_scene_waves(s) && o->max_depth == 1 && o->kernel != RT_KERNEL_LANE && !s->deep;
-    if (!samples || o->spp > (64 >> half) || big_path) half = 0;
+    if (!samples || o->spp > (64 >> half)) half = 0;
     P.half_waves = half;
     int ppb = samples ? (BLOCK >> half) / o->spp : BLOCK;  // pixels per block
     int tw = 1;
@@ -2818,7 +2567,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.lane_samples = samples ? 1 : 0;
     P.tile_order = o->tile_order == RT_TILES_AUTO ? RT_TILES_ROWS : o->tile_order;
     P.cull = (o->flags & RT_FLAG_NO_CULL) ? 0 : 1;
-    if (!P.cull) P.sc.ncut = 0;  // the render kernel reads the cut flags only when the cut pass ran
+    if (!P.cull) P.sc.ncut = 0;  // the render kernel reads the cut pass's lists only when it ran
     P.miss_pixel = miss_pixel_value(o);
     P.nqueues = P.tile_order == RT_TILES_LINEAR ? 1 : 8;
     // a list holds at most tiles_x * ceil(tiles_y / 8) tiles (RT_TILES_ROWS) or ceil(tiles / 8)
@@ -2831,22 +2580,18 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // (0: off).
     double heavy_frac = 0.08;
     if (const char* e = std::getenv("RT_HEAVY_FRAC")) heavy_frac = std::atof(e);
-    // the kernel launch() will pick: the big-scene build has no heavy-first support
-    const bool big = big_scene_waves(s);
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
-    const bool heavy_kernel = !(big && o->max_depth == 1 && samples && mode != RT_KERNEL_LANE && !s->deep);
-    const bool costs = heavy_kernel && P.cull && P.sc.ncut > 0 && P.nqueues == 8 && heavy_frac > 0.0;
+    const bool costs = P.cull && P.sc.ncut > 0 && P.nqueues == 8 && heavy_frac > 0.0;
     int heavy_cap = 512;  // RT_HEAVY_CAP: entries per (class, list) (speed experiments)
     if (const char* e = std::getenv("RT_HEAVY_CAP")) heavy_cap = std::max(1, std::atoi(e));
     P.heavy_cap = costs ? std::min(P.queue_cap, heavy_cap) : 0;
     // kSets counter sets (8 live lists, one spare, 8 heavy lists each) at fixed offsets, then
-    // kSets x (live lists | cut flags | heavy lists) sized for this geometry; rotating by frame
+    // kSets x (live lists | cut survivor lists | heavy lists) sized for this geometry; rotating by frame
     constexpr size_t kCounterBytes = COUNTER_SET_U32 * sizeof(uint32_t);
     const size_t list_bytes = size_t(P.nqueues) * size_t(P.queue_cap) * sizeof(int32_t);
     const size_t cut_bytes = P.sc.ncut > 0 ? list_bytes : 0;
-    const size_t flag_bytes = P.sc.ncut > 0 ? (size_t(P.nqueues) * size_t(P.queue_cap) + 255) / 256 * 256 : 0;
     const size_t heavy_bytes = size_t(8 * NCLASS) * size_t(P.heavy_cap) * sizeof(int32_t);
-    const size_t set_bytes = list_bytes + cut_bytes + heavy_bytes + flag_bytes;
+    const size_t set_bytes = list_bytes + cut_bytes + heavy_bytes;
     const size_t work_bytes = rt_scene::kSets * (kCounterBytes + set_bytes);
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint64_t k = s->launches;
@@ -2912,7 +2657,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         {uintptr_t(hit_idx), uintptr_t(hit_idx) + (hit_idx ? npx * size_t(o->spp) * sizeof(int32_t) : 0)},
         {uintptr_t(hit_t), uintptr_t(hit_t) + (hit_t ? npx * size_t(o->spp) * sizeof(float) : 0)}};
     // a new list layout may place this frame's lists over the previous frame's: serialise too
-    bool overlap = s->set_bytes != set_bytes || cost_reset || std::getenv("RT_EXP_SERIAL_PREP") != nullptr;
+    bool overlap = s->set_bytes != set_bytes || cost_reset;
     for (const auto& a : out_now)
         for (const auto& b : s->prev_out)
             overlap = overlap || (a.lo < a.hi && b.lo < b.hi && a.lo < b.hi && b.lo < a.hi);
@@ -2930,7 +2675,6 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.live_tiles = reinterpret_cast<int32_t*>(lists);
     P.cut_tiles = reinterpret_cast<int32_t*>(lists + list_bytes);
     P.heavy_tiles = reinterpret_cast<int32_t*>(lists + list_bytes + cut_bytes);
-    P.cut_flag = reinterpret_cast<uint8_t*>(lists + list_bytes + cut_bytes + heavy_bytes);
     const int slot = int(k % rt_scene::kRing);
     // From the cull launch on, a failure leaves the counter sets unknown (counters_dirty).
     auto frame = [&]() -> int {
@@ -2959,15 +2703,12 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
-        const bool sep = std::getenv("RT_EXP_EVENT_RECORD") != nullptr;  // A/B: separate event records
-        if (sep) HIP_TRY(hipEventRecord(s->evm[slot], st));
-        const Launch L{st, sep ? nullptr : s->evm[slot], sep ? nullptr : s->ev1[slot]};
-        if (s->deep) launch<MODE_DEEP>(P, samples, false, L);
-        else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, big, L);
-        else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, big, L);
-        else launch<RT_KERNEL_WAVE>(P, samples, big, L);
+        const Launch L{st, s->evm[slot], s->ev1[slot]};
+        if (s->deep) launch<MODE_DEEP>(P, samples, L);
+        else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, L);
+        else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, L);
+        else launch<RT_KERNEL_WAVE>(P, samples, L);
         HIP_TRY(hipGetLastError());
-        if (sep) HIP_TRY(hipEventRecord(s->ev1[slot], st));
         return RT_OK;
     };
     std::copy(std::begin(out_now), std::end(out_now), std::begin(s->prev_out));

@@ -133,26 +133,6 @@ def test_half_waves_parity(name, monkeypatch):
     _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
 
 
-@pytest.mark.parametrize("name", ["c3_small", "c5_small", "frog_bounce"])
-def test_big_scene_kernel_build_parity(name, monkeypatch):
-    """The 7-wave build of the depth-1 sample kernels (picked for scenes far beyond the L2s)
-    forced on small scenes: the reference's outputs bit for bit."""
-    monkeypatch.setenv("RT_RENDER_WAVES_BIG", "1")
-    meta = golden_meta(name)
-    scene = G_SCENES[name]
-    hs = host_scene(scene)
-    cam = hs.camera(meta["width"], meta["height"])
-    ds = rt.DeviceScene.from_host(hs, device=0)
-    rgb, hi, ht = ds.render(cam, spp=meta["spp"], max_depth=meta["max_depth"],
-                            diffuse_bounce=bool(meta["diffuse_bounce"]), miss_color=hexv(meta["miss_color"]),
-                            aov=True)
-    assert np.array_equal(hi.reshape(-1), golden_array(name, "hits.i32.gz", np.int32))
-    assert np.array_equal(ht.reshape(-1).view(np.uint32),
-                          golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
-    _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
-    ds.close()
-
-
 @pytest.mark.parametrize("flags,tiles", LAUNCHES)
 def test_c3_full_frame_matches_reference(flags, tiles):
     """1920x1080x16 frog (config c3) against the reference's own full-size outputs, for every
@@ -211,21 +191,6 @@ def test_heavy_first_dispatch_changes_nothing(env, monkeypatch):
     assert heavy[0] == 0 and heavy[1] > 0 and heavy[4] > 0, heavy
     if "RT_HEAVY_CAP" in env:
         assert heavy[4] <= 8 * 3 * int(env["RT_HEAVY_CAP"])
-    ds.close()
-
-
-def test_packed_big_scene_kernels_match_reference(monkeypatch):
-    """The 8-wave packed-FMA kernels (traverse_wave_impl), no longer picked by scene size but kept
-    for A/B (RT_RENDER_WAVES_BIG=1): the c3 frame still equals the reference's own outputs."""
-    monkeypatch.setenv("RT_RENDER_WAVES_BIG", "1")
-    meta = golden_meta("c3_full")
-    hs = host_scene("frog.json")
-    cam = hs.camera(1920, 1080)
-    ds = rt.DeviceScene.from_host(hs, device=0)
-    rgb, hi, ht = ds.render(cam, spp=16, max_depth=1, aov=True)
-    assert hashlib.sha256(hi.tobytes()).hexdigest() == meta["sha256"]["hits.i32"]
-    assert hashlib.sha256(ht.tobytes()).hexdigest() == meta["sha256"]["hitt.f32"]
-    _check_fb(rgb, golden_array("c3_full", "fb.f32.gz", np.float32))
     ds.close()
 
 

@@ -140,7 +140,8 @@ def test_bench_two_ranks_gloo_on_one_gpu(gather):
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", str(repo / "bench.py"), "--gpus", "2",
-           "--steps", "3", "--warmup", "1", "--comm", "torch", "--backend", "gloo", "--gather-payload", gather]
+           "--steps", "3", "--warmup", "1", "--comm", "torch", "--backend", "gloo", "--gather-payload", gather,
+           "--share-gpu"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(repo))
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])

@@ -53,6 +53,7 @@ constexpr uint32_t LEAF_BIT = 0x80000000u;
 constexpr uint32_t NO_REF = 0xFFFFFFFFu;
 constexpr uint32_t VER_FORCE = 0xFFFFFFFFu;   // pop must re-test (root)
 constexpr int STACK_CAP = 64;                 // one entry per lane of the wave stack
+constexpr int LANE_LDS_CAP = 16;              // traverse_lane_lds: per-lane stack entries in LDS
 constexpr int BLOCK = 256;
 // Kernel instantiation flag on top of RT_KERNEL_WAVE: traverse the 4-ary records (SceneView::wide).
 // A compile-time choice, so each kernel holds one traversal loop per ray kind.
@@ -89,6 +90,7 @@ struct SceneView {
     float root_box[6];
     float bmax[3];  // per axis max |coordinate| over every AABB of the scene (make_ray)
     int32_t wide;
+    int32_t lane_stack;  // the binary DFS fits LANE_LDS_CAP entries: bounce rays take traverse_lane_lds
     const float* __restrict__ cut;  // tile culling: boxes of a cut of the tree (6 floats each)
     int32_t ncut;
     const float4* __restrict__ tri;  // deep trees: v0 | e1, e2.x | e2.y, e2.z by triangle index (brute force)
@@ -588,6 +590,70 @@ __device__ void traverse_deep(const SceneView& sc, const RayPre& r, bool active,
     }
 }
 
+// ---- LANE traversal with its stack in LDS (incoherent rays: bounce rays, their shadow rays) --
+// A wave-shared DFS visits the union of its lanes' paths: fine for the coherent camera rays of a
+// 2x2-pixel quad and their shadow rays toward one light, but 64 diffuse bounce rays leave the
+// surface in 64 directions, and the union of their paths is most of the tree (c3b, frog.json's
+// own 8 bounces: 10.9 ms per frame with wave-shared bounce traversals).  Here each lane runs
+// SearchBVH's DFS over the binary records on its own: the wave's time is its longest path, not
+// the union.  The stack holds LANE_LDS_CAP entries per lane in LDS (stride BLOCK; trees whose
+// DFS needs more take the wave traversal); as in the wave traversal, the last entry an internal
+// node would push is held and processed at once (its pop-time test would repeat the push-time
+// one with the same bestT), and a stale watermark selects the entries that were pushed before
+// the latest bestT change: only those take the pop-time re-test.  Same tests, same order, same
+// bestT at every test as the reference: exact.
+__device__ __forceinline__ void traverse_lane_lds(const SceneView& sc, const RayPre& r, bool active, bool any_hit,
+                                                  float any_hit_dist, HitState& hs, uint32_t* stk) {
+    hs.bestT = FLT_MAX;
+    hs.slot = -1;
+    if (!active) return;
+    if (!box_hit(r, own_box(sc, sc.root_ref, true), kRayTMin, hs.bestT)) return;  // the root's pop-time test
+    uint32_t ref = sc.root_ref;
+    int sp = 0, stale = 0;
+    while (true) {
+        uint32_t next = NO_REF;  // the entry to hold
+        if (ref & LEAF_BIT) {
+            const uint32_t slot = ref & ~LEAF_BIT;
+            const float4* L = sc.leaf + 4 * (size_t)slot;
+            const float4 a = L[0], b = L[1], c = L[2];
+            float t, u, v;
+            if (mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin, hs.bestT, t, u, v)) {
+                hs.bestT = t;
+                hs.slot = (int32_t)slot;
+                stale = sp;
+                if (any_hit && t < any_hit_dist) return;
+            }
+        } else {
+            const float4* N = sc.inode + 4 * (size_t)ref;
+            const float4 q0 = N[0], q1 = N[1], q2 = N[2];
+            const uint4 q3 = *reinterpret_cast<const uint4*>(N + 3);
+            const bool hl = q3.x != NO_REF && box_hit(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, kRayTMin, hs.bestT);
+            const bool hr = q3.y != NO_REF && box_hit(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, kRayTMin, hs.bestT);
+            if (hl && hr) {
+                stk[sp * BLOCK] = q3.x;
+                ++sp;
+            }
+            next = hr ? q3.y : (hl ? q3.x : NO_REF);
+        }
+        if (next != NO_REF) {
+            ref = next;
+            continue;
+        }
+        bool found = false;
+        while (sp > 0) {
+            --sp;
+            ref = stk[sp * BLOCK];
+            if (sp < stale) {  // pushed before the latest bestT change: the pop-time re-test
+                stale = sp;
+                if (!box_hit(r, own_box(sc, ref, false), kRayTMin, hs.bestT)) continue;
+            }
+            found = true;
+            break;
+        }
+        if (!found) return;
+    }
+}
+
 // any_hit (wave-uniform): shadow query, stop a lane once bestT < any_hit_dist.
 template <int MODE>
 __device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, bool active, bool any_hit,
@@ -595,6 +661,21 @@ __device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, b
     if constexpr ((MODE & MODE_DEEP) != 0) traverse_deep(sc, r, active, any_hit, any_hit_dist, hs);
     else if constexpr (MODE == RT_KERNEL_LANE) traverse_lane(sc, r, active, any_hit, any_hit_dist, hs);
     else traverse_wave_split<(MODE & MODE_WIDE) != 0>(sc, r, active, any_hit, any_hit_dist, hs);
+}
+
+// The traversal of a ray at bounce depth `depth` (wave-uniform): camera rays (depth 0) and their
+// shadow rays are coherent and take the kernel's traversal; in the WAVE kernels the bounce rays
+// and their shadow rays take traverse_lane_lds when the tree's DFS fits its LDS stack.
+template <int MODE>
+__device__ __forceinline__ void traverse_at(const SceneView& sc, int depth, const RayPre& r, bool active, bool any_hit,
+                                            float any_hit_dist, HitState& hs, float* lds) {
+    if constexpr (MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0) {
+        if (depth > 0 && sc.lane_stack) {
+            traverse_lane_lds(sc, r, active, any_hit, any_hit_dist, hs, reinterpret_cast<uint32_t*>(lds) + threadIdx.x);
+            return;
+        }
+    }
+    traverse<MODE>(sc, r, active, any_hit, any_hit_dist, hs);
 }
 
 // Triangle index of a hit (the primary-hit AOV): the leaf's, or (DEEP kernels) the triangle a
@@ -817,7 +898,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
         if (ballot(alive) == 0) break;
         HitState hs;
         if (depth > 0) count_rays<MODE>(P.ray_count, 2, alive);
-        traverse<MODE>(sc, ray, alive, false, 0.0f, hs);
+        traverse_at<MODE>(sc, depth, ray, alive, false, 0.0f, hs, park);
         const bool hit = alive && hs.slot >= 0;
         SurfHit sh;
         sh.tri = -1;
@@ -870,7 +951,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
             }
             HitState shs;
             count_rays<MODE>(P.ray_count, 1, need);
-            traverse<MODE>(sc, sray, need, true, dist, shs);
+            traverse_at<MODE>(sc, depth, sray, need, true, dist, shs, park);
             const bool occluded = need && shs.slot >= 0 && shs.bestT < dist;
             if (lit && !occluded) Lo = add(Lo, contrib);
         }
@@ -1310,8 +1391,10 @@ __device__ __forceinline__ int planned_tile(const RenderParams& P, int len, int 
 // One sample per lane: a block covers a tile_w x tile_h pixel tile x spp samples (spp a power
 // of two <= 256, tile_w*tile_h*spp == BLOCK); per-pixel sums run in sample order from LDS.
 template <int MODE, bool D1, int LS = 0>
-__device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, float* col, int* kpix, float* park) {
+__device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, float* col, int* kpix, float* park,
+                                             const int* lds_zero) {
     const int t = (int)threadIdx.x;
+    const uint32_t wv = uni((uint32_t)t) >> 6;  // the wave's index in the block (an SGPR)
     // LS = 1, half waves (band shards of a multi-GPU frame, spp <= 32): each wave traces 32
     // samples in its low lanes, so a tile's longest wave, which bounds a short kernel, has half
     // the rays' path union; lt is the sample's index in the (half-size) tile.  A template
@@ -1349,10 +1432,18 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
         const int64_t aov = valid && P.hit_idx ? (int64_t)pix * P.spp + s : -1;
         const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, aov, park);
         RT_PHASE(P, x, r, 1);
-        col[3 * t] = c.x;
-        col[3 * t + 1] = c.y;
-        col[3 * t + 2] = c.z;
+        // The thread index again, from the wave's index and a lane id the compiler cannot
+        // merge with the first one (mbcnt of a zero read back from LDS): keeping t itself live
+        // across the traversals cost a 4-byte scratch spill per lane (c3: ~8 MB of writes per
+        // launch).
+        const int te = (int)((wv << 6) | __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(
+                                                  ~0u, (uint32_t)*(const volatile int*)lds_zero)));
+        col[3 * te] = c.x;
+        col[3 * te + 1] = c.y;
+        col[3 * te + 2] = c.z;
     }
+    const int t2 = (int)((wv << 6) | __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(
+                                             ~0u, (uint32_t)*(const volatile int*)lds_zero)));
     if (P.spp <= 64) {
         // A pixel's samples are consecutive lanes of one wave: only this wave's LDS writes are
         // read below, so the wave synchronises alone (its siblings in the block may still be
@@ -1363,13 +1454,13 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
     } else {
         __syncthreads();
     }
-    if ((t & (P.spp - 1)) == 0) {
-        const int pix = kpix[t >> P.spp_log2];
+    if ((t2 & (P.spp - 1)) == 0) {
+        const int pix = kpix[t2 >> P.spp_log2];
         if (pix >= 0) {
             // col = col + TraceRayIterative(...) in sample order, then col / float(spp)
             f3 acc = mk(0.f, 0.f, 0.f);
             for (int k = 0; k < P.spp; ++k)
-                acc = add(acc, mk(col[3 * (t + k)], col[3 * (t + k) + 1], col[3 * (t + k) + 2]));
+                acc = add(acc, mk(col[3 * (t2 + k)], col[3 * (t2 + k) + 1], col[3 * (t2 + k) + 2]));
             // x / 2^k and x * 2^-k are the same correctly rounded value (the exact quotients
             // are equal), so the power-of-two divide is a multiply here.
             const float rs = 1.0f / (float)P.spp;
@@ -1433,17 +1524,27 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, flo
 #ifndef RT_RENDER_WAVES
 #define RT_RENDER_WAVES 7
 #endif
+// The multi-bounce kernels (D1 false): the bounce loop keeps more state live than the depth-1
+// shading (RNG, throughput, the ray, two rays' RayPre) and spills at 7 waves: c3b 9.70 ms at 7
+// waves (336 B scratch), 5.80 at 5 (240 B), 5.01 at 4 (84 B, 128 VGPRs).
+#ifndef RT_BOUNCE_WAVES
+#define RT_BOUNCE_WAVES 4
+#endif
 // Heavy-first dispatch: the kernel takes the heavy lists and records its tiles' costs.
 template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0>
 __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
     __shared__ int kpix[SAMPLES ? BLOCK : 1];
-    __shared__ float park[D1 ? PARK_SLOTS * BLOCK : 1];  // shade_d1's state across shadow rays
+    // D1: shade_d1's state across shadow rays; else (WAVE kernels) traverse_lane_lds's stacks
+    __shared__ float park[D1 ? PARK_SLOTS * BLOCK
+                             : (MODE == RT_KERNEL_LANE || (MODE & MODE_DEEP) != 0 ? 1 : LANE_LDS_CAP * BLOCK)];
 #ifdef RT_WAVE_TIMES
     const unsigned long long wt0 = wall_clock64();
 #endif
     // the wave's start time goes through LDS (an SGPR pair live across the whole tile spilled)
     __shared__ uint32_t t_start[BLOCK / 64], t_tile[BLOCK / 64];
+    __shared__ int lds_zero;  // 0, written by every lane (samples_tile's fresh lane id)
+    if constexpr (SAMPLES) lds_zero = 0;
     if (P.tile_cost && lane_id() == 0) t_start[threadIdx.x / 64] = (uint32_t)wall_clock64();
     const int b = (int)blockIdx.x;
     int tile = -1;
@@ -1484,7 +1585,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
         }
     }
     if (P.tile_cost && lane_id() == 0) t_tile[threadIdx.x / 64] = (uint32_t)tile;
-    if constexpr (SAMPLES) samples_tile<MODE, D1, LS>(P, tile, col, kpix, park);
+    if constexpr (SAMPLES) samples_tile<MODE, D1, LS>(P, tile, col, kpix, park, &lds_zero);
     else pixels_tile<MODE, D1>(P, tile, park);
     if (P.tile_cost && lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
         asm volatile("" ::: "memory");
@@ -1958,6 +2059,7 @@ struct rt_scene {
     bool deep = false;  // the DFS may need more than STACK_CAP entries: MODE_DEEP kernels
     DevBuf tri;         // deep: triangles by index (brute-force completion)
     bool wide = false;
+    bool lane_stack = false;  // binary DFS stack <= LANE_LDS_CAP (traverse_lane_lds)
     DevBuf work;  // kSets counter sets, then kSets x (live lists | cut survivor lists | heavy lists)
     int64_t last_tiles_total = 0;
     int cus = 256;
@@ -2082,6 +2184,7 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
                o.max_corner.y >= i.max_corner.y && o.max_corner.z >= i.max_corner.z;
     };
     bool wide_ok = true, deep = false;
+    int binary_stack = 0;
     {
         std::vector<uint8_t> state(NN, 0);  // 0 new, 1 on path, 2 done
         std::vector<int> S(NN, 0), SW(NN, 0);
@@ -2125,6 +2228,7 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
             }
         }
         deep = std::max(1, S[0]) > STACK_CAP;
+        binary_stack = std::max(1, S[0]);
         // traverse_wave_split addresses records by 32-bit byte offsets (ref << 7 into the 4-ary
         // array, << 5 into ibox, slot << 6 into the leaves): larger trees take the MODE_DEEP
         // kernels, which are exact for any tree.
@@ -2267,6 +2371,7 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     if ((rc = s->inode.upload(hin.data(), hin.size() * sizeof(float4))) != RT_OK) return rc;
     if (wide_ok && (rc = s->wnode.upload(hwn.data(), hwn.size() * sizeof(float4))) != RT_OK) return rc;
     s->wide = wide_ok && !(s->root_ref & LEAF_BIT);
+    s->lane_stack = !deep && binary_stack <= LANE_LDS_CAP;
     s->deep = deep;
     if (deep) {  // v0 | e1, e2.x | e2.y, e2.z by triangle index, e1/e2 as intersectTriangle computes them
         std::vector<float4> ht(3 * P);
@@ -2311,6 +2416,7 @@ extern "C" int rt_scene_clone(const rt_scene* src, int device, rt_scene** out) {
     std::memcpy(s->bmax, src->bmax, sizeof(s->bmax));
     s->ncut = src->ncut;
     s->wide = src->wide;
+    s->lane_stack = src->lane_stack;
     s->deep = src->deep;
     s->cus = src->cus;
     s->bytes = src->bytes;
@@ -2407,11 +2513,11 @@ void launch_mode(const RenderParams& P, const Launch& L) {
     } else {
         if constexpr (SAMPLES) {
             if (P.half_waves) {
-                launch_render(render_tiles_kernel<MODE, SAMPLES, false, RT_RENDER_WAVES, 1>, grid, P, L);
+                launch_render(render_tiles_kernel<MODE, SAMPLES, false, RT_BOUNCE_WAVES, 1>, grid, P, L);
                 return;
             }
         }
-        launch_render(render_tiles_kernel<MODE, SAMPLES, false>, grid, P, L);
+        launch_render(render_tiles_kernel<MODE, SAMPLES, false, RT_BOUNCE_WAVES>, grid, P, L);
     }
 }
 
@@ -2496,6 +2602,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.sc.inode = static_cast<const float4*>(s->inode.p);
     P.sc.wnode = static_cast<const float4*>(s->wnode.p);
     P.sc.wide = s->wide && !(o->flags & RT_FLAG_BINARY) ? 1 : 0;
+    P.sc.lane_stack = s->lane_stack ? 1 : 0;
     P.sc.ibox = static_cast<const float4*>(s->ibox.p);
     P.sc.rootb = static_cast<const float4*>(s->ibox.p) + s->ibox.n / sizeof(float4) - 2;
     P.sc.leaf = static_cast<const float4*>(s->leaf.p);

@@ -28,11 +28,14 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -209,6 +212,92 @@ bool spin_until(F pred) {
     }
 }
 
+// Worker threads of an in-process renderer over several GPUs: a frame's host work per rank
+// (the scene's pre-pass and render launches, the rank's copy) goes out in parallel, one thread
+// per rank, so submitting a frame does not take N times one rank's host time.  run(n, job)
+// runs job(0) on the caller and job(i) on worker i-1, and returns when all have finished; the
+// first failing rank's code and message become the caller's.
+class RankPool {
+  public:
+    ~RankPool() { stop(); }
+    bool started() const { return !th_.empty(); }
+    void start(int workers) {
+        for (int i = 0; i < workers; ++i) th_.emplace_back([this, i] { loop(i); });
+    }
+    void stop() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread& t : th_) t.join();
+        th_.clear();
+        quit_ = false;
+    }
+    int run(int n, const std::function<int(int)>& job) {
+        if (n <= 1 || th_.empty()) {
+            for (int i = 0; i < n; ++i) {
+                const int rc = job(i);
+                if (rc != RT_OK) return rc;
+            }
+            return RT_OK;
+        }
+        rc_.assign(size_t(n), RT_OK);
+        msg_.assign(size_t(n), std::string());
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &job;
+            n_ = n;
+            pending_ = n - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        rc_[0] = job(0);
+        if (rc_[0] != RT_OK) msg_[0] = rt_last_error();
+        {
+            std::unique_lock<std::mutex> lk(m_);
+            done_.wait(lk, [this] { return pending_ == 0; });
+            job_ = nullptr;
+        }
+        for (int i = 0; i < n; ++i)
+            if (rc_[i] != RT_OK) return set_error(rc_[i], msg_[i]);
+        return RT_OK;
+    }
+
+  private:
+    void loop(int w) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<int(int)>* job;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+                job = job_;
+            }
+            const int i = w + 1;
+            if (job && i < n_) {
+                rc_[i] = (*job)(i);
+                if (rc_[i] != RT_OK) msg_[i] = rt_last_error();
+            }
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                if (i < n_ && --pending_ == 0) done_.notify_one();
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<int(int)>* job_ = nullptr;
+    int n_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+    std::vector<int> rc_;
+    std::vector<std::string> msg_;
+};
+
 struct LocalRank {
     int device = 0;
     int rank = 0;  // global rank
@@ -258,6 +347,7 @@ struct rt_renderer {
     hipEvent_t tg0[kTimeRing] = {}, tg1[kTimeRing] = {}, td0[kTimeRing] = {}, td1[kTimeRing] = {};
     hipEvent_t ta[3][kTimeRing] = {}, tb[3][kTimeRing] = {};
     bool owns_scenes = true;
+    RankPool pool;  // in-process renderers over several GPUs: per-rank submission threads
 
     ~rt_renderer() { release(); }
     void release_buffers() {
@@ -275,6 +365,7 @@ struct rt_renderer {
         }
     }
     void release() {
+        pool.stop();
         for (LocalRank& L : ranks) {
             DeviceGuard g(L.device);
             if (L.compute) (void)hipStreamSynchronize(L.compute);
@@ -602,6 +693,13 @@ extern "C" int rt_renderer_create(size_t P, const rt_bvh_node* nodes, const rt_a
             for (int i = 0; i < kTimeRing; ++i) HIP_TRY(hipEventCreate(&ring[i]));
     }
     if (r->uses_rccl() && (rc = init_comms(r.get(), o)) != RT_OK) return rc;
+    // several GPUs in this process: one submission thread per further rank (RT_RENDERER_SERIAL=1
+    // submits every rank from the calling thread, for A/B; RT_RENDERER_THREADS=1 uses the threads
+    // for repeated device ids too, for tests on one GPU)
+    const char* serial = std::getenv("RT_RENDERER_SERIAL");
+    const char* threads = std::getenv("RT_RENDERER_THREADS");
+    const bool use_pool = (distinct && !(serial && std::atoi(serial) != 0)) || (threads && std::atoi(threads) != 0);
+    if (n > 1 && use_pool) r->pool.start(n - 1);
     *out = r.release();
     return RT_OK;
 }
@@ -634,24 +732,59 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
     if (shared && r->rank0_local && t + 1 >= uint64_t(r->depth))
         SharedFrames::raise_to(r->shared->word(kOffReleased), t + 1 - uint64_t(r->depth));
     for (int k = 0; k < 3; ++k) r->ta[k][ring] = r->tb[k][ring] = nullptr;
-    // 1. every local rank renders its bands into strip[s]: the scene's frame and nothing else
-    for (LocalRank& L : r->ranks) {
-        L.rendered[s] = L.released[s] = nullptr;
-        if (&L == &R0 && r->rank0_local) r->delivered[s] = nullptr;
-        if (L.rows == 0) continue;
+    const hipMemcpyKind kind = r->deliver == RT_DELIVER_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    char* dst = nullptr;
+    if (r->deliver != RT_DELIVER_NONE && (r->rank0_local || shared))
+        dst = static_cast<char*>(r->deliver == RT_DELIVER_DEVICE ? r->dev_frame[s].p : r->host[s]);
+    for (LocalRank& L : r->ranks) L.rendered[s] = L.released[s] = nullptr;
+    if (r->rank0_local) r->delivered[s] = nullptr;
+    // 1. every local rank renders its bands into strip[s] (the scene's frame and nothing else on
+    // its compute stream); DIRECT / HOST_SHARED: then copies its own bands into their rows of
+    // the host frame over its own PCIe link (the same job, so with several GPUs in this process
+    // each rank's host work runs on its own thread).
+    const bool copies = !rccl_mode && r->deliver != RT_DELIVER_NONE;
+    auto rank_job = [&](int i) -> int {
+        LocalRank& L = r->ranks[i];
+        const bool own = &L == &R0 && r->rank0_local;  // rank 0's copy: delivered_ev below
+        if (L.rows > 0) {
+            DeviceGuard g(L.device);
+            rt_render_opts o = *opts;
+            o.band_rows = r->band_rows;
+            o.band_index = L.rank;
+            o.band_count = r->world;
+            void* buf = L.strip[s].p;
+            int q = rt_render_device_p6(L.scene, cam, &o, f32 ? static_cast<float*>(buf) : nullptr, nullptr, nullptr,
+                                        f32 ? nullptr : static_cast<uint8_t*>(buf), L.compute);
+            if (q != RT_OK) return q;
+            hipEvent_t first = nullptr;
+            rt::scene_frame_events(L.scene, &first, &L.rendered[s]);
+            if (own) r->ta[RT_TIME_FRAME][ring] = first;
+        }
+        if (!copies) return RT_OK;
+        // With a frame shared by the job's processes, a rank other than 0's first waits for rank
+        // 0's caller to give up this slot's previous frame (rank 0 publishes that at its submit).
+        if (shared && !r->rank0_local && t + 1 >= uint64_t(r->depth) && L.rendered[s]) {
+            const uint64_t need = t + 1 - uint64_t(r->depth);
+            if (!spin_until([&] { return SharedFrames::load(r->shared->word(kOffReleased)) >= need; }))
+                return set_error(RT_ERR_COMM, "rank " + std::to_string(L.rank) + ": rank 0 did not release frame " +
+                                                  std::to_string(t - uint64_t(r->depth)) + " within RT_PEER_TIMEOUT_S");
+        }
         DeviceGuard g(L.device);
-        rt_render_opts o = *opts;
-        o.band_rows = r->band_rows;
-        o.band_index = L.rank;
-        o.band_count = r->world;
-        void* buf = L.strip[s].p;
-        rc = rt_render_device_p6(L.scene, cam, &o, f32 ? static_cast<float*>(buf) : nullptr, nullptr, nullptr,
-                                 f32 ? nullptr : static_cast<uint8_t*>(buf), L.compute);
-        if (rc != RT_OK) return rc;
-        hipEvent_t first = nullptr;
-        rt::scene_frame_events(L.scene, &first, &L.rendered[s]);
-        if (&L == &R0 && r->rank0_local) r->ta[RT_TIME_FRAME][ring] = first;
-    }
+        if (own) {
+            if (L.rendered[s]) HIP_TRY(hipStreamWaitEvent(L.copy, L.rendered[s], 0));
+            HIP_TRY(hipEventRecord(r->td0[ring], L.copy));
+        }
+        if (!L.rendered[s]) return RT_OK;
+        if (!own) HIP_TRY(hipStreamWaitEvent(L.copy, L.rendered[s], 0));
+        HIP_TRY(scatter_strip(dst, static_cast<const char*>(L.strip[s].p), L.rank, r->world, r->H, r->band_rows,
+                              r->row_bytes, kind, L.copy));
+        if (!own) {
+            HIP_TRY(hipEventRecord(L.released_ev[s], L.copy));
+            L.released[s] = L.released_ev[s];
+        }
+        return RT_OK;
+    };
+    if ((rc = r->pool.run(int(r->ranks.size()), rank_job)) != RT_OK) return rc;
     r->slot_ticket[s] = t + 1;
     r->next = t + 1;
     if (ticket) *ticket = t;
@@ -660,10 +793,6 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
         if (r->rank0_local) r->delivered[s] = r->tb[RT_TIME_FRAME][ring] = R0.rendered[s];
         return RT_OK;
     }
-    const hipMemcpyKind kind = r->deliver == RT_DELIVER_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    char* dst = nullptr;
-    if (r->rank0_local || shared)
-        dst = static_cast<char*>(r->deliver == RT_DELIVER_DEVICE ? r->dev_frame[s].p : r->host[s]);
     if (rccl_mode) {
         // 2. strips -> rank 0 (one group: every send and receive of this process)
         const Rccl& N = rccl();
@@ -727,32 +856,8 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
         }
         return RT_OK;
     }
-    // 2'. DIRECT / HOST_SHARED: every local rank copies its own bands into the frame.  With a
-    // frame shared by the job's processes, a rank other than 0's first waits for rank 0's caller
-    // to give up this slot's previous frame (rank 0 publishes that at its submit of frame t).
-    if (shared && !r->rank0_local && t + 1 >= uint64_t(r->depth)) {
-        const uint64_t need = t + 1 - uint64_t(r->depth);
-        if (!spin_until([&] { return SharedFrames::load(r->shared->word(kOffReleased)) >= need; }))
-            return set_error(RT_ERR_COMM, "rank " + std::to_string(R0.rank) + ": rank 0 did not release frame " +
-                                              std::to_string(t - uint64_t(r->depth)) + " within RT_PEER_TIMEOUT_S");
-    }
-    if (r->rank0_local) {
-        DeviceGuard g(R0.device);
-        if (R0.rendered[s]) HIP_TRY(hipStreamWaitEvent(R0.copy, R0.rendered[s], 0));
-        HIP_TRY(hipEventRecord(r->td0[ring], R0.copy));
-    }
-    for (LocalRank& L : r->ranks) {
-        if (!L.rendered[s]) continue;
-        DeviceGuard g(L.device);
-        const bool own = &L == &R0 && r->rank0_local;  // rank 0's copy: delivered_ev below
-        if (!own) HIP_TRY(hipStreamWaitEvent(L.copy, L.rendered[s], 0));
-        HIP_TRY(scatter_strip(dst, static_cast<const char*>(L.strip[s].p), L.rank, r->world, r->H, r->band_rows,
-                              r->row_bytes, kind, L.copy));
-        if (!own) {
-            HIP_TRY(hipEventRecord(L.released_ev[s], L.copy));
-            L.released[s] = L.released_ev[s];
-        }
-    }
+    // 2'. DIRECT / HOST_SHARED: the copies went out with the ranks' jobs; rank 0's frame is
+    // complete when every local copy is.
     if (r->rank0_local) {
         DeviceGuard g(R0.device);
         for (size_t i = 1; i < r->ranks.size(); ++i)  // the frame is complete when every local copy is

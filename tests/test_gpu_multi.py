@@ -215,6 +215,35 @@ def test_pipelined_alternating_cameras(devices, depth):
         r.close()
 
 
+@pytest.mark.parametrize("threads", ["0", "1"])
+def test_in_process_submission_threads(threads, monkeypatch):
+    """Several ranks in one process, their per-rank host work on submission threads (the default
+    over distinct GPUs, forced here for band shards sharing GPU 0) or on the calling thread:
+    pipelined frames with alternating cameras are the single-frame images."""
+    monkeypatch.setenv("RT_RENDERER_THREADS", threads)
+    monkeypatch.setenv("RT_RENDERER_SERIAL", "1" if threads == "0" else "0")
+    hs = host_scene("frog.json")
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    cams = [hs.camera(W, H), _moved(hs.camera(W, H), 0.005, 0.001)]
+    want = [_p6_body(ds.render(c, spp=SPP, max_depth=1)) for c in cams]
+    ds.close()
+    r = rt.Renderer.from_host(hs, devices=(0,) * 4, gather=rt.RT_GATHER_DIRECT, depth=3)
+    try:
+        o, _j = rt.DeviceScene.make_opts(spp=SPP, max_depth=1)
+        pend = []
+        for k in range(9):
+            pend.append((k, r.submit(cams[k % 2], o)))
+            if len(pend) >= 3:
+                kk, t = pend.pop(0)
+                addr, n = r.wait(t)
+                assert bytes((C.c_uint8 * n).from_address(addr)) == want[kk % 2], f"frame {kk}"
+        for kk, t in pend:
+            addr, n = r.wait(t)
+            assert bytes((C.c_uint8 * n).from_address(addr)) == want[kk % 2], f"frame {kk}"
+    finally:
+        r.close()
+
+
 def test_render_device_is_stream_ordered():
     """One buffer reused on one stream: fill, render A, copy, render B, copy.  Frame B's culling
     pre-passes (on the scene's own stream) must not write the buffer before copy A read it, nor

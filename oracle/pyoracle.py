@@ -27,10 +27,12 @@ class Cam(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("rays", C.c_uint64 * 3), ("pops", C.c_uint64 * 3), ("internal_entered", C.c_uint64 * 3),
-                ("leaf_entered", C.c_uint64 * 3), ("hits", C.c_uint64 * 3), ("occluded", C.c_uint64)]
+                ("leaf_entered", C.c_uint64 * 3), ("hits", C.c_uint64 * 3), ("occluded", C.c_uint64),
+                ("max_pops", C.c_uint64 * 3)]
 
     def as_dict(self) -> dict:
-        d = {k: list(getattr(self, k)) for k in ("rays", "pops", "internal_entered", "leaf_entered", "hits")}
+        d = {k: list(getattr(self, k)) for k in ("rays", "pops", "internal_entered", "leaf_entered", "hits",
+                                                  "max_pops")}
         d["occluded"] = int(self.occluded)
         return d
 

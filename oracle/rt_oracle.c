@@ -190,7 +190,7 @@ static int intersect_tri(const Ray* r, const orc_tri* tri, float tmin, float tma
     return 1;
 }
 
-typedef struct { uint64_t pops, internal, leaf; } TravCount;
+typedef struct { uint64_t pops, internal, leaf, max_pops; } TravCount;
 
 /* G/include/query.h:224-311 */
 static void search_bvh(int numTriangles, const Ray* ray, const orc_node* nodes,
@@ -206,9 +206,11 @@ static void search_bvh(int numTriangles, const Ray* ray, const orc_node* nodes,
     enum { CAP = 512 };
     uint32_t stack[CAP];
     int sp = 0, overflow = 0;
+    uint64_t pops = 0;
     stack[sp++] = 0;
     while (sp > 0) {
         const uint32_t n = stack[--sp];
+        ++pops;
         if (tc) tc->pops++;
         if (!intersect_aabb(ray, &aabbs[n], (double)tmin, (double)bestT)) continue;
         const orc_node node = nodes[n];
@@ -232,6 +234,7 @@ static void search_bvh(int numTriangles, const Ray* ray, const orc_node* nodes,
             if (sp < CAP) stack[sp++] = node.right; else overflow = 1;
         }
     }
+    if (tc && pops > tc->max_pops) tc->max_pops = pops;
     if (overflow) {
         for (int i = 0; i < numTriangles; ++i) {
             Hit rec;
@@ -473,6 +476,7 @@ int orc_render_g(size_t num_triangles, int W, int H, const orc_camera* cam, orc_
                 total.pops[k] += c.tc[k].pops;
                 total.internal_entered[k] += c.tc[k].internal;
                 total.leaf_entered[k] += c.tc[k].leaf;
+                if (c.tc[k].max_pops > total.max_pops[k]) total.max_pops[k] = c.tc[k].max_pops;
                 total.hits[k] += c.hits[k];
             }
             total.occluded += c.occluded;

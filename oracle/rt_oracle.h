@@ -38,6 +38,7 @@ typedef struct { orc_vec3 center, pixel00, du, dv; int32_t width, height; } orc_
 typedef struct {
     uint64_t rays[3], pops[3], internal_entered[3], leaf_entered[3], hits[3];
     uint64_t occluded;
+    uint64_t max_pops[3];  /* the most pops of one SearchBVH call */
 } orc_stats;
 
 /* std::mt19937(seed) + uniform_real_distribution<float>(0,1), libstdc++ generate_canonical;

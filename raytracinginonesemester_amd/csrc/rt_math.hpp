@@ -126,15 +126,9 @@ __host__ __device__ inline bool box_hit_exact(const RayPre& r, const BoxP& b, do
     double t0 = tmin, t1 = tmax;
     // No register-pinning asm here: an empty asm "+v" on o/d (to keep the compiler from hoisting
     // double(o) and 1/double(d) out of the traversal loops) measured no faster and, in the 6-wave
-    // build, exposed a miscompile of the bounce and binary-record kernels (golden parity failures).
-#ifndef RT_EXP_ASM_PIN
+    // build, exposed a miscompile of the bounce and binary-record kernels (golden parity failures;
+    // DESIGN.md §7).
     const float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
-#else  // reproducer of the round-1 failure: the removed register-pinning asm
-    float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
-#if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(d[0]), "+v"(d[1]), "+v"(d[2]));
-#endif
-#endif
     const float mn[3] = {b.x.x, b.y.x, b.z.x}, mx[3] = {b.x.y, b.y.y, b.z.y};
     bool ok = true;
 #pragma unroll

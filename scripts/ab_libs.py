@@ -26,6 +26,7 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--no-check", action="store_true", help="timing experiments whose frames differ by design")
+ap.add_argument("--flags", type=int, default=0, help="rt_render_opts.flags for every build (e.g. 8: RT_FLAG_NO_WAVEFRONT)")
 ap.add_argument("libs", nargs="+")
 a = ap.parse_args()
 
@@ -47,7 +48,8 @@ for r in range(a.rounds):
     for name, h, ds in builds:
         _lib._lib = h
         for _ in range(a.reps):
-            img = ds.render(cam, spp=cfg["spp"], max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"])
+            img = ds.render(cam, spp=cfg["spp"], max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
+                            diffuse_bounce=hs.settings["diffuse_bounce"], flags=a.flags)
         times[name] += list(ds.kernel_times(a.reps))
         ftimes[name] += list(ds.frame_times(a.reps))
         if ref is None:

@@ -152,6 +152,26 @@ def test_c3_full_frame_matches_reference(flags, tiles):
     assert diff.max() <= 1
 
 
+@pytest.mark.parametrize("name", ["c3b_small", "frog_bounce", "cornell", "sphere_single"])
+@pytest.mark.parametrize("flags", [0, rt._lib.RT_FLAG_NO_WAVEFRONT, rt._lib.RT_FLAG_BINARY])
+def test_bounce_paths_wavefront_and_in_kernel(name, flags):
+    """Multi-bounce frames traced depth by depth over compacted path queues (the default:
+    render kernel for depth 0, bounce_kernel per further depth, finish_kernel for the pixel sums)
+    and inside the render kernel (RT_FLAG_NO_WAVEFRONT): the reference's outputs bit for bit."""
+    meta = golden_meta(name)
+    assert meta["max_depth"] > 1
+    scene = G_SCENES[name]
+    hs = host_scene(scene)
+    cam = hs.camera(meta["width"], meta["height"])
+    rgb, hi, ht = _device_scene(scene).render(cam, spp=meta["spp"], max_depth=meta["max_depth"],
+                                              diffuse_bounce=bool(meta["diffuse_bounce"]),
+                                              miss_color=hexv(meta["miss_color"]), aov=True, flags=flags)
+    assert np.array_equal(hi.reshape(-1), golden_array(name, "hits.i32.gz", np.int32))
+    assert np.array_equal(ht.reshape(-1).view(np.uint32),
+                          golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
+    _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
+
+
 def test_c3b_full_frame_matches_reference():
     """c3b: frog.json as shipped (max_bounces 8, diffuse bounces) at 1920x1080x16 against the
     reference's own full-size outputs (hit AOVs by sha256, float frame, P6 file)."""

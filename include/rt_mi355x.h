@@ -207,9 +207,7 @@ typedef struct {
 
 enum {
     RT_FLAG_NO_CULL = 1,      /* disable tile culling against the root box (A/B; same output) */
-    RT_FLAG_BINARY = 4,       /* wave traversal over the binary nodes, not the 4-ary records */
-    RT_FLAG_NO_WAVEFRONT = 8  /* max_depth > 1: trace every path's bounces inside the render kernel
-                                 instead of depth by depth over compacted queues (A/B; same output) */
+    RT_FLAG_BINARY = 4        /* wave traversal over the binary nodes, not the 4-ary records */
 };
 
 enum {

@@ -21,7 +21,6 @@ RT_KERNEL_AUTO, RT_KERNEL_WAVE, RT_KERNEL_LANE, RT_KERNEL_WAVE_PIXELS = 0, 1, 2,
 RT_TILES_AUTO, RT_TILES_LINEAR, RT_TILES_XCD_CHUNK, RT_TILES_ROWS = 0, 1, 2, 3
 RT_FLAG_NO_CULL = 1
 RT_FLAG_BINARY = 4
-RT_FLAG_NO_WAVEFRONT = 8
 RT_DELIVER_P6, RT_DELIVER_F32, RT_DELIVER_DEVICE, RT_DELIVER_NONE = 0, 1, 2, 3
 RT_GATHER_AUTO, RT_GATHER_RCCL, RT_GATHER_DIRECT, RT_GATHER_HOST_SHARED = 0, 1, 2, 3
 RT_RENDERER_SELF_SEND = 1

@@ -99,15 +99,6 @@ struct SceneView {
 
 __device__ __forceinline__ f3 scene_bmax(const SceneView& sc) { return mk(sc.bmax[0], sc.bmax[1], sc.bmax[2]); }
 
-// One queued bounce ray of the wavefront multi-bounce path (48 B): the ray, the path's
-// throughput and RNG state after the bounce, and the sample it belongs to.
-struct alignas(16) BounceRay {
-    float o[3], d[3], thr[3];
-    uint32_t rng;
-    uint32_t sample;  // pix * spp + s (pix = local row * W + x)
-    uint32_t pad;
-};
-
 struct RenderParams {
     SceneView sc;
     f3 cam_center, cam_p00, cam_du, cam_dv;
@@ -150,17 +141,6 @@ struct RenderParams {
     // W*H*spp by definition and counted on the host), [3] camera rays of the tiles the culling
     // passes left to the render kernel (the camera rays that are actually traversed)
     unsigned long long* ray_count;
-    // Wavefront multi-bounce (max_depth > 1, WAVE sample kernels): the render kernel traces depth
-    // 0 and queues the paths that bounce; bounce_kernel traces depth `depth` of the queued paths
-    // (one lane per path, compacted) and queues the next; finish_kernel sums each pixel's
-    // samples.  srad: per-sample radiance so far (3 floats at 3 * sample, unclamped, accumulated
-    // in depth order as TraceRayIterative does); queue counts in the frame's counter set.
-    float* srad;
-    const BounceRay* bq_in;
-    BounceRay* bq_out;
-    uint32_t* bq_count_in;
-    uint32_t* bq_count_out;
-    int32_t depth;
 };
 
 // ---- wave primitives ------------------------------------------------------------------
@@ -962,35 +942,13 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, con
 }
 
 
-// Wave-aggregated append of the lanes' bounced paths to P.bq_out (every lane of the wave calls
-// it): one atomic per wave; a path's next depth is traced by bounce_kernel.
-__device__ __forceinline__ void queue_bounce(const RenderParams& P, bool push, const RayPre& ray, f3 thr,
-                                             uint32_t rng, uint32_t sample) {
-    const uint64_t m = ballot(push);
-    if (m == 0) return;
-    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-    uint32_t base = 0;
-    if (lane_id() == leader) base = atomicAdd(P.bq_count_out, (uint32_t)__popcll(m));
-    base = rdlane(base, leader);
-    if (push) {
-        const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1));
-        float4* q = reinterpret_cast<float4*>(P.bq_out + idx);
-        q[0] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.d.x);
-        q[1] = make_float4(ray.d.y, ray.d.z, thr.x, thr.y);
-        q[2] = make_float4(thr.z, __uint_as_float(rng), __uint_as_float(sample), 0.f);
-    }
-}
-
 // One camera sample through TraceRayIterative (query.h:156-220) + ShadeDirect (shader.h).
 // All lanes of a wave call it; `valid` marks lanes owning a sample.  D1: max_depth == 1 (no
 // bounce; the configuration the benchmarks run).
-// WF (wavefront multi-bounce, max_depth > 1): only depth 0 here; the sample's radiance goes to
-// P.srad[sample] and a path that bounces is queued for bounce_kernel.
-template <int MODE, bool D1, bool WF = false>
+template <int MODE, bool D1>
 // The primary-hit AOV (P.hit_idx / P.hit_t at element aov, when aov >= 0) is written as soon as
 // the camera ray's traversal ends, so nothing of it stays live across the shading.
-__device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int64_t aov, float* park,
-                           uint32_t sample = 0) {
+__device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int64_t aov, float* park) {
     const SceneView& sc = P.sc;
     RayPre ray = camera_ray(P, valid, x, y, s);
     count_rays<MODE>(P.ray_count, 3, valid && P.max_depth > 0);  // camera rays that reach traversal
@@ -1020,7 +978,7 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
     f3 thr = mk(1.f, 1.f, 1.f);
     const int max_depth = P.max_depth;
     bool alive = valid && max_depth > 0;
-    for (int depth = 0; depth < (WF ? 1 : max_depth); ++depth) {
+    for (int depth = 0; depth < max_depth; ++depth) {
         if (ballot(alive) == 0) break;
         HitState hs;
         if (depth > 0) count_rays<MODE>(P.ray_count, 2, alive);
@@ -1110,15 +1068,6 @@ __device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int 
                 alive = false;
             }
         }
-    }
-    if constexpr (WF) {
-        if (valid) {
-            float* o = P.srad + 3 * (size_t)sample;
-            o[0] = radiance.x;
-            o[1] = radiance.y;
-            o[2] = radiance.z;
-        }
-        queue_bounce(P, alive, ray, thr, rng, sample);
     }
     return clamp01(radiance);
 }
@@ -1313,9 +1262,7 @@ constexpr int NCLASS = 3;                        // heavy cost classes
 // few wide scalar loads; their appends are few).
 constexpr int HEAVY_SLOT0 = 9;
 constexpr int CUT_SLOT0 = HEAVY_SLOT0 + 8 * NCLASS;  // then 8: lengths of the cut pass's survivor lists
-constexpr int BQ_SLOT0 = CUT_SLOT0 + 8;  // then MAX_WF_DEPTH: bounce queue lengths, slot d = paths of depth d
-constexpr int MAX_WF_DEPTH = 64;         // deeper paths take the in-wave bounce loop
-constexpr int COUNTER_SLOTS = BQ_SLOT0 + MAX_WF_DEPTH;
+constexpr int COUNTER_SLOTS = CUT_SLOT0 + 8;
 constexpr int COUNTER_SET_U32 = COUNTER_SLOTS * COUNTER_STRIDE;
 __host__ __device__ constexpr int heavy_counter(int k, int q) { return (HEAVY_SLOT0 + 8 * k + q) * COUNTER_STRIDE; }
 __device__ __forceinline__ int queue_of_tile(const RenderParams& P, int tile) {
@@ -1570,7 +1517,7 @@ __device__ __forceinline__ int block_tile(const RenderParams& P, int b) {
 
 // One sample per lane: a block covers a tile_w x tile_h pixel tile x spp samples (spp a power
 // of two <= 256, tile_w*tile_h*spp == BLOCK); per-pixel sums run in sample order from LDS.
-template <int MODE, bool D1, int LS = 0, bool WF = false>
+template <int MODE, bool D1, int LS = 0>
 __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, float* col, int* kpix, float* park,
                                              const int* lds_zero) {
     const int t = (int)threadIdx.x;
@@ -1610,10 +1557,8 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
         // it, or addresses made from it, live (and spilled) across the shading.
         if (s == 0) kpix[t >> P.spp_log2] = pix;
         const int64_t aov = valid && P.hit_idx ? (int64_t)pix * P.spp + s : -1;
-        const f3 c = trace_sample<MODE, D1, WF>(P, valid, x, y, s, aov, park,
-                                                (uint32_t)(valid ? pix : 0) * (uint32_t)P.spp + (uint32_t)s);
+        const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, aov, park);
         RT_PHASE(P, x, r, 1);
-        if constexpr (WF) return;  // the pixel sums come after the last depth (finish_kernel)
         // The thread index again, from the wave's index and a lane id the compiler cannot
         // merge with the first one (mbcnt of a zero read back from LDS): keeping t itself live
         // across the traversals cost a 4-byte scratch spill per lane (c3: ~8 MB of writes per
@@ -1707,21 +1652,14 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, flo
 #define RT_RENDER_WAVES 7
 #endif
 // The multi-bounce kernels (D1 false): the bounce loop keeps more state live than the depth-1
-// shading (RNG, throughput, the ray, two rays' RayPre) and spills at 7 waves: c3b 9.70 ms at 7
-// waves (336 B scratch), 5.80 at 5 (240 B), 5.01 at 4 (84 B, 128 VGPRs).
+// shading (RNG, throughput, the ray, two rays' RayPre, the 4-ary record in the lane traversal).
+// c3b with the lane traversal over 4-ary records: 2.26 ms at 3 waves (167 VGPRs, no scratch)
+// vs 2.81 at 4 (164 B scratch); binary records at 4 waves 3.20 (profiles/r03/exp/).
 #ifndef RT_BOUNCE_WAVES
-#define RT_BOUNCE_WAVES 4
-#endif
-// Wavefront multi-bounce: depth 0 in the render kernel (the camera ray and its shadow rays) and
-// bounce_kernel (one queued path per lane).
-#ifndef RT_WF0_WAVES
-#define RT_WF0_WAVES 5
-#endif
-#ifndef RT_WFB_WAVES
-#define RT_WFB_WAVES 3
+#define RT_BOUNCE_WAVES 3
 #endif
 // Heavy-first dispatch: the kernel takes the heavy lists and records its tiles' costs.
-template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0, bool WF = false>
+template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0>
 __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
     __shared__ int kpix[SAMPLES ? BLOCK : 1];
@@ -1735,16 +1673,19 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
     __shared__ uint32_t t_start[BLOCK / 64], t_tile[BLOCK / 64];
     __shared__ int lds_zero;  // 0, written by every lane (samples_tile's fresh lane id)
     if constexpr (SAMPLES) lds_zero = 0;
-    if (P.tile_cost && lane_id() == 0) t_start[threadIdx.x / 64] = (uint32_t)wall_clock64();
+    // the wave's index in the block as a uniform value (threadIdx.x itself, kept live to the
+    // tile-cost write at the end, was spilled to scratch)
+    const uint32_t wv = uni((uint32_t)threadIdx.x) >> 6;
+    if (P.tile_cost && lane_id() == 0) t_start[wv] = (uint32_t)wall_clock64();
     const int tile = block_tile(P, (int)blockIdx.x);
     if (tile < 0) return;
-    if (P.tile_cost && lane_id() == 0) t_tile[threadIdx.x / 64] = (uint32_t)tile;
-    if constexpr (SAMPLES) samples_tile<MODE, D1, LS, WF>(P, tile, col, kpix, park, &lds_zero);
+    if (P.tile_cost && lane_id() == 0) t_tile[wv] = (uint32_t)tile;
+    if constexpr (SAMPLES) samples_tile<MODE, D1, LS>(P, tile, col, kpix, park, &lds_zero);
     else pixels_tile<MODE, D1>(P, tile, park);
     if (P.tile_cost && lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
         asm volatile("" ::: "memory");
-        const uint32_t d = (uint32_t)wall_clock64() - t_start[threadIdx.x / 64];
-        P.tile_cost[4 * (size_t)t_tile[threadIdx.x / 64] + threadIdx.x / 64] = (uint16_t)(d < 0xffffu ? d : 0xffffu);
+        const uint32_t d = (uint32_t)wall_clock64() - t_start[wv];
+        P.tile_cost[4 * (size_t)t_tile[wv] + wv] = (uint16_t)(d < 0xffffu ? d : 0xffffu);
     }
 #ifdef RT_WAVE_TIMES
     if (g_wave_times && lane_id() == 0) {
@@ -1753,158 +1694,6 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
         g_wave_times[k + 1] = wall_clock64();
     }
 #endif
-}
-
-// ---- wavefront multi-bounce: the rest of the queued paths ------------------------------------
-// TraceRayIterative's iterations from `depth` on (query.h:178-216) for every path the render
-// kernel queued after depth 0, one lane per path: the queue is compact, so a wave holds 64 live
-// paths, not the finished samples of a tile.  Each lane carries its path to the end (the frame's
-// time is then bounded by a wave's longest path, not by the sum over depths of the longest
-// traversal of each depth, as with one launch per depth: c3b 4.5 ms vs 3.2 with the bounces
-// inside the render kernel).  Rays are incoherent: the bounce ray and each light's shadow ray
-// take traverse_lane_lds.  The sample's radiance gets, per depth and in depth order, the miss
-// colour or ShadeDirect's Lo times the throughput, as the reference's loop adds them.
-// Grid-stride over the queue length (read on the device); waves leave together.
-template <int WAVES, bool WIDE>
-__global__ __launch_bounds__(BLOCK, WAVES) void bounce_kernel(RenderParams P) {
-    __shared__ uint32_t stk[LANE_LDS_CAP * BLOCK];
-    const SceneView& sc = P.sc;
-    const uint32_t n = ldc_u32(P.bq_count_in);
-    const uint32_t stride = gridDim.x * BLOCK;
-    for (uint32_t base = blockIdx.x * BLOCK + (threadIdx.x & ~63u); base < n; base += stride) {  // per wave
-        const uint32_t i = base + lane_id();
-        const bool valid = i < n;
-        float4 q0 = make_float4(0.f, 0.f, 0.f, 1.f), q1 = make_float4(0.f, 0.f, 0.f, 0.f), q2 = q1;
-        if (valid) {
-            const float4* e = reinterpret_cast<const float4*>(P.bq_in + i);
-            q0 = e[0];
-            q1 = e[1];
-            q2 = e[2];
-        }
-        RayPre ray = make_ray(mk(q0.x, q0.y, q0.z), mk(q0.w, q1.x, q1.y), scene_bmax(sc));
-        f3 thr = mk(q1.z, q1.w, q2.x);
-        uint32_t rng = __float_as_uint(q2.y);
-        const uint32_t sample = __float_as_uint(q2.z);
-        float* srad = P.srad + 3 * (size_t)sample;
-        f3 radiance = valid ? mk(srad[0], srad[1], srad[2]) : mk(0.f, 0.f, 0.f);
-        bool alive = valid;
-        for (int depth = P.depth; depth < P.max_depth; ++depth) {
-            if (ballot(alive) == 0) break;
-            HitState hs;
-            traverse_lane<WIDE>(sc, ray, alive, false, 0.0f, hs, stk + threadIdx.x);
-            const bool hit = alive && hs.slot >= 0;
-            SurfHit sh;
-            sh.tri = -1;
-            if (hit) sh = resolve_hit(sc, ray, hs.slot);
-            if (alive && !hit) {
-                radiance = add(radiance, mul(thr, P.miss));
-                alive = false;
-            }
-            // ShadeDirect (shader.h:65-110)
-            f3 N = mk(0.f, 0.f, 1.f), V = N, Lo = mk(0.f, 0.f, 0.f);
-            if (hit) {
-                const DevMaterial m = material_of(sc, sh.tri);
-                N = unit(sh.n);
-                V = unit(sub(ray.o, sh.p));
-                Lo = add(Lo, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 0.05f));
-                Lo = add(Lo, mk(m.emission[0], m.emission[1], m.emission[2]));
-            }
-            for (int li = 0; li < sc.num_lights; ++li) {
-                const DevLight& lt = sc.lights[li];
-                const f3 lpos = mk(lt.pos[0], lt.pos[1], lt.pos[2]);
-                float dist = 0.f;
-                bool need = false, lit = false;
-                f3 contrib = mk(0.f, 0.f, 0.f);
-                RayPre sray;
-                if (hit) {
-                    const f3 L = unit(sub(lpos, sh.p));
-                    const float NdotL = fmaxf(dot(N, L), 0.0f);
-                    if (NdotL > 0.0f) {
-                        const DevMaterial m = material_of(sc, sh.tri);
-                        const f3 f = eval_brdf(m, sh.n, V, L);
-                        const f3 rad = scale(mk(lt.color[0], lt.color[1], lt.color[2]), (float)lt.intensity);
-                        contrib = scale(mul(rad, f), NdotL);
-                        lit = true;
-                        // IsInShadow (shader.h:44-62)
-                        const f3 toL = sub(lpos, sh.p);
-                        dist = sqrtf(dot(toL, toL));
-                        if (dist > 0.0f) {
-                            need = true;
-                            sray = make_ray(add(sh.p, scale(N, RT_EPS)), divf(toL, dist), scene_bmax(sc));
-                        }
-                    }
-                }
-                HitState shs;
-                traverse_lane<WIDE>(sc, sray, need, true, dist, shs, stk + threadIdx.x);
-                const bool occluded = need && shs.slot >= 0 && shs.bestT < dist;
-                if (lit && !occluded) Lo = add(Lo, contrib);
-            }
-            if (hit) {
-                radiance = add(radiance, mul(thr, Lo));
-                // bounce (query.h:193-216); none after the last depth
-                if (depth + 1 < P.max_depth) {
-                    const DevMaterial m = material_of(sc, sh.tri);
-                    const float kd = m.kd, kr = m.kr, total = kd + kr;
-                    if (total <= 0.0f) {
-                        alive = false;
-                    } else {
-                        const f3 Nb = unit(sh.n);
-                        const float xi = rng_next(rng);
-                        if (P.diffuse_bounce && xi < kd / total) {
-                            f3 dd = random_unit_vector(rng);
-                            if (!(dot(dd, Nb) > 0.0f)) dd = mk(-dd.x, -dd.y, -dd.z);
-                            ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), dd, scene_bmax(sc));
-                            const float nl = fmaxf(dot(Nb, dd), 0.0f);
-                            thr = mul(thr, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 2.0f * nl));
-                        } else {
-                            const f3 I = unit(ray.d);
-                            const f3 refl = sub(I, scale(Nb, 2.0f * dot(I, Nb)));
-                            ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), refl, scene_bmax(sc));
-                            thr = mul(thr, scale(mk(m.spec[0], m.spec[1], m.spec[2]), kr));
-                        }
-                        if (thr.x < 1e-4f && thr.y < 1e-4f && thr.z < 1e-4f) alive = false;
-                    }
-                } else {
-                    alive = false;
-                }
-            }
-        }
-        if (valid) {
-            srad[0] = radiance.x;
-            srad[1] = radiance.y;
-            srad[2] = radiance.z;
-        }
-    }
-}
-
-// ---- wavefront multi-bounce: the pixel sums -------------------------------------------------
-// After the last depth, each rendered tile's pixels: col = col + clamp(radiance) over the
-// samples in order, then col / float(spp) (query.cu:146-163, query.h:219), with the P6 samples
-// (write_p6 defaults).  Same block -> tile mapping as the render kernel; one lane per pixel.
-__global__ __launch_bounds__(BLOCK) void finish_kernel(RenderParams P) {
-    const int tile = block_tile(P, (int)blockIdx.x);
-    if (tile < 0) return;
-    const int t = (int)threadIdx.x;
-    if (t >= P.tile_w * P.tile_h) return;
-    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-    const int x = tx * P.tile_w + t % P.tile_w, r = ty * P.tile_h + t / P.tile_w;
-    if (x >= P.W || r >= P.rows) return;
-    const size_t pix = (size_t)r * P.W + x;
-    const float* sr = P.srad + 3 * pix * (size_t)P.spp;
-    f3 acc = mk(0.f, 0.f, 0.f);
-    for (int k = 0; k < P.spp; ++k) acc = add(acc, clamp01(mk(sr[3 * k], sr[3 * k + 1], sr[3 * k + 2])));
-    const float rs = 1.0f / (float)P.spp;  // spp a power of two: x / 2^k == x * 2^-k
-    const f3 px = mk(acc.x * rs, acc.y * rs, acc.z * rs);
-    if (P.rgb) {
-        P.rgb[3 * pix] = px.x;
-        P.rgb[3 * pix + 1] = px.y;
-        P.rgb[3 * pix + 2] = px.z;
-    }
-    if (P.p6) {
-        P.p6[3 * pix] = rtp::p6_default_sample(px.x);
-        P.p6[3 * pix + 1] = rtp::p6_default_sample(px.y);
-        P.p6[3 * pix + 2] = rtp::p6_default_sample(px.z);
-    }
 }
 
 // ---- HW1 brute force (HW1/src/render.cpp:72-116) ----------------------------------------
@@ -2373,8 +2162,6 @@ struct rt_scene {
     // heavy-first dispatch: per-tile wave durations of the last frames (4 x u16 per tile) for
     // the tile geometry cost_key, and the latest finished frame's render-kernel time
     DevBuf cost;
-    // wavefront multi-bounce: per-sample radiance and the two bounce queues (grow-only)
-    DevBuf srad, bq[2];
     uint64_t cost_key = 0;
     float kernel_ms_est = 0.f;
     int last_heavy_cap = 0;
@@ -2833,13 +2620,6 @@ void launch_mode(const RenderParams& P, const Launch& L) {
     }
 }
 
-// Depth 0 of a wavefront multi-bounce frame (the sample kernels, max_depth > 1).
-template <int MODE>
-void launch_wf(const RenderParams& P, const dim3& grid, const Launch& L) {
-    if (P.half_waves) launch_render(render_tiles_kernel<MODE, true, false, RT_WF0_WAVES, 1, true>, grid, P, L);
-    else launch_render(render_tiles_kernel<MODE, true, false, RT_WF0_WAVES, 0, true>, grid, P, L);
-}
-
 template <int MODE>
 void launch(const RenderParams& P, bool samples, const Launch& L) {
     if (samples) launch_mode<MODE, true>(P, L);
@@ -3074,23 +2854,6 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         if ((rc = s->work.alloc(work_bytes)) != RT_OK) return rc;
         s->counters_dirty = true;
     }
-    // Wavefront multi-bounce (max_depth > 1 on the WAVE sample kernels): depth 0 in the render
-    // kernel, then one bounce_kernel launch per depth over the compacted queue of the paths still
-    // going, then finish_kernel for the pixel sums.  The buffers hold every sample of the frame
-    // (a bound on the queued paths; 60 B per sample: c3b 2.0 GB of 288).
-    const uint64_t nsamples = uint64_t(rows) * uint64_t(W) * uint64_t(o->spp);
-    const bool wf = samples && o->max_depth > 1 && o->max_depth <= MAX_WF_DEPTH && mode == RT_KERNEL_WAVE &&
-                    !s->deep && (P.sc.wide ? s->lane_wide : s->lane_stack) && nsamples < (uint64_t(1) << 31) &&
-                    !(o->flags & RT_FLAG_NO_WAVEFRONT);
-    if (wf && (s->srad.n < nsamples * 12 || s->bq[0].n < nsamples * sizeof(BounceRay))) {
-        if (k > 0) {  // the old buffers may still be in use
-            HIP_TRY(hipStreamSynchronize(s->prep));
-            HIP_TRY(hipEventSynchronize(ev1_of(k - 1)));
-        }
-        if ((rc = s->srad.alloc(nsamples * 12)) != RT_OK) return rc;
-        for (DevBuf& b : s->bq)
-            if ((rc = b.alloc(nsamples * sizeof(BounceRay))) != RT_OK) return rc;
-    }
     // This frame's outputs against the previous frame's: overlapping ranges (a caller reusing
     // one buffer) make the pre-passes, which write the culled tiles' pixels, wait for the
     // previous render kernel; distinct buffers (rt_renderer's frame slots) let them overlap it.
@@ -3147,29 +2910,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
-        const Launch L{st, s->evm[slot], wf ? nullptr : s->ev1[slot]};
-        if (wf) {
-            // paths of depth d are queued in bq[d & 1], their count in counter slot BQ_SLOT0 + d
-            auto slot_of = [&](int d) { return P.live_count + (BQ_SLOT0 + d) * COUNTER_STRIDE; };
-            P.srad = static_cast<float*>(s->srad.p);
-            P.bq_out = static_cast<BounceRay*>(s->bq[1].p);
-            P.bq_count_out = slot_of(1);
-            const dim3 grid((P.tiles_virtual + 7) / 8 * 8 + 8 * NCLASS * P.heavy_cap);
-            if (P.sc.wide) launch_wf<RT_KERNEL_WAVE | MODE_WIDE>(P, grid, L);
-            else launch_wf<RT_KERNEL_WAVE>(P, grid, L);
-            HIP_TRY(hipGetLastError());
-            const dim3 bgrid(unsigned(std::min<uint64_t>((nsamples + BLOCK - 1) / BLOCK, uint64_t(8) * s->cus)));
-            RenderParams B = P;
-            B.depth = 1;
-            B.bq_in = static_cast<const BounceRay*>(s->bq[1].p);
-            B.bq_count_in = slot_of(1);
-            if (P.sc.wide) hipLaunchKernelGGL((bounce_kernel<RT_WFB_WAVES, true>), bgrid, dim3(BLOCK), 0, st, B);
-            else hipLaunchKernelGGL((bounce_kernel<RT_WFB_WAVES, false>), bgrid, dim3(BLOCK), 0, st, B);
-            HIP_TRY(hipGetLastError());
-            hipExtLaunchKernelGGL(finish_kernel, grid, dim3(BLOCK), 0, st, nullptr, s->ev1[slot], 0, P);
-            HIP_TRY(hipGetLastError());
-            return RT_OK;
-        }
+        const Launch L{st, s->evm[slot], s->ev1[slot]};
         if (s->deep) launch<MODE_DEEP>(P, samples, L);
         else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, L);
         else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, L);

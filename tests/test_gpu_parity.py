@@ -153,11 +153,11 @@ def test_c3_full_frame_matches_reference(flags, tiles):
 
 
 @pytest.mark.parametrize("name", ["c3b_small", "frog_bounce", "cornell", "sphere_single"])
-@pytest.mark.parametrize("flags", [0, rt._lib.RT_FLAG_NO_WAVEFRONT, rt._lib.RT_FLAG_BINARY])
-def test_bounce_paths_wavefront_and_in_kernel(name, flags):
-    """Multi-bounce frames traced depth by depth over compacted path queues (the default:
-    render kernel for depth 0, bounce_kernel per further depth, finish_kernel for the pixel sums)
-    and inside the render kernel (RT_FLAG_NO_WAVEFRONT): the reference's outputs bit for bit."""
+@pytest.mark.parametrize("flags", [0, rt._lib.RT_FLAG_BINARY])
+def test_bounce_paths_per_lane_traversal(name, flags):
+    """Multi-bounce frames: camera rays and their shadow rays on the wave-shared DFS, bounce rays
+    and theirs on each lane's own DFS (traverse_lane_lds over 4-ary or binary records): the
+    reference's outputs bit for bit."""
     meta = golden_meta(name)
     assert meta["max_depth"] > 1
     scene = G_SCENES[name]

@@ -120,7 +120,6 @@ struct RenderParams {
     int32_t cut_force;    // test every candidate in tile_cut_kernel (no pass-through)
     int32_t nqueues;
     int32_t queue_cap;
-    int32_t tiles_virtual;                            // virtual blocks (planned_tile)
     float* __restrict__ rgb;
     int32_t* __restrict__ hit_idx;
     float* __restrict__ hit_t;
@@ -183,6 +182,7 @@ __device__ unsigned long long g_rt_stats[24];
 // per-wave phase ends (primary traversal, whole sample) and per tile the number of cut boxes
 // its rays may meet (tile_cut_kernel)
 __device__ unsigned long long* g_wave_times;
+__device__ uint32_t* g_wave_meta;  // per item: block << 8 | XCC << 4 | first item << 2 | wave in block
 __device__ unsigned long long* g_wave_phase;
 __device__ int* g_cut_counts;
 #define RT_PHASE(P, x, y, k)                                                                           \
@@ -755,7 +755,7 @@ __device__ __forceinline__ void traverse_at(const SceneView& sc, int depth, cons
     if constexpr (MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0) {
         constexpr bool W = (MODE & MODE_WIDE) != 0;
         if (depth > 0 && lane_ok<W>(sc)) {
-            traverse_lane<W>(sc, r, active, any_hit, any_hit_dist, hs, reinterpret_cast<uint32_t*>(lds) + threadIdx.x);
+            traverse_lane<W>(sc, r, active, any_hit, any_hit_dist, hs, reinterpret_cast<uint32_t*>(lds));
             return;
         }
     }
@@ -855,7 +855,7 @@ template <int MODE>
 __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, const RayPre& ray, const HitState& hs,
                                        float* park_lds) {
     const SceneView& sc = P.sc;
-    const Park pk{park_lds + threadIdx.x};
+    const Park pk{park_lds};
     bool valid = valid_in;
     bool hit = valid && hs.slot >= 0;
     // radiance = 0 + (1,1,1) * missColor on a miss (query.h:181-183), 0 + (1,1,1) * Lo on a hit:
@@ -948,7 +948,9 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, con
 template <int MODE, bool D1>
 // The primary-hit AOV (P.hit_idx / P.hit_t at element aov, when aov >= 0) is written as soon as
 // the camera ray's traversal ends, so nothing of it stays live across the shading.
-__device__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int64_t aov, float* park) {
+// park: the lane's own LDS slot (slot k of the lane at park[k * BLOCK]).
+__device__ __forceinline__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int64_t aov,
+                                          float* park) {
     const SceneView& sc = P.sc;
     RayPre ray = camera_ray(P, valid, x, y, s);
     count_rays<MODE>(P.ray_count, 3, valid && P.max_depth > 0);  // camera rays that reach traversal
@@ -1262,7 +1264,8 @@ constexpr int NCLASS = 3;                        // heavy cost classes
 // few wide scalar loads; their appends are few).
 constexpr int HEAVY_SLOT0 = 9;
 constexpr int CUT_SLOT0 = HEAVY_SLOT0 + 8 * NCLASS;  // then 8: lengths of the cut pass's survivor lists
-constexpr int COUNTER_SLOTS = CUT_SLOT0 + 8;
+constexpr int HEAD_SLOT0 = CUT_SLOT0 + 8;  // then 8: the render kernel's work-queue heads (one per XCD)
+constexpr int COUNTER_SLOTS = HEAD_SLOT0 + 8;
 constexpr int COUNTER_SET_U32 = COUNTER_SLOTS * COUNTER_STRIDE;
 __host__ __device__ constexpr int heavy_counter(int k, int q) { return (HEAVY_SLOT0 + 8 * k + q) * COUNTER_STRIDE; }
 __device__ __forceinline__ int queue_of_tile(const RenderParams& P, int tile) {
@@ -1455,72 +1458,62 @@ __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
     }
 }
 
-// Virtual block -> live tile, without atomics.  With 8 lists there are tiles_virtual =
-// 8 * tiles_x * ceil(tiles_y / 8) virtual blocks, at least 8 times the longest list (RT_TILES_ROWS
-// puts at most tiles_x * ceil(tiles_y / 8) tiles in a list, RT_TILES_XCD_CHUNK at most
-// ceil(tiles / 8)); virtual block j = 8*i + k takes slot i of list k, or nothing.  Dispatch
-// deals blocks round-robin over the XCDs and a real block runs the virtual blocks
-// blockIdx.x + m*gridDim.x with gridDim.x a multiple of 8, so list k is rendered on XCD k.
-// With one list (RT_TILES_LINEAR) virtual block j takes slot j.  The list lengths are read once
-// per block: the lists are immutable while the render kernel runs, so they and their entries
-// are read through the constant address space (scalar loads).
-
-__device__ __forceinline__ int list_length(const RenderParams& P, int q) {
-    return (int)ldc_u32(&P.live_count[q * COUNTER_STRIDE]);
+// The render kernel's work: list q's entries, its heavy lists' first (classes in order,
+// heaviest first; each capped at heavy_cap), then its survivors (the cut pass's list, or the
+// cull pass's live list when there is no cut).  The lists are immutable while the render
+// kernel runs, so their lengths and entries are read through the constant address space
+// (scalar loads).
+__device__ __forceinline__ int work_length(const RenderParams& P, int q, int& heavy) {
+    heavy = 0;
+    if (P.heavy_cap > 0)
+        for (int k = 0; k < NCLASS; ++k) heavy += min((int)ldc_u32(P.live_count + heavy_counter(k, q)), P.heavy_cap);
+    const int slot = P.sc.ncut > 0 ? CUT_SLOT0 + q : q;
+    return heavy + (int)ldc_u32(&P.live_count[slot * COUNTER_STRIDE]);
 }
 
-__device__ __forceinline__ int planned_tile(const RenderParams& P, int len, int q, int i) {
-    return i < len ? (int)ldc_u32(reinterpret_cast<const uint32_t*>(P.live_tiles) + (size_t)q * P.queue_cap + i) : -1;
+// cls: the entry's heavy class (0 heaviest), NCLASS for a survivor.
+__device__ __forceinline__ int work_tile(const RenderParams& P, int q, int e, int heavy, int& cls) {
+    const uint32_t* list;
+    cls = NCLASS;
+    if (e < heavy) {
+        int k = 0;
+        for (; k < NCLASS - 1; ++k) {
+            const int n = min((int)ldc_u32(P.live_count + heavy_counter(k, q)), P.heavy_cap);
+            if (e < n) break;
+            e -= n;
+        }
+        list = reinterpret_cast<const uint32_t*>(P.heavy_tiles) + ((size_t)k * 8 + q) * P.heavy_cap;
+        cls = k;
+    } else {
+        e -= heavy;
+        list = reinterpret_cast<const uint32_t*>(P.sc.ncut > 0 ? P.cut_tiles : P.live_tiles) + (size_t)q * P.queue_cap;
+    }
+    return (int)ldc_u32(list + e);
 }
 
-// Render block b -> its pixel tile, or -1 (a block with no tile leaves at once).
-__device__ __forceinline__ int block_tile(const RenderParams& P, int b) {
-    int tile = -1;
-    if (b >= P.tiles_virtual + 8 * NCLASS * P.heavy_cap) return -1;
-    // Virtual index i = b >> 3 of list q = b & 7 (the block's XCD).  Heavy phase: the first
-    // NCLASS * heavy_cap indices, list q's heavy entries (its classes in order, heaviest first)
-    // and then nothing; then the list's slots.  Dispatch is in block order across the XCDs, so
-    // every list's heavy tiles go before any list's normal slots.  A block reads only its own
-    // list's counters: empty blocks must leave at once (every extra scalar load of the ~10^5
-    // empty blocks showed in the kernel time).  (Sizing the heavy phase to the longest
-    // list's heavy entries instead, with the cut pass's last wave computing that maximum, measured
-    // no faster: 0.2245 vs 0.2224 ms, and the done-count fences slowed the cut pass.)
-    const int q = P.nqueues == 1 ? 0 : (b & 7);
-    int i = P.nqueues == 1 ? b : (b >> 3);
-    if (P.heavy_cap > 0) {
-        if (i < NCLASS * P.heavy_cap) {
-            int k = 0;
-            for (; k < NCLASS; ++k) {
-                const int n = min((int)ldc_u32(P.live_count + heavy_counter(k, q)), P.heavy_cap);
-                if (i < n) break;
-                i -= n;
-            }
-            if (k == NCLASS) return -1;
-            tile = (int)ldc_u32(reinterpret_cast<const uint32_t*>(P.heavy_tiles) + ((size_t)k * 8 + q) * P.heavy_cap + i);
-            i = -1;
-        } else {
-            i -= NCLASS * P.heavy_cap;
-        }
-    }
-    if (i >= 0) {
-        if (P.sc.ncut > 0) {  // the cut pass's survivors
-            const int len = (int)ldc_u32(&P.live_count[(CUT_SLOT0 + q) * COUNTER_STRIDE]);
-            if (i >= len) return -1;
-            tile = (int)ldc_u32(reinterpret_cast<const uint32_t*>(P.cut_tiles) + (size_t)q * P.queue_cap + i);
-        } else {
-            tile = planned_tile(P, list_length(P, q), q, i);
-            if (tile < 0) return -1;
-        }
-    }
-    return tile;
+// A lane id the compiler cannot merge with any other (mbcnt of an opaque zero): one kept for a
+// whole loop of items is live across all of them (and spills).
+__device__ __forceinline__ uint32_t fresh_lane_id() {
+    uint32_t z = 0;
+    asm volatile("" : "+s"(z));
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, z));
+}
+
+// The next work item of a queue: one returning device-scope atomic from lane 0 (a vector
+// atomic), the value made wave-uniform.
+__device__ __forceinline__ uint32_t dequeue(uint32_t* head, uint32_t lane) {
+    uint32_t v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return uni(v);
 }
 
 // One sample per lane: a block covers a tile_w x tile_h pixel tile x spp samples (spp a power
 // of two <= 256, tile_w*tile_h*spp == BLOCK); per-pixel sums run in sample order from LDS.
 template <int MODE, bool D1, int LS = 0>
-__device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, float* col, int* kpix, float* park,
-                                             const int* lds_zero) {
-    const int t = (int)threadIdx.x;
+// qw: the wave's quarter of the tile (its work item); LDS is indexed by the thread's own slot,
+// t (the thread index, made afresh for each item).
+__device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, uint32_t qw, int t, float* col,
+                                             int* kpix, float* park, const int* lds_zero) {
     const uint32_t wv = uni((uint32_t)t) >> 6;  // the wave's index in the block (an SGPR)
     // LS = 1, half waves (band shards of a multi-GPU frame, spp <= 32): each wave traces 32
     // samples in its low lanes, so a tile's longest wave, which bounds a short kernel, has half
@@ -1528,7 +1521,7 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
     // parameter: a run-time flag here cost the full-wave c3 kernel 0.8 % (register allocation).
     constexpr int wl = 64 >> LS;  // lanes that trace
     const bool on = (t & 63) < wl;
-    const int lt = ((t >> 6) * wl) | (t & (wl - 1));
+    const int lt = ((int)qw * wl) | (t & (wl - 1));
     {
         const int s = lt & (P.spp - 1);  // spp and tile_w are powers of two here
         const int pit = lt >> P.spp_log2;
@@ -1557,7 +1550,7 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
         // it, or addresses made from it, live (and spilled) across the shading.
         if (s == 0) kpix[t >> P.spp_log2] = pix;
         const int64_t aov = valid && P.hit_idx ? (int64_t)pix * P.spp + s : -1;
-        const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, aov, park);
+        const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, aov, park + t);
         RT_PHASE(P, x, r, 1);
         // The thread index again, from the wave's index and a lane id the compiler cannot
         // merge with the first one (mbcnt of a zero read back from LDS): keeping t itself live
@@ -1609,8 +1602,8 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, fl
 
 // General spp: one pixel per lane looping over its samples in order (query.cu:146-163).
 template <int MODE, bool D1>
-__device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, float* park) {
-    const int t = (int)threadIdx.x;
+__device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, uint32_t qw, int tid, float* park) {
+    const int t = (int)((qw << 6) | (tid & 63));
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int x = tx * P.tile_w + t % P.tile_w;
     const int r = ty * P.tile_h + t / P.tile_w;
@@ -1619,7 +1612,7 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, flo
     f3 acc = mk(0.f, 0.f, 0.f);
     for (int s = 0; s < P.spp; ++s) {
         const int64_t aov = valid && P.hit_idx ? ((int64_t)r * P.W + x) * P.spp + s : -1;
-        acc = add(acc, trace_sample<MODE, D1>(P, valid, x, y, s, aov, park));
+        acc = add(acc, trace_sample<MODE, D1>(P, valid, x, y, s, aov, park + tid));
     }
     if (valid) {
         const float fs = (float)P.spp;
@@ -1638,16 +1631,15 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, flo
     }
 }
 
-// One virtual block (planned_tile) per workgroup; a block whose slot holds no live tile leaves
-// at once.  (One-wave blocks, each a quarter of a tile, so that a CU takes new work one wave slot
-// at a time: c3 0.286 vs 0.223 ms, c5 93 vs 84 ms — 4x the workgroups, empty ones included, cost
-// more in dispatch than the freer packing gains.)  (Looping a block over several slots measured no faster on c3 and, by keeping the
-// per-sample invariants live across the loop, spilled 224 B instead of 144 B per lane: c5 -6 %
-// without the loop.)
-// WAVES: waves per SIMD the kernel is compiled for.  With the shading spills removed 7 waves
-// (72 VGPRs) is fastest: c3 7 waves 0.267 ms < 6 waves 0.273 < 5 waves 0.294 (one box,
-// interleaved), and with traverse_wave_split c5 too (76.0 ms vs 84.9 for the 8-wave packed-FMA
-// build that was the big-scene choice before).
+// A persistent grid (the blocks one dispatch keeps resident) over per-XCD work queues: block b
+// serves queue g = b % 8 (dispatch deals blocks round-robin over the XCDs, so queue g is served
+// on XCD g and list g's tiles share an L2).  With 8 lists queue g is list g; with one list
+// (RT_TILES_LINEAR) queue g takes the list's entries g, g+8, ....  Each wave dequeues its own
+// item, a quarter of a tile (BLOCK / 64 waves per tile), so a wave that finishes early takes
+// the next quarter at once; with spp > 64 a pixel's samples span the block's waves and the
+// block takes whole tiles.  (One block per live-list slot of a frame-sized virtual grid, empty
+// blocks leaving at once, cost c3 0.207 ms vs 0.183 for a grid sized exactly to the lists read
+// back on the host: the ~10^5 empty blocks' dispatch is not free; the queues need neither.)
 #ifndef RT_RENDER_WAVES
 #define RT_RENDER_WAVES 7
 #endif
@@ -1658,42 +1650,95 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, flo
 #ifndef RT_BOUNCE_WAVES
 #define RT_BOUNCE_WAVES 3
 #endif
-// Heavy-first dispatch: the kernel takes the heavy lists and records its tiles' costs.
+// Heavy-first dispatch: the queues hand out the heavy lists first; the waves record their
+// items' costs.
 template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0>
 __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
+    constexpr int WPT = BLOCK / 64;  // waves per tile
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
     __shared__ int kpix[SAMPLES ? BLOCK : 1];
     // D1: shade_d1's state across shadow rays; else (WAVE kernels) traverse_lane_lds's stacks
     __shared__ float park[D1 ? PARK_SLOTS * BLOCK
                              : (MODE == RT_KERNEL_LANE || (MODE & MODE_DEEP) != 0 ? 1 : LANE_LDS_CAP * BLOCK)];
-#ifdef RT_WAVE_TIMES
-    const unsigned long long wt0 = wall_clock64();
-#endif
-    // the wave's start time goes through LDS (an SGPR pair live across the whole tile spilled)
-    __shared__ uint32_t t_start[BLOCK / 64], t_tile[BLOCK / 64];
+    // the wave's item start time goes through LDS (an SGPR pair live across the whole tile spilled)
+    __shared__ uint32_t t_start[WPT], t_item[WPT];
     __shared__ int lds_zero;  // 0, written by every lane (samples_tile's fresh lane id)
+    __shared__ uint32_t block_item;  // spp > 64: the block's item
     if constexpr (SAMPLES) lds_zero = 0;
     // the wave's index in the block as a uniform value (threadIdx.x itself, kept live to the
     // tile-cost write at the end, was spilled to scratch)
     const uint32_t wv = uni((uint32_t)threadIdx.x) >> 6;
-    if (P.tile_cost && lane_id() == 0) t_start[wv] = (uint32_t)wall_clock64();
-    const int tile = block_tile(P, (int)blockIdx.x);
-    if (tile < 0) return;
-    if (P.tile_cost && lane_id() == 0) t_tile[wv] = (uint32_t)tile;
-    if constexpr (SAMPLES) samples_tile<MODE, D1, LS>(P, tile, col, kpix, park, &lds_zero);
-    else pixels_tile<MODE, D1>(P, tile, park);
-    if (P.tile_cost && lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
-        asm volatile("" ::: "memory");
-        const uint32_t d = (uint32_t)wall_clock64() - t_start[wv];
-        P.tile_cost[4 * (size_t)t_tile[wv] + wv] = (uint16_t)(d < 0xffffu ? d : 0xffffu);
-    }
+    // The first item of each wave (block) is its place in the grid, the rest come from the
+    // queue after those: 900 dequeues per head at once when the grid starts took ~10 us to serve.
+    for (bool first = true;; first = false) {
+        // Everything the item needs is derived inside the loop from a laundered block index and
+        // parameter pointer (the kernel's argument segment): hoisted out of the loop, the
+        // parameters' loads and the values made from them stay live across every item and spill.
+        typedef const __attribute__((address_space(4))) RenderParams* KernargP;
+        KernargP pp = (KernargP)__builtin_amdgcn_kernarg_segment_ptr();
+        uint32_t bx = blockIdx.x;
+        asm volatile("" : "+s"(pp), "+s"(bx));
+        const RenderParams& R = *(const RenderParams*)pp;
+        const int g = (int)(bx & 7);
+        const int q = R.nqueues == 1 ? 0 : g;
+        uint32_t* head = R.live_count + (HEAD_SLOT0 + g) * COUNTER_STRIDE;
+        const bool blockwise = SAMPLES && R.spp > 64;
+        const uint32_t lane = fresh_lane_id();
+        const int tid = (int)((wv << 6) | lane);
+        const uint32_t per_queue = (gridDim.x >> 3) * (blockwise ? 1u : (uint32_t)WPT);  // first items
+        uint32_t j;
+        if (first) {
+            j = (bx >> 3) * (blockwise ? 1u : (uint32_t)WPT) + (blockwise ? 0u : wv);
+        } else if (blockwise) {
+            // one barrier per item: the previous item's LDS reads finished at samples_tile's
+            // own barrier, before thread 0 overwrites block_item
+            if (tid == 0) block_item = dequeue(head, lane);
+            __syncthreads();
+            j = per_queue + uni(block_item);
+        } else {
+            j = per_queue + dequeue(head, lane);
+        }
+        int heavy;
+        const int n = work_length(R, q, heavy);
+        const int e = (R.nqueues == 1 ? g : 0) + (R.nqueues == 1 ? 8 : 1) * (int)(blockwise ? j : j / WPT);
+        if (e >= n) break;
+        const uint32_t qw = blockwise ? wv : j % WPT;
+        int cls;
+        const int tile = work_tile(R, q, e, heavy, cls);
+        // Issue priority by cost class: every SIMD keeps all its wave slots busy until the queues
+        // drain, so the heaviest items (the kernel's critical path, started first) would share
+        // their SIMD with six other waves throughout; ahead of the rest they finish sooner
+        // (c3 0.182 vs 0.210 ms without priorities, 0.199 with class 0 alone raised).
+        if (cls == 0) __builtin_amdgcn_s_setprio(3);
+        else if (cls == 1) __builtin_amdgcn_s_setprio(2);
+        else if (cls == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
 #ifdef RT_WAVE_TIMES
-    if (g_wave_times && lane_id() == 0) {
-        const size_t k = ((size_t)tile * (BLOCK / 64) + threadIdx.x / 64) * 2;
-        g_wave_times[k] = wt0;
-        g_wave_times[k + 1] = wall_clock64();
-    }
+        const unsigned long long wt0 = wall_clock64();
 #endif
+        if (R.tile_cost && lane == 0) {
+            t_start[wv] = (uint32_t)wall_clock64();
+            t_item[wv] = (uint32_t)tile * WPT + qw;
+        }
+        if constexpr (SAMPLES) samples_tile<MODE, D1, LS>(R, tile, qw, tid, col, kpix, park, &lds_zero);
+        else pixels_tile<MODE, D1>(R, tile, qw, tid, park);
+        if (R.tile_cost && fresh_lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
+            asm volatile("" ::: "memory");
+            const uint32_t d = (uint32_t)wall_clock64() - t_start[wv];
+            R.tile_cost[t_item[wv]] = (uint16_t)(d < 0xffffu ? d : 0xffffu);
+        }
+#ifdef RT_WAVE_TIMES
+        if (g_wave_times && fresh_lane_id() == 0) {
+            const size_t k = ((size_t)tile * WPT + qw) * 2;
+            g_wave_times[k] = wt0;
+            g_wave_times[k + 1] = wall_clock64();
+            if (g_wave_meta) {
+                const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID
+                g_wave_meta[(size_t)tile * WPT + qw] = bx << 8 | xcc << 4 | (first ? 4u : 0u) | wv;
+            }
+        }
+#endif
+    }
 }
 
 // ---- HW1 brute force (HW1/src/render.cpp:72-116) ----------------------------------------
@@ -2583,40 +2628,46 @@ int prepare_jitter(rt_scene* s, const rt_render_opts* o) {
     return RT_OK;
 }
 
-// 8 * NCLASS * heavy_cap heavy-phase blocks, then tiles_virtual blocks (rounded up to a multiple of 8),
-// one per planned virtual block.
-// (A grid sized to the longest list, read back on the host, measured no faster on c3 than the
-// full virtual grid: the empty blocks leave at once.)
-// The render kernel's start / end events (rt_kernel_times) go into its dispatch
+// The render kernel's persistent grid: the blocks of it one dispatch keeps resident on every CU
+// (the occupancy the kernel was compiled for, LDS permitting), a multiple of 8 (one share per
+// XCD queue), at most one block per tile.  Blocks beyond residency would only find the queues
+// empty.  The render kernel's start / end events (rt_kernel_times) go into its dispatch
 // (hipExtLaunchKernel): no separate event packets on the stream between the frames' kernels.
 struct Launch {
     hipStream_t st;
     hipEvent_t start, stop;
+    int cus;
 };
-template <typename K>
-void launch_render(K kernel, const dim3& grid, const RenderParams& P, const Launch& L) {
-    hipExtLaunchKernelGGL(kernel, grid, dim3(BLOCK), 0, L.st, L.start, L.stop, 0, P);
+template <auto KERNEL>
+void launch_render(const RenderParams& P, const Launch& L) {
+    static const int per_cu = [] {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, KERNEL, BLOCK, 0) != hipSuccess || n < 1) n = 1;
+        return n;
+    }();
+    const int tiles8 = (P.tiles_total + 7) / 8 * 8;
+    const dim3 grid((unsigned)std::max(8, std::min(tiles8, L.cus * per_cu / 8 * 8)));
+    hipExtLaunchKernelGGL(KERNEL, grid, dim3(BLOCK), 0, L.st, L.start, L.stop, 0, P);
 }
 
 template <int MODE, bool SAMPLES>
 void launch_mode(const RenderParams& P, const Launch& L) {
-    const dim3 grid((P.tiles_virtual + 7) / 8 * 8 + 8 * NCLASS * P.heavy_cap);
     if (P.max_depth == 1) {
         if constexpr (SAMPLES) {
             if (P.half_waves) {
-                launch_render(render_tiles_kernel<MODE, SAMPLES, true, RT_RENDER_WAVES, 1>, grid, P, L);
+                launch_render<render_tiles_kernel<MODE, SAMPLES, true, RT_RENDER_WAVES, 1>>(P, L);
                 return;
             }
         }
-        launch_render(render_tiles_kernel<MODE, SAMPLES, true>, grid, P, L);
+        launch_render<render_tiles_kernel<MODE, SAMPLES, true>>(P, L);
     } else {
         if constexpr (SAMPLES) {
             if (P.half_waves) {
-                launch_render(render_tiles_kernel<MODE, SAMPLES, false, RT_BOUNCE_WAVES, 1>, grid, P, L);
+                launch_render<render_tiles_kernel<MODE, SAMPLES, false, RT_BOUNCE_WAVES, 1>>(P, L);
                 return;
             }
         }
-        launch_render(render_tiles_kernel<MODE, SAMPLES, false, RT_BOUNCE_WAVES>, grid, P, L);
+        launch_render<render_tiles_kernel<MODE, SAMPLES, false, RT_BOUNCE_WAVES>>(P, L);
     }
 }
 
@@ -2756,7 +2807,9 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // the doubled wave count costs more: N = 4 0.106 -> 0.116, N = 1 0.211 -> 0.373;
     // scripts/half_waves_ab.py).  RT_HALF_WAVES=0/1 overrides.  (Quarter waves,
     // 16 samples, measured slower at N = 8 and were dropped.)
-    int half = o->band_count >= 8 ? 1 : 0;
+    // The multi-bounce kernels take half waves at any split: a wave's bounce paths end with its
+    // longest lane's, and the longest waves bound the kernel (c3b 1.96 vs 2.37 ms per frame).
+    int half = o->band_count >= 8 || o->max_depth > 1 ? 1 : 0;
     if (const char* e = std::getenv("RT_HALF_WAVES")) half = std::clamp(std::atoi(e), 0, 1);
     if (!samples || o->spp > (64 >> half)) half = 0;
     P.half_waves = half;
@@ -2778,14 +2831,13 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.miss_pixel = miss_pixel_value(o);
     P.nqueues = P.tile_order == RT_TILES_LINEAR ? 1 : 8;
     // a list holds at most tiles_x * ceil(tiles_y / 8) tiles (RT_TILES_ROWS) or ceil(tiles / 8)
-    // (RT_TILES_XCD_CHUNK): tiles_virtual / 8 bounds both
+    // (RT_TILES_XCD_CHUNK): tiles_x * ceil(tiles_y / 8) bounds both
     P.queue_cap = P.tile_order == RT_TILES_LINEAR ? P.tiles_total : P.tiles_x * ((tiles_y + 7) / 8);
-    P.tiles_virtual = P.nqueues == 1 ? P.tiles_total : 8 * P.tiles_x * ((tiles_y + 7) / 8);
     // Heavy-first dispatch needs the cut pass (it builds the heavy lists) and the 8 lists.
     // RT_HEAVY_FRAC (speed experiments): a tile is in heavy class c when one of its waves took
     // at least 2^(NCLASS-1-c) times this fraction of the latest finished frame's render kernel
     // (0: off).
-    double heavy_frac = 0.08;
+    double heavy_frac = 0.12;  // c3: 0.04 0.197, 0.06 0.188, 0.08 0.179, 0.12 0.177, 0.16 0.177 ms
     if (const char* e = std::getenv("RT_HEAVY_FRAC")) heavy_frac = std::atof(e);
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
     const bool costs = P.cull && P.sc.ncut > 0 && P.nqueues == 8 && heavy_frac > 0.0;
@@ -2910,7 +2962,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
-        const Launch L{st, s->evm[slot], s->ev1[slot]};
+        const Launch L{st, s->evm[slot], s->ev1[slot], s->cus};
         if (s->deep) launch<MODE_DEEP>(P, samples, L);
         else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, L);
         else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, L);
@@ -3012,6 +3064,10 @@ extern "C" int rt_debug_stats(unsigned long long* out, int reset) {
 #endif
 
 #ifdef RT_WAVE_TIMES
+extern "C" int rt_debug_wave_meta_set(void* dev_ptr) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wave_meta), &dev_ptr, sizeof(dev_ptr)));
+    return RT_OK;
+}
 extern "C" int rt_debug_wave_phase_set(void* dev_ptr) {
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wave_phase), &dev_ptr, sizeof(dev_ptr)));
     return RT_OK;

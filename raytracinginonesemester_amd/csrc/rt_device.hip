@@ -1308,8 +1308,9 @@ __device__ __forceinline__ void write_culled_tile(const RenderParams& P, int til
         for (int i = first; i < tw * th * 3; i += lanes) {
             const int px = i / 3, c = i - 3 * px;
             const int r = ra + px / tw, x = xa + px % tw;
-            if (P.rgb) P.rgb[((size_t)r * P.W + x) * 3 + c] = mp[c];
-            if (P.p6) P.p6[((size_t)r * P.W + x) * 3 + c] = P.miss_p6[c];
+            // component c by selects (an array indexed by c would live in scratch)
+            if (P.rgb) P.rgb[((size_t)r * P.W + x) * 3 + c] = c == 0 ? mp[0] : c == 1 ? mp[1] : mp[2];
+            if (P.p6) P.p6[((size_t)r * P.W + x) * 3 + c] = c == 0 ? P.miss_p6[0] : c == 1 ? P.miss_p6[1] : P.miss_p6[2];
         }
     }
     if (P.hit_idx) {
@@ -1344,6 +1345,7 @@ __device__ __forceinline__ void append_live(const RenderParams& P, bool live, in
 
 // Pass 1, one lane per tile: the root test; the survivors go to the live lists.
 __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
+    __builtin_amdgcn_s_setprio(3);  // ahead of the previous frame's render waves (see Launch)
     const int tile = (int)(blockIdx.x * BLOCK + threadIdx.x);
     // Counter sets rotate over three frames (no reset launch): this frame's set was zeroed by
     // the previous frame's pass; zero the next frame's (its last user, frame k-2, has finished:
@@ -1374,6 +1376,7 @@ __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
 #endif
 constexpr int CUT_GROUP = RT_CUT_GROUP;
 __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
+    __builtin_amdgcn_s_setprio(3);
     const uint32_t lane = lane_id();
     const int waves = (int)(gridDim.x * (BLOCK / 64));
     int n = 0, max_len = 0;
@@ -1401,6 +1404,9 @@ __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
         const int m = min(CUT_GROUP, len - CUT_GROUP * g);
         const size_t slot0 = (size_t)q * P.queue_cap + (size_t)(CUT_GROUP * g);
         const int my_tile = (int)lane < m ? P.live_tiles[slot0 + lane] : -1;
+        // the tile's last render cost, loaded before the tests so the load overlaps them
+        uint2 cost = make_uint2(0u, 0u);
+        if (P.heavy_cap > 0 && (int)lane < m) cost = *reinterpret_cast<const uint2*>(P.tile_cost + 4 * (size_t)my_tile);
         uint64_t culled = 0;
         for (int j = 0; test && j < m; ++j) {
             const int tile = (int)rdlane((uint32_t)my_tile, (uint32_t)j);
@@ -1420,40 +1426,48 @@ __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
                 culled |= 1ull << j;
             }
         }
-        // Heavy-first: surviving tiles whose last render took >= heavy_ticks[c] go to list q's
-        // class-c heavy list (a full heavy list leaves the tile to the survivor list).
-        bool heavy = false;
-        if (P.heavy_cap > 0) {
-            int cls = NCLASS;
-            if ((int)lane < m && !((culled >> lane) & 1ull)) {
-                const uint2 c = *reinterpret_cast<const uint2*>(P.tile_cost + 4 * (size_t)my_tile);
-                const uint32_t mx = max(max(c.x & 0xffffu, c.x >> 16), max(c.y & 0xffffu, c.y >> 16));
+        // Heavy-first: a surviving tile whose last render took >= heavy_ticks[c] goes to list q's
+        // class-c heavy list, the others to its survivor list (the render kernel's normal part).
+        // The appends take one vector atomic, lane k adding class k's count (lane NCLASS the
+        // survivors'), so a group pays one round trip for them.
+        int cls = -1;  // -1: no tile, or culled
+        if ((int)lane < m && !((culled >> lane) & 1ull)) {
+            cls = NCLASS;
+            if (P.heavy_cap > 0) {
+                const uint32_t mx = max(max(cost.x & 0xffffu, cost.x >> 16), max(cost.y & 0xffffu, cost.y >> 16));
                 for (int k = NCLASS - 1; k >= 0; --k)
                     if (mx >= P.heavy_ticks[k]) cls = k;
             }
-            for (int k = 0; k < NCLASS; ++k) {
-                const uint64_t hm = ballot(cls == k);
-                if (hm == 0) continue;
-                const uint32_t leader = (uint32_t)__builtin_ctzll(hm);
-                uint32_t base = 0;
-                if (lane == leader)
-                    base = atomicAdd(&P.live_count[heavy_counter(k, q)], (uint32_t)__popcll(hm));
-                const uint32_t idx = rdlane(base, leader) + (uint32_t)__popcll(hm & ((1ull << lane) - 1));
-                if (cls == k && idx < (uint32_t)P.heavy_cap) {
-                    P.heavy_tiles[((size_t)k * 8 + q) * P.heavy_cap + idx] = my_tile;
-                    heavy = true;
+        }
+        uint64_t cm[NCLASS + 1];
+        uint32_t add = 0;
+#pragma unroll
+        for (int k = 0; k <= NCLASS; ++k) {
+            cm[k] = ballot(cls == k);
+            if ((int)lane == k) add = (uint32_t)__popcll(cm[k]);
+        }
+        const uint64_t below = (1ull << lane) - 1;
+        if (ballot(add != 0) != 0) {
+            uint32_t base = 0;
+            if ((int)lane <= NCLASS && add != 0)
+                base = atomicAdd(&P.live_count[(int)lane < NCLASS ? heavy_counter((int)lane, q) : (CUT_SLOT0 + q) * COUNTER_STRIDE], add);
+            bool spill = false;  // a heavy tile past its list's capacity goes to the survivor list
+#pragma unroll
+            for (int k = 0; k <= NCLASS; ++k) {
+                const uint32_t idx = rdlane(base, (uint32_t)k) + (uint32_t)__popcll(cm[k] & below);
+                if (cls == k) {
+                    if (k == NCLASS) P.cut_tiles[(size_t)q * P.queue_cap + idx] = my_tile;
+                    else if (idx < (uint32_t)P.heavy_cap) P.heavy_tiles[((size_t)k * 8 + q) * P.heavy_cap + idx] = my_tile;
+                    else spill = true;
                 }
             }
-        }
-        // the rest go to list q's survivor list (the render kernel's normal phase)
-        const bool keep = (int)lane < m && !((culled >> lane) & 1ull) && !heavy;
-        const uint64_t km = ballot(keep);
-        if (km != 0) {
-            const uint32_t leader = (uint32_t)__builtin_ctzll(km);
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&P.live_count[(CUT_SLOT0 + q) * COUNTER_STRIDE], (uint32_t)__popcll(km));
-            if (keep)
-                P.cut_tiles[(size_t)q * P.queue_cap + rdlane(base, leader) + (uint32_t)__popcll(km & ((1ull << lane) - 1))] = my_tile;
+            const uint64_t sm = ballot(spill);
+            if (sm != 0) {  // rare: a full heavy list
+                const uint32_t leader = (uint32_t)__builtin_ctzll(sm);
+                uint32_t b2 = 0;
+                if (lane == leader) b2 = atomicAdd(&P.live_count[(CUT_SLOT0 + q) * COUNTER_STRIDE], (uint32_t)__popcll(sm));
+                if (spill) P.cut_tiles[(size_t)q * P.queue_cap + rdlane(b2, leader) + (uint32_t)__popcll(sm & below)] = my_tile;
+            }
         }
     }
 }

@@ -33,6 +33,7 @@ import argparse
 import gzip
 import hashlib
 import json
+import math
 import os
 import platform
 import subprocess
@@ -63,6 +64,9 @@ def parse():
                          "launcher this process drives GPUs 0..N-1 itself")
     ap.add_argument("--steps", type=int, default=100)  # ~35 ms of frames: a steadier average
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--preroll-ms", type=float, default=100.0,
+                    help="untimed frames for about this much GPU time before the W warmup frames (clocks; "
+                         "0: none); the frames run are reported as warmup_frames_run")
     ap.add_argument("--config", default="c3", choices=sorted(configs.G_CONFIGS))
     ap.add_argument("--kernel", default="auto", choices=["auto", "wave", "lane"])
     ap.add_argument("--deliver", default="p6", choices=["p6", "f32"])
@@ -199,7 +203,29 @@ def run_frames(r, cam, opts, n, depth):
     return last
 
 
-def timed_native(r, cam, opts, steps, warmup, depth, ctx):
+PREROLL = {"frames": 0}
+
+
+def timed_native(r, cam, opts, steps, warmup, depth, ctx, preroll_ms=0.0):
+    """W warmup frames, then K timed frames.  preroll_ms > 0: before the warmup, frames for about
+    that much GPU time.  The GPU's clocks rise only under sustained load: a c3 frame's render
+    kernel takes 0.22 ms in the first frames after an idle period and 0.18 ms after ~100 of them
+    (`scripts/profile_frames.py --series`, profiles/r03/exp/clock_ramp_series.log), so a
+    few-millisecond timed region that starts cold measures the ramp.  The count is agreed over
+    the ranks (every rank renders every frame) and reported as warmup_frames_run."""
+    n_pre, chunk = 0, 2
+    t0 = time.perf_counter()
+    while preroll_ms > 0 and n_pre < 5000:  # chunks of ~10 ms of frames; the ranks agree on each step
+        tc = time.perf_counter()
+        run_frames(r, cam, opts, chunk, depth)
+        n_pre += chunk
+        per = (time.perf_counter() - tc) / chunk
+        done, nxt = ctx.max([1.0 if time.perf_counter() - t0 >= preroll_ms * 1e-3 else 0.0,
+                             float(max(1, min(64, int(0.01 / max(per, 1e-6)))))])
+        if done > 0:
+            break
+        chunk = int(nxt)
+    PREROLL["frames"] = n_pre + warmup
     run_frames(r, cam, opts, warmup, depth)
     ctx.sync()
     t0 = time.perf_counter()
@@ -301,7 +327,8 @@ def native(a, hs, cam, cfg, ctx):
         gather = GATHERS[a.gather]
     deliver = rt.RT_DELIVER_F32 if a.deliver == "f32" else rt.RT_DELIVER_P6
     r = make_renderer(hs, ctx, a, deliver, gather, a.depth)
-    elapsed, last = timed_native(r, cam, opts, a.steps, a.warmup, a.depth, ctx)
+    elapsed, last = timed_native(r, cam, opts, a.steps, a.warmup, a.depth, ctx, a.preroll_ms)
+    warm_run = PREROLL["frames"]
     kts, fts, pts = [], [], []
     for i in range(r.local_ranks):
         sc = r.scene(i)
@@ -311,7 +338,7 @@ def native(a, hs, cam, cfg, ctx):
     sc = r.scene(0)
     res = {"elapsed": elapsed, "kernel_ms": max(kts), "frame_ms": max(fts), "prepass_ms": max(pts),
            "kernel_ms_local": kts, "live_tiles": list(sc.live_tiles()), "heavy_tiles": sc.heavy_tiles(),
-           "gather_path": GATHER_NAMES[gather]}
+           "gather_path": GATHER_NAMES[gather], "warmup_frames_run": warm_run}
     if ctx.rank == 0:
         g, d, f = (r.times(k, a.steps) for k in (rt.RT_TIME_GATHER, rt.RT_TIME_DELIVER, rt.RT_TIME_FRAME))
         res.update(gather_ms=float(g.mean()), deliver_ms=float(d.mean()), frame_latency_ms=float(f.mean()))
@@ -322,7 +349,7 @@ def native(a, hs, cam, cfg, ctx):
         return res
     # secondary: render only (strips stay in HBM), the rate the round-1 bench reported
     rn = make_renderer(hs, ctx, a, rt.RT_DELIVER_NONE, gather, a.depth)
-    res["render_only_s"], _ = timed_native(rn, cam, opts, a.steps, a.warmup, a.depth, ctx)
+    res["render_only_s"], _ = timed_native(rn, cam, opts, a.steps, a.warmup, a.depth, ctx, a.preroll_ms)
     rn.close()
     # secondary: the other payload (f32 = the reference's Vec3 framebuffer), also the float parity
     other = rt.RT_DELIVER_P6 if deliver == rt.RT_DELIVER_F32 else rt.RT_DELIVER_F32
@@ -583,6 +610,7 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
+        "warmup_frames_run": res.get("warmup_frames_run", a.warmup),
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "strong",

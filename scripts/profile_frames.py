@@ -30,6 +30,8 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--frames", type=int, default=50)
 ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--mode", default="serial", choices=["serial", "none", "p6"])
+ap.add_argument("--series", action="store_true", help="also print every timed frame's render-kernel ms")
+ap.add_argument("--busy-ms", type=float, default=0.0, help="keep the GPU busy (matmuls) this long first")
 a = ap.parse_args()
 
 cfg = configs.G_CONFIGS[a.config]
@@ -39,6 +41,13 @@ cam = hs.camera(cfg["width"], cfg["height"])
 kw = dict(spp=cfg["spp"], max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
           diffuse_bounce=hs.settings["diffuse_bounce"])
 n = a.warmup + a.frames
+if a.busy_ms > 0:  # clocks: the GPU busy before the first frame
+    x = torch.randn(4096, 4096, device="cuda")
+    t_end = time.perf_counter() + a.busy_ms * 1e-3
+    while time.perf_counter() < t_end:
+        for _ in range(8):
+            x = (x @ x).clamp_(-1, 1)
+        torch.cuda.synchronize()
 if a.mode == "serial":
     ds = rt.DeviceScene.from_host(hs)
     o, _j = ds.make_opts(**kw)
@@ -74,6 +83,8 @@ else:
     sc = r.scene(0)
 kt = sc.kernel_times(a.frames)
 pt = sc.prepass_times(a.frames)
+if a.series:
+    print(json.dumps({"kernel_ms_series": [round(float(x), 4) for x in kt]}), flush=True)
 print(json.dumps({"config": a.config, "mode": a.mode, "frames": a.frames,
                   "render_kernel_ms_mean": round(float(kt.mean()), 4),
                   "render_kernel_ms_median": round(float(np.median(kt)), 4),

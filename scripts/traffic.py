@@ -21,6 +21,9 @@ ap.add_argument("prof")
 ap.add_argument("config")
 ap.add_argument("--out", default=str(REPO / "profiles" / "r01"))
 ap.add_argument("--kernel", default="render_tiles_kernel")
+ap.add_argument("--skip", type=int, default=0,
+                help="drop each kernel's first N dispatches (profile_frames.py's warmup frames: the first "
+                     "frames run before the heavy-first lists exist and before the clocks rise)")
 a = ap.parse_args()
 
 
@@ -34,8 +37,16 @@ def short(name):
 
 pmc = collections.defaultdict(lambda: collections.defaultdict(list))
 for p in sorted(glob.glob(os.path.join(a.prof, "*", "*counter_collection.csv"))):
+    per = collections.defaultdict(lambda: collections.defaultdict(float))  # (kernel, dispatch) -> counter sums
     for r in csv.DictReader(open(p)):
-        pmc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        per[(short(r["Kernel_Name"]), int(r["Dispatch_Id"]))][r["Counter_Name"]] += float(r["Counter_Value"])
+    seen = collections.Counter()
+    for (kn, _d), cs in sorted(per.items(), key=lambda kv: kv[0][1]):
+        seen[kn] += 1
+        if seen[kn] <= a.skip:
+            continue
+        for c, v in cs.items():
+            pmc[kn][c].append(v)
 summary = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in pmc.items()}
 os.makedirs(a.out, exist_ok=True)
 with open(os.path.join(a.out, f"{a.config}_pmc_per_launch.csv"), "w") as f:
@@ -45,7 +56,23 @@ with open(os.path.join(a.out, f"{a.config}_pmc_per_launch.csv"), "w") as f:
             f.write(f"{k},{c},{sum(v) / len(v):.6g},{len(v)}\n")
 for st in glob.glob(os.path.join(a.prof, "trace", "*kernel_stats.csv")):
     os.makedirs(a.out, exist_ok=True)
-    Path(a.out, f"{a.config}_kernel_stats.csv").write_text(Path(st).read_text())
+    Path(a.out, f"{a.config}_kernel_stats_all.csv").write_text(Path(st).read_text())
+for tr in glob.glob(os.path.join(a.prof, "trace", "*kernel_trace.csv")):
+    # the same statistics over each kernel's dispatches after the first --skip
+    by = collections.defaultdict(list)
+    for r in csv.DictReader(open(tr)):
+        by[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    rows = []
+    for name, v in by.items():
+        d = [x[1] for x in sorted(v)[a.skip:]] or [x[1] for x in v]
+        m = sum(d) / len(d)
+        sd = (sum((x - m) ** 2 for x in d) / len(d)) ** 0.5
+        rows.append((name, len(d), sum(d), m, min(d), max(d), sd))
+    tot = sum(r[2] for r in rows) or 1
+    with open(os.path.join(a.out, f"{a.config}_kernel_stats.csv"), "w") as f:
+        f.write('"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n')
+        for r in sorted(rows, key=lambda r: -r[2]):
+            f.write(f'"{r[0]}",{r[1]},{r[2]},{r[3]:.6f},{100 * r[2] / tot:.4f},{r[4]},{r[5]},{r[6]:.6f}\n')
 k = summary.get(a.kernel, {})
 
 SIMDS, CUS = 1024, 256  # MI355X: 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)

@@ -326,7 +326,24 @@ def native(a, hs, cam, cfg, ctx):
     else:
         gather = GATHERS[a.gather]
     deliver = rt.RT_DELIVER_F32 if a.deliver == "f32" else rt.RT_DELIVER_P6
-    r = make_renderer(hs, ctx, a, deliver, gather, a.depth)
+    gather_note = None
+    if gather == rt.RT_GATHER_HOST_SHARED and a.gather == "auto":
+        # the shared host frame needs room in /dev/shm on the node; if any rank cannot make or
+        # attach it, every rank takes the RCCL strip gather instead (named in config.comm)
+        r, err = None, ""
+        try:
+            r = make_renderer(hs, ctx, a, deliver, gather, a.depth)
+        except rt.RTError as e:
+            err = str(e)
+        if ctx.max([1.0 if err else 0.0])[0] > 0:
+            if r is not None:
+                r.close()
+            gather_note = f"shared host frame failed ({err or 'on another rank'}); RCCL strip gather used"
+            print(f"bench: {gather_note}", file=sys.stderr, flush=True)
+            gather = rt.RT_GATHER_RCCL
+            r = make_renderer(hs, ctx, a, deliver, gather, a.depth)
+    else:
+        r = make_renderer(hs, ctx, a, deliver, gather, a.depth)
     elapsed, last = timed_native(r, cam, opts, a.steps, a.warmup, a.depth, ctx, a.preroll_ms)
     warm_run = PREROLL["frames"]
     kts, fts, pts = [], [], []
@@ -338,7 +355,7 @@ def native(a, hs, cam, cfg, ctx):
     sc = r.scene(0)
     res = {"elapsed": elapsed, "kernel_ms": max(kts), "frame_ms": max(fts), "prepass_ms": max(pts),
            "kernel_ms_local": kts, "live_tiles": list(sc.live_tiles()), "heavy_tiles": sc.heavy_tiles(),
-           "gather_path": GATHER_NAMES[gather], "warmup_frames_run": warm_run}
+           "gather_path": GATHER_NAMES[gather], "warmup_frames_run": warm_run, "gather_note": gather_note}
     if ctx.rank == 0:
         g, d, f = (r.times(k, a.steps) for k in (rt.RT_TIME_GATHER, rt.RT_TIME_DELIVER, rt.RT_TIME_FRAME))
         res.update(gather_ms=float(g.mean()), deliver_ms=float(d.mean()), frame_latency_ms=float(f.mean()))
@@ -635,6 +652,8 @@ def main():
         line["config"]["rehearsal"] = "--share-gpu: ranks share GPUs (not a multi-GPU measurement)"
     if fallback:
         line["config"]["fallback"] = fallback
+    if res.get("gather_note"):
+        line["config"]["gather_note"] = res["gather_note"]
     per_gpu_samples = samples / world
     bps = configs.BYTES_PER_SAMPLE.get(a.config)
     tr = load_traffic(Path(a.traffic_file), a.config) if world == 1 else None

@@ -473,6 +473,14 @@ int open_shared(rt_renderer* r) {
             (void)shm_unlink(sf->name.c_str());
             return set_error(RT_ERR_NOMEM, "ftruncate " + sf->name + ": " + std::strerror(e));
         }
+        // reserve the pages now: a tmpfs too small for the frames fails here with ENOSPC instead
+        // of raising SIGBUS in whichever process first touches a missing page
+        if (const int e = posix_fallocate(fd, 0, off_t(sf->bytes)); e != 0) {
+            ::close(fd);
+            (void)shm_unlink(sf->name.c_str());
+            return set_error(RT_ERR_NOMEM, "posix_fallocate " + sf->name + " (" + std::to_string(sf->bytes) +
+                                               " B in /dev/shm): " + std::strerror(e));
+        }
         void* p = mmap(nullptr, sf->bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
         ::close(fd);
         if (p == MAP_FAILED) {

@@ -431,7 +431,10 @@ __host__ __device__ __forceinline__ float exp2_inline(double xd, uint32_t sign_b
     const double r = xd - kd;
     uint64_t t = exp2_tab(int(ki % 32u));
     const uint64_t ski = ki + sign_bias;
-    t += ski << (52 - 5);
+    // t += ski << (52 - 5), on the high word: the shifted value's low word is 0, so there is no
+    // carry.  (A 64-bit value with a zero low word made the compiler keep a zero VGPR live
+    // across the render kernel's item loop, spilled.)
+    t = (uint64_t)((uint32_t)(t >> 32) + ((uint32_t)ski << 15)) << 32 | (uint32_t)t;
     const double s = asd(t);
     const double z = fma(C0, r, C1);
     const double r2 = r * r;
@@ -488,10 +491,11 @@ __host__ __device__ inline float ref_powf(float x, float y) {
     }
     const double logx = log2_inline(ix);
     const double ylogx = double(y) * logx;
-    if ((asu64(ylogx) >> 47 & 0xffff) >= asu64(126.0) >> 47) {
-        if (ylogx > 0x1.fffffffd1d571p+6) return sign_bias ? -INFINITY : INFINITY;
-        if (ylogx <= -150.0) return sign_bias ? -0.0f : 0.0f;
-    }
+    // The library gates these two tests with (asuint64(ylogx) >> 47 & 0xffff) >= asuint64(126.0)
+    // >> 47, i.e. |ylogx| >= 124 or NaN, a superset of both: they decide alone, so the gate is
+    // dropped (its 64-bit mask kept a zero VGPR live across the render kernel's item loop).
+    if (ylogx > 0x1.fffffffd1d571p+6) return sign_bias ? -INFINITY : INFINITY;
+    if (ylogx <= -150.0) return sign_bias ? -0.0f : 0.0f;
     return exp2_inline(ylogx, sign_bias);
 }
 

@@ -27,6 +27,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3")
 ap.add_argument("--frames", type=int, default=3)
 ap.add_argument("--out", default=str(REPO / "gpurun_out" / "queue_times.json"))
+ap.add_argument("--bands", type=int, default=1, help="render band shard --band of an N-way split (8-row bands)")
+ap.add_argument("--band", type=int, default=0)
 a = ap.parse_args()
 cfg = configs.G_CONFIGS[a.config]
 sp = configs.scene_path(cfg["scene"])
@@ -37,8 +39,13 @@ lib = _lib.lib()
 lib.rt_debug_wave_times_set.argtypes = [C.c_void_p, C.c_void_p]
 lib.rt_debug_wave_meta_set.argtypes = [C.c_void_p]
 ds = rt.DeviceScene.from_host(hs)
-opts, _j = ds.make_opts(spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"])
-tw = (128 if os.environ.get("RT_HALF_WAVES") == "1" else 256) // spp if spp <= 256 else 1  # samples per tile / spp
+band_kw = dict(band_rows=8, band_index=a.band, band_count=a.bands) if a.bands > 1 else {}
+opts, _j = ds.make_opts(spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"], **band_kw)
+half = os.environ.get("RT_HALF_WAVES") == "1" or (a.bands >= 8 and "RT_HALF_WAVES" not in os.environ) or \
+    (cfg["max_depth"] > 1 and "RT_HALF_WAVES" not in os.environ)
+if a.bands > 1:
+    H = _lib.lib().rt_shard_rows(H, 8, a.band, a.bands)
+tw = (128 if half and spp <= 32 else 256) // spp if spp <= 256 else 1  # pixels per tile
 side = 1
 while side * side < tw:
     side *= 2

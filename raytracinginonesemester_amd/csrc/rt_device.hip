@@ -58,6 +58,7 @@ constexpr int BLOCK = 256;
 // Kernel instantiation flag on top of RT_KERNEL_WAVE: traverse the 4-ary records (SceneView::wide).
 // A compile-time choice, so each kernel holds one traversal loop per ray kind.
 constexpr int MODE_WIDE = 16;
+constexpr int MODE_PK = 32;  // the wave traversal's box tests in packed FMAs (box_ends_pk): depth-1 kernels
 // Trees whose DFS needs more than STACK_CAP entries: SearchBVH literally, per lane, with the
 // reference's 512-entry stack, its overflow rule and brute-force completion (traverse_deep).
 constexpr int MODE_DEEP = 64;
@@ -279,8 +280,11 @@ __device__ __forceinline__ BoxP leaf_box(const NodeRec& r) {
 // box_hit for the lanes in `act` (a wave mask; all lanes call it), as the mask of lanes that
 // pass: the float pre-classification for everyone, the exact double test only behind a
 // wave-uniform branch taken when some lane is ambiguous.
+template <bool PK = false>
 __device__ __forceinline__ uint64_t box_hit_mask(const RayPre& r, const BoxP& b, float tmax, uint64_t act) {
-    const AxisEnds e = box_ends(r, b);
+    AxisEnds e;
+    if constexpr (PK) e = box_ends_pk(r, b);
+    else e = box_ends(r, b);
     const BoxEnds c = box_lc_hc(e, kRayTMin, tmax);
     uint64_t hit = ballot(box_sure_hit1(r, c)) & act;
     uint64_t amb = act & ~(hit | ballot(box_miss(c)));
@@ -340,7 +344,7 @@ struct HitState {
 // - records addressed by 32-bit byte offsets, which the scalar loads take as their SGPR offset
 //   (rt_scene_create sends larger trees to MODE_DEEP);
 // - the camera ray's query skips the `alive` AND (only a shadow query's lanes leave early).
-template <bool WIDE>
+template <bool WIDE, bool PK = false>
 __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const RayPre& r, bool active,
                                                   bool any_hit, float any_hit_dist, HitState& hs) {
     uint64_t alive = ballot(active);
@@ -355,7 +359,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
     RT_STAT(13 + so, __popcll(alive));
     // The root's pop-time test (SearchBVH tests every popped node, query.h:252-254) is made
     // here with the initial bestT; the root is then the first entry in hand.
-    uint64_t mask = box_hit_mask(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
+    uint64_t mask = box_hit_mask<PK>(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
     if (mask == 0) {
         if (!any_hit) RT_STAT(17, 1);
         return;
@@ -412,7 +416,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                         if (refs[k] == NO_REF) continue;
                         const float4 p = wv[(3 * k) / 2], q = wv[(3 * k) / 2 + 1];
                         const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
-                        const uint64_t mk_ = box_hit_mask(r, bk, hs.bestT, mask);
+                        const uint64_t mk_ = box_hit_mask<PK>(r, bk, hs.bestT, mask);
                         if (mk_ != 0) {
                             if (pmask != 0) {  // the previous passing entry goes to the stack
                                 st_ref = wrlane(pref, sp, st_ref);
@@ -430,14 +434,14 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                     const uint4 q3 = ldc_u(N + 3);
                     const uint32_t lref = q3.x, rref = q3.y;
                     if (lref != NO_REF) {
-                        const uint64_t ml = box_hit_mask(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
+                        const uint64_t ml = box_hit_mask<PK>(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
                         if (ml != 0) {
                             pref = lref;
                             pmask = ml;
                         }
                     }
                     if (rref != NO_REF) {
-                        const uint64_t mr = box_hit_mask(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
+                        const uint64_t mr = box_hit_mask<PK>(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
                         if (mr != 0) {
                             if (pmask != 0) {
                                 st_ref = wrlane(pref, sp, st_ref);
@@ -477,7 +481,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                     const float4 p = ldc(B), q = ldc(B + 1);
                     ob = BoxP{lo2(p), hi2(p), lo2(q)};
                 }
-                mask = box_hit_mask(r, ob, hs.bestT, mask);
+                mask = box_hit_mask<PK>(r, ob, hs.bestT, mask);
             }
         }
     }
@@ -743,7 +747,7 @@ __device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, b
                                          float any_hit_dist, HitState& hs) {
     if constexpr ((MODE & MODE_DEEP) != 0) traverse_deep(sc, r, active, any_hit, any_hit_dist, hs);
     else if constexpr (MODE == RT_KERNEL_LANE) traverse_lane(sc, r, active, any_hit, any_hit_dist, hs);
-    else traverse_wave_split<(MODE & MODE_WIDE) != 0>(sc, r, active, any_hit, any_hit_dist, hs);
+    else traverse_wave_split<(MODE & MODE_WIDE) != 0, (MODE & MODE_PK) != 0>(sc, r, active, any_hit, any_hit_dist, hs);
 }
 
 // The traversal of a ray at bounce depth `depth` (wave-uniform): camera rays (depth 0) and their
@@ -2666,14 +2670,16 @@ void launch_render(const RenderParams& P, const Launch& L) {
 
 template <int MODE, bool SAMPLES>
 void launch_mode(const RenderParams& P, const Launch& L) {
+    // depth-1 kernels of the wave traversal: packed box tests (box_ends_pk)
+    constexpr int D1_MODE = (MODE & (MODE_DEEP | RT_KERNEL_LANE)) == 0 ? (MODE | MODE_PK) : MODE;
     if (P.max_depth == 1) {
         if constexpr (SAMPLES) {
             if (P.half_waves) {
-                launch_render<render_tiles_kernel<MODE, SAMPLES, true, RT_RENDER_WAVES, 1>>(P, L);
+                launch_render<render_tiles_kernel<D1_MODE, SAMPLES, true, RT_RENDER_WAVES, 1>>(P, L);
                 return;
             }
         }
-        launch_render<render_tiles_kernel<MODE, SAMPLES, true>>(P, L);
+        launch_render<render_tiles_kernel<D1_MODE, SAMPLES, true>>(P, L);
     } else {
         if constexpr (SAMPLES) {
             if (P.half_waves) {

@@ -196,6 +196,32 @@ __host__ __device__ __forceinline__ AxisEnds box_ends(const RayPre& r, const Box
     e.hHz = __builtin_fmaf(b.z.y, r.ivz.x, __builtin_fmaf(b.z.x, r.ivz.y, r.cz.y));
     return e;
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+// The same in packed FMAs (v_pk_fma_f32, two lanes of math per instruction; the min/max swap is
+// an operand select): [lL, hH] = fma([min, max], [ivp, ivp], fma([max, min], [ivn, ivn], [c1, c2]))
+// -- the same two roundings per end, so the same bits.  The depth-1 kernels' wave traversal uses
+// it: c5 72.6 vs 76.1 ms, c3 0.1834 vs 0.1841 ms (`scripts/ab_libs.py`, one box, frames
+// identical; profiles/r03/exp/packed_box_ends_ab_*.log).  The bounce kernels keep the scalar
+// form (packed, their 3-wave build spilled 28 B per lane).
+__device__ __forceinline__ v2f axis_ends(v2f b, v2f iv, v2f c) {
+    const v2f sw = __builtin_shufflevector(b, b, 1, 0);
+    const v2f ivn = __builtin_shufflevector(iv, iv, 1, 1), ivp = __builtin_shufflevector(iv, iv, 0, 0);
+    return __builtin_elementwise_fma(b, ivp, __builtin_elementwise_fma(sw, ivn, c));
+}
+__device__ __forceinline__ AxisEnds box_ends_pk(const RayPre& r, const BoxP& b) {
+    const v2f x = axis_ends(b.x, r.ivx, r.cx), y = axis_ends(b.y, r.ivy, r.cy), z = axis_ends(b.z, r.ivz, r.cz);
+    AxisEnds e;
+    e.lLx = x.x;
+    e.hHx = x.y;
+    e.lLy = y.x;
+    e.hHy = y.y;
+    e.lLz = z.x;
+    e.hHz = z.y;
+    return e;
+}
+#else
+__device__ __forceinline__ AxisEnds box_ends_pk(const RayPre& r, const BoxP& b) { return box_ends(r, b); }  // host pass: parsed, never emitted
+#endif
 // Lc = max(tmin, lowLo) and Hc = min(tmax, highHi): MISS iff Lc > Hc.
 struct BoxEnds {
     float Lc, Hc;

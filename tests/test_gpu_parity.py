@@ -216,14 +216,31 @@ def test_heavy_first_dispatch_changes_nothing(env, monkeypatch):
 
 @pytest.mark.parametrize("tiles", [rt.RT_TILES_ROWS, rt.RT_TILES_LINEAR])
 @pytest.mark.parametrize("kernel", KERNELS)
-@pytest.mark.parametrize("spp,W,H", [(1, 37, 23), (3, 40, 21), (64, 9, 7), (2, 1, 1), (16, 65, 3)])
+@pytest.mark.parametrize("spp,W,H", [(1, 37, 23), (3, 40, 21), (64, 9, 7), (2, 1, 1), (16, 65, 3), (128, 12, 9),
+                                     (256, 7, 5)])
 def test_odd_shapes_against_oracle(spp, W, H, kernel, tiles):
+    """spp 128 / 256: a pixel's samples span the block's waves, and the work queues hand out
+    whole tiles (one barrier per item) instead of wave quarters."""
     hs = host_scene("frog.json")
     cam = hs.camera(W, H)
     rgb, hi, ht = _device_scene("frog.json").render(cam, spp=spp, max_depth=1, aov=True, kernel=kernel,
                                                     tile_order=tiles)
     ref, rhi, rht = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,
                                  hs.tri_object_ids, hs.materials, hs.lights, spp=spp, max_depth=1, aov=True)
+    assert np.array_equal(hi, rhi)
+    assert np.array_equal(ht.view(np.uint32), rht.view(np.uint32))
+    _check_fb(rgb, ref)
+
+
+@pytest.mark.parametrize("spp", [128, 5])
+def test_bounces_whole_tile_items_against_oracle(spp):
+    """Multi-bounce frames through the work queues' whole-tile items (spp 128) and the
+    pixel-loop kernel (spp 5), against the oracle."""
+    hs = host_scene("frog.json")
+    cam = hs.camera(10, 7)
+    rgb, hi, ht = _device_scene("frog.json").render(cam, spp=spp, max_depth=4, aov=True)
+    ref, rhi, rht = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,
+                                 hs.tri_object_ids, hs.materials, hs.lights, spp=spp, max_depth=4, aov=True)
     assert np.array_equal(hi, rhi)
     assert np.array_equal(ht.view(np.uint32), rht.view(np.uint32))
     _check_fb(rgb, ref)

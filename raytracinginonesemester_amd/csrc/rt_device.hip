@@ -130,8 +130,8 @@ struct RenderParams {
     // record their duration per tile (tile_cost, 4 x u16 per tile, 10 ns ticks); the next frame's
     // cut pass moves tiles whose last cost is >= heavy_ticks[c] (descending) to list q's class-c
     // heavy list (heavy_tiles, heavy_cap entries per (class, list), lengths in counter slots
-    // heavy_counter(c, q)).  The first 8 * NCLASS * heavy_cap render blocks take the heavy tiles,
-    // each list's heaviest class first, so the longest tiles start first.  heavy_cap == 0: off.
+    // heavy_counter(c, q)).  Each work queue hands out its list's heavy entries first, heaviest
+    // class first, so the longest tiles start first (render_tiles_kernel).  heavy_cap == 0: off.
     uint16_t* __restrict__ tile_cost;
     int32_t* heavy_tiles;
     int32_t heavy_cap;
@@ -1255,7 +1255,7 @@ __device__ __forceinline__ int global_row(const RenderParams& P, int r) {
 // its pixels written here (P.miss_pixel = the reference's sum of spp miss samples / spp; hit
 // AOV -1), every other tile is appended to a live list the render kernels dequeue.
 // There are P.nqueues lists.  Workgroups are dealt round-robin over the 8 XCDs, so with 8
-// lists a block's home list is blockIdx % 8: RT_TILES_ROWS gives XCD k the tile rows k, k+8,
+// lists the render kernel's queue blockIdx % 8 runs on one XCD: RT_TILES_ROWS gives it the tile rows k, k+8,
 // ... (neighbouring tiles share an L2, the work spreads evenly); RT_TILES_XCD_CHUNK gives it
 // a contiguous 1/8 of the frame.
 // RT_TILES_LINEAR is one list in raster order.  The order is a speed property only.
@@ -1264,8 +1264,8 @@ __device__ __forceinline__ int global_row(const RenderParams& P, int r) {
 constexpr int COUNTER_STRIDE = 64;
 constexpr int NCLASS = 3;                        // heavy cost classes
 // A counter set: 9 list counters COUNTER_STRIDE apart (8 live lists + a spare), then the
-// heavy list lengths packed (class-major, 8 per class: the render blocks read them all with a
-// few wide scalar loads; their appends are few).
+// heavy list lengths packed (class-major, 8 per class), the 8 cut survivor lengths and the 8
+// work-queue heads, each in its own slot.
 constexpr int HEAVY_SLOT0 = 9;
 constexpr int CUT_SLOT0 = HEAVY_SLOT0 + 8 * NCLASS;  // then 8: lengths of the cut pass's survivor lists
 constexpr int HEAD_SLOT0 = CUT_SLOT0 + 8;  // then 8: the render kernel's work-queue heads (one per XCD)

@@ -135,7 +135,7 @@ struct RenderParams {
     uint16_t* __restrict__ tile_cost;
     int32_t* heavy_tiles;
     int32_t heavy_cap;
-    uint32_t heavy_ticks[4];  // NCLASS thresholds, descending
+    uint32_t heavy_ticks[8];  // NCLASS thresholds, descending
     // rt_count_rays only (LANE and DEEP kernels; null otherwise): [1] shadow rays cast, [2]
     // bounce rays traced, the classes of the oracle's orc_stats.rays ([0], camera rays, is
     // W*H*spp by definition and counted on the host), [3] camera rays of the tiles the culling
@@ -1262,7 +1262,14 @@ __device__ __forceinline__ int global_row(const RenderParams& P, int r) {
 // The lists' length counters sit 256 B apart (separate channels) so the appends do not
 // serialise.
 constexpr int COUNTER_STRIDE = 64;
-constexpr int NCLASS = 3;                        // heavy cost classes
+// Heavy cost classes: 5, of which depth-1 frames use the first 3 (c3 0.1835 ms with 3 vs
+// 0.1859 with 4 and 0.1862 with 5) and multi-bounce frames all 5 (c3b 1.768 vs 1.898 ms with 3:
+// their waves' durations spread wider; profiles/r03/exp/heavy_classes_ab_*.log).
+#ifndef RT_NCLASS
+#define RT_NCLASS 5
+#endif
+constexpr int NCLASS = RT_NCLASS;                // (<= 8)
+constexpr int NCLASS_D1 = 3;
 // A counter set: 9 list counters COUNTER_STRIDE apart (8 live lists + a spare), then the
 // heavy list lengths packed (class-major, 8 per class), the 8 cut survivor lengths and the 8
 // work-queue heads, each in its own slot.
@@ -2855,7 +2862,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.queue_cap = P.tile_order == RT_TILES_LINEAR ? P.tiles_total : P.tiles_x * ((tiles_y + 7) / 8);
     // Heavy-first dispatch needs the cut pass (it builds the heavy lists) and the 8 lists.
     // RT_HEAVY_FRAC (speed experiments): a tile is in heavy class c when one of its waves took
-    // at least 2^(NCLASS-1-c) times this fraction of the latest finished frame's render kernel
+    // at least 2^(2-c) times this fraction of the latest finished frame's render kernel
     // (0: off).
     double heavy_frac = 0.12;  // c3: 0.04 0.197, 0.06 0.188, 0.08 0.179, 0.12 0.177, 0.16 0.177 ms
     if (const char* e = std::getenv("RT_HEAVY_FRAC")) heavy_frac = std::atof(e);
@@ -2896,8 +2903,9 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         (void)hipGetLastError();  // a not-ready query is not an error of this call
         // 10 ns ticks (wall_clock64 runs at 100 MHz)
         for (int c = 0; c < NCLASS; ++c) {
-            const double ticks = std::ldexp(heavy_frac, NCLASS - 1 - c) * double(s->kernel_ms_est) * 1e5;
-            P.heavy_ticks[c] = s->kernel_ms_est > 0.f ? uint32_t(std::clamp(ticks, 1.0, 65535.0)) : 0xffffffffu;
+            const double ticks = std::ldexp(heavy_frac, 2 - c) * double(s->kernel_ms_est) * 1e5;
+            const bool used = c < (o->max_depth == 1 ? NCLASS_D1 : NCLASS);
+            P.heavy_ticks[c] = s->kernel_ms_est > 0.f && used ? uint32_t(std::clamp(ticks, 1.0, 65535.0)) : 0xffffffffu;
         }
         // the costs are per tile of this geometry
         const uint64_t key = (uint64_t(uint32_t(P.tiles_total)) * 0x9E3779B97F4A7C15ull) ^

@@ -196,6 +196,15 @@ __device__ int* g_cut_counts;
 #define RT_PHASE(P, x, y, k) do { } while (0)
 #endif
 
+#ifdef RT_LANE_ITERS  // instrumented variant builds only (with RT_WAVE_TIMES): per work item, the
+// loop iterations (record visits) of the per-lane traversals of its bounce and bounce-shadow
+// rays: [0] sum over the wave's traversal calls of its longest lane's iterations, [1] the longest
+// lane's total over all calls, [2] all lanes' total, [3] calls.  [0] is what the wave waits for
+// when lanes meet after every traversal; [1] what it would wait for if they did not.
+__device__ uint32_t* g_lane_iters;
+__device__ uint32_t* g_lane_acc;  // per thread slot of the grid: 4 running words
+#endif
+
 // ---- node accessors ---------------------------------------------------------------------
 // Scene arrays are immutable while a frame renders: read them through the constant address
 // space, so wave-uniform node addresses become scalar loads even inside loops that also
@@ -321,7 +330,37 @@ struct HitState {
 #ifdef RT_STATS
     uint32_t pops;
 #endif
+#ifdef RT_LANE_ITERS
+    uint32_t iters;
+#endif
 };
+
+#ifdef RT_LANE_ITERS
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
+    return v;
+}
+// every lane of the wave calls it after a per-lane traversal
+__device__ __forceinline__ void lane_iters_note(uint32_t it) {
+    if (g_lane_acc == nullptr) return;
+    uint32_t* a = g_lane_acc + 4 * ((size_t)blockIdx.x * 256 + threadIdx.x);
+    a[1] += it;
+    const uint32_t m = wave_max_u32(it);
+    if ((threadIdx.x & 63) == 0) {
+        a[0] += m;
+        a[3] += 1;
+    }
+}
+#define RT_LI_ZERO(hs) ((hs).iters = 0)
+#define RT_LI_STEP(hs) (++(hs).iters)
+#else
+#define RT_LI_ZERO(hs) do { } while (0)
+#define RT_LI_STEP(hs) do { } while (0)
+#endif
 
 // ---- WAVE traversal ---------------------------------------------------------------------
 // One DFS per wavefront over a shared stack held in three VGPRs (entry k in lane k: node ref
@@ -611,11 +650,13 @@ __device__ __forceinline__ void traverse_lane_lds(const SceneView& sc, const Ray
                                                   float any_hit_dist, HitState& hs, uint32_t* stk) {
     hs.bestT = FLT_MAX;
     hs.slot = -1;
+    RT_LI_ZERO(hs);
     if (!active) return;
     if (!box_hit(r, own_box(sc, sc.root_ref, true), kRayTMin, hs.bestT)) return;  // the root's pop-time test
     uint32_t ref = sc.root_ref;
     int sp = 0, stale = 0;
     while (true) {
+        RT_LI_STEP(hs);
         uint32_t next = NO_REF;  // the entry to hold
         if (ref & LEAF_BIT) {
             const uint32_t slot = ref & ~LEAF_BIT;
@@ -670,11 +711,13 @@ __device__ __forceinline__ void traverse_lane_lds_wide(const SceneView& sc, cons
                                                        float any_hit_dist, HitState& hs, uint32_t* stk) {
     hs.bestT = FLT_MAX;
     hs.slot = -1;
+    RT_LI_ZERO(hs);
     if (!active) return;
     if (!box_hit(r, own_box(sc, sc.root_ref, true), kRayTMin, hs.bestT)) return;  // the root's pop-time test
     uint32_t ref = sc.root_ref;
     int sp = 0, stale = 0;
     while (true) {
+        RT_LI_STEP(hs);
         uint32_t next = NO_REF;  // the entry to hold
         if (ref & LEAF_BIT) {
             const uint32_t slot = ref & ~LEAF_BIT;
@@ -760,6 +803,9 @@ __device__ __forceinline__ void traverse_at(const SceneView& sc, int depth, cons
         constexpr bool W = (MODE & MODE_WIDE) != 0;
         if (depth > 0 && lane_ok<W>(sc)) {
             traverse_lane<W>(sc, r, active, any_hit, any_hit_dist, hs, reinterpret_cast<uint32_t*>(lds));
+#ifdef RT_LANE_ITERS
+            lane_iters_note(active ? hs.iters : 0u);
+#endif
             return;
         }
     }
@@ -1741,6 +1787,12 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
 #ifdef RT_WAVE_TIMES
         const unsigned long long wt0 = wall_clock64();
 #endif
+#ifdef RT_LANE_ITERS
+        if (g_lane_acc) {
+            uint32_t* a = g_lane_acc + 4 * ((size_t)blockIdx.x * 256 + threadIdx.x);
+            a[0] = a[1] = a[2] = a[3] = 0;
+        }
+#endif
         if (R.tile_cost && lane == 0) {
             t_start[wv] = (uint32_t)wall_clock64();
             t_item[wv] = (uint32_t)tile * WPT + qw;
@@ -1752,11 +1804,28 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
             const uint32_t d = (uint32_t)wall_clock64() - t_start[wv];
             R.tile_cost[t_item[wv]] = (uint16_t)(d < 0xffffu ? d : 0xffffu);
         }
+#if defined(RT_WAVE_TIMES) && defined(RT_LANE_ITERS)
+        if (g_lane_iters) {
+            const uint32_t* a = g_lane_acc + 4 * ((size_t)blockIdx.x * 256 + threadIdx.x);
+            const uint32_t mx = wave_max_u32(a[1]), sm = wave_sum_u32(a[1]);
+            if ((threadIdx.x & 63) == 0) {
+                g_lane_iters[((size_t)tile * WPT + qw) * 4 + 1] = mx;
+                g_lane_iters[((size_t)tile * WPT + qw) * 4 + 2] = sm;
+            }
+        }
+#endif
 #ifdef RT_WAVE_TIMES
         if (g_wave_times && fresh_lane_id() == 0) {
             const size_t k = ((size_t)tile * WPT + qw) * 2;
             g_wave_times[k] = wt0;
             g_wave_times[k + 1] = wall_clock64();
+#ifdef RT_LANE_ITERS
+            if (g_lane_iters) {
+                const uint32_t* a = g_lane_acc + 4 * ((size_t)blockIdx.x * 256 + threadIdx.x);
+                g_lane_iters[((size_t)tile * WPT + qw) * 4 + 0] = a[0];
+                g_lane_iters[((size_t)tile * WPT + qw) * 4 + 3] = a[3];
+            }
+#endif
             if (g_wave_meta) {
                 const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID
                 g_wave_meta[(size_t)tile * WPT + qw] = bx << 8 | xcc << 4 | (first ? 4u : 0u) | wv;
@@ -3100,6 +3169,13 @@ extern "C" int rt_debug_wave_phase_set(void* dev_ptr) {
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wave_phase), &dev_ptr, sizeof(dev_ptr)));
     return RT_OK;
 }
+#ifdef RT_LANE_ITERS
+extern "C" int rt_debug_lane_iters_set(void* iters_ptr, void* acc_ptr) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_lane_iters), &iters_ptr, sizeof(iters_ptr)));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_lane_acc), &acc_ptr, sizeof(acc_ptr)));
+    return RT_OK;
+}
+#endif
 extern "C" int rt_debug_wave_times_set(void* dev_ptr, void* cut_counts_ptr) {
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wave_times), &dev_ptr, sizeof(dev_ptr)));
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_cut_counts), &cut_counts_ptr, sizeof(cut_counts_ptr)));

@@ -715,58 +715,78 @@ __device__ __forceinline__ void traverse_lane_lds_wide(const SceneView& sc, cons
     if (!active) return;
     if (!box_hit(r, own_box(sc, sc.root_ref, true), kRayTMin, hs.bestT)) return;  // the root's pop-time test
     uint32_t ref = sc.root_ref;
+    bool retest = false;  // the entry in ref was popped and takes the pop-time re-test first
     int sp = 0, stale = 0;
+    // One batch of loads per iteration and lane: the entry's record (a leaf's 64 bytes, which
+    // hold its own box, or a 4-ary record) and, for a popped internal entry that takes the
+    // re-test, its box.  The lanes of a wave sit at leaves and internal entries at once; with
+    // the loads inside the leaf and internal branches, and the re-test's inside the pop loop,
+    // an iteration waited for up to three memory round trips one after another.
     while (true) {
         RT_LI_STEP(hs);
+        const bool leaf = (ref & LEAF_BIT) != 0;
+        const uint32_t idx = ref & ~LEAF_BIT;
+        const float4* R = leaf ? sc.leaf + 4 * (size_t)idx : sc.wnode + 8 * (size_t)idx;
+        const float4 w0 = R[0], w1 = R[1], w2 = R[2], w3 = R[3];
+        // (defaults that do not read w0: a copy of a loaded value waits for the load)
+        float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f), w5 = w4, w6 = w4;
+        if (!leaf) {
+            w4 = R[4];
+            w5 = R[5];
+            w6 = R[6];
+        }
+        // own_box's six floats are consecutive in both layouts: a leaf's at word 10 of its
+        // record, an internal node's at the start of its ibox entry; loaded as such (a select
+        // between loaded values would wait for the record before the other loads are issued)
+        const float* bp = leaf ? reinterpret_cast<const float*>(R + 2) + 2 : reinterpret_cast<const float*>(sc.ibox + 2 * (size_t)idx);
+        v2f bx = {0.f, 0.f}, by = bx, bz = bx;
+        if (retest) {
+            bx = *reinterpret_cast<const v2f*>(bp);
+            by = *reinterpret_cast<const v2f*>(bp + 2);
+            bz = *reinterpret_cast<const v2f*>(bp + 4);
+        }
+        // pushed before the latest bestT change: the pop-time re-test
+        const bool go = !retest || box_hit(r, BoxP{bx, by, bz}, kRayTMin, hs.bestT);
         uint32_t next = NO_REF;  // the entry to hold
-        if (ref & LEAF_BIT) {
-            const uint32_t slot = ref & ~LEAF_BIT;
-            const float4* L = sc.leaf + 4 * (size_t)slot;
-            const float4 a = L[0], b = L[1], c = L[2];
-            float t, u, v;
-            if (mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin, hs.bestT, t, u, v)) {
-                hs.bestT = t;
-                hs.slot = (int32_t)slot;
-                stale = sp;
-                if (any_hit && t < any_hit_dist) return;
-            }
-        } else {
-            const float4* W = sc.wnode + 8 * (size_t)ref;
-            float4 wv[7];
+        if (go) {
+            if (leaf) {
+                float t, u, v;
+                if (mt_g(r, mk(w0.x, w0.y, w0.z), mk(w1.x, w1.y, w1.z), mk(w1.w, w2.x, w2.y), kRayTMin, hs.bestT, t, u,
+                         v)) {
+                    hs.bestT = t;
+                    hs.slot = (int32_t)idx;
+                    stale = sp;
+                    if (any_hit && t < any_hit_dist) return;
+                }
+            } else {
+                const float4 wv[7] = {w0, w1, w2, w3, w4, w5, w6};
+                const uint32_t refs[4] = {__float_as_uint(w6.x), __float_as_uint(w6.y), __float_as_uint(w6.z),
+                                          __float_as_uint(w6.w)};
 #pragma unroll
-            for (int k = 0; k < 7; ++k) wv[k] = W[k];
-            const uint32_t refs[4] = {__float_as_uint(wv[6].x), __float_as_uint(wv[6].y), __float_as_uint(wv[6].z),
-                                      __float_as_uint(wv[6].w)};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (refs[k] == NO_REF) continue;
-                const float4 p = wv[(3 * k) / 2], q = wv[(3 * k) / 2 + 1];
-                const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
-                if (box_hit(r, bk, kRayTMin, hs.bestT)) {
-                    if (next != NO_REF) {
-                        stk[sp * BLOCK] = next;
-                        ++sp;
+                for (int k = 0; k < 4; ++k) {
+                    if (refs[k] == NO_REF) continue;
+                    const float4 p = wv[(3 * k) / 2], q = wv[(3 * k) / 2 + 1];
+                    const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
+                    if (box_hit(r, bk, kRayTMin, hs.bestT)) {
+                        if (next != NO_REF) {
+                            stk[sp * BLOCK] = next;
+                            ++sp;
+                        }
+                        next = refs[k];
                     }
-                    next = refs[k];
                 }
             }
         }
         if (next != NO_REF) {
             ref = next;
+            retest = false;
             continue;
         }
-        bool found = false;
-        while (sp > 0) {
-            --sp;
-            ref = stk[sp * BLOCK];
-            if (sp < stale) {  // pushed before the latest bestT change: the pop-time re-test
-                stale = sp;
-                if (!box_hit(r, own_box(sc, ref, false), kRayTMin, hs.bestT)) continue;
-            }
-            found = true;
-            break;
-        }
-        if (!found) return;
+        if (sp == 0) return;
+        --sp;
+        ref = stk[sp * BLOCK];
+        retest = sp < stale;
+        if (retest) stale = sp;
     }
 }
 
@@ -992,13 +1012,130 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, con
 }
 
 
+// TraceRayIterative (query.h:156-220) from the camera ray's hit on, for half waves over one
+// light, the lanes in pairs: a sample's path lives in lane l < 32 (the lanes that trace in a half
+// wave), and lane l + 32, otherwise idle, traces that path's shadow rays.  The bounce direction
+// does not depend on the shadow ray's answer (ShadeDirect draws no random numbers;
+// shader.h:65-110), so the shadow ray of depth d and the bounce ray of depth d + 1 are traced by
+// one per-lane traversal call, and depth d's `radiance += throughput * Lo` waits for that call:
+// the adds keep their order.  Each call's time is its longest lane's, so a wave's path time
+// drops from two calls per depth to one (c3b: the longest waves bound the kernel, DESIGN.md
+// §4.10).  Same tests, same arithmetic and same order per sample as the unpaired loop: exact.
+template <int MODE>
+__device__ __forceinline__ void paired_bounces(const RenderParams& P, RayPre& ray, bool alive, f3& thr, f3& radiance,
+                                               uint32_t& rng, float* park, HitState hs) {
+    constexpr bool W = (MODE & MODE_WIDE) != 0;
+    const SceneView& sc = P.sc;
+    const bool upper = lane_id() >= 32;
+    const int max_depth = P.max_depth;
+    bool need_up = false;  // upper lanes: `ray` holds the shadow ray to trace
+    float dist_up = 0.f;
+    bool pend = false, lit_p = false;  // lower lanes: a depth's Lo awaits its shadow ray
+    f3 thr_p = mk(0.f, 0.f, 0.f), Lo_p = thr_p, Lo_lit_p = thr_p;
+    // hs: the closest hit of the path ray of `depth` (depth 0: the camera ray's, wave traversal)
+    for (int depth = 0;; ++depth) {
+        need_up = false;
+        const bool hit = alive && hs.slot >= 0;
+        if (alive && !hit) {
+            radiance = add(radiance, mul(thr, P.miss));
+            alive = false;
+        }
+        bool need = false;
+        float dist = 0.f;
+        f3 so = mk(0.f, 0.f, 0.f), sd = so;
+        if (hit) {
+            const SurfHit sh = resolve_hit<false>(sc, ray, hs.slot);
+            const DevMaterial m = material_of(sc, sh.tri);
+            // ShadeDirect (shader.h:65-110) over the one light
+            const f3 N = unit(sh.n);
+            const f3 V = unit(sub(ray.o, sh.p));
+            f3 Lo = mk(0.f, 0.f, 0.f);
+            Lo = add(Lo, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 0.05f));
+            Lo = add(Lo, mk(m.emission[0], m.emission[1], m.emission[2]));
+            const DevLight& lt = sc.lights[0];
+            const f3 lpos = mk(lt.pos[0], lt.pos[1], lt.pos[2]);
+            f3 contrib = mk(0.f, 0.f, 0.f);
+            bool lit = false;
+            const f3 L = unit(sub(lpos, sh.p));
+            const float NdotL = fmaxf(dot(N, L), 0.0f);
+            if (NdotL > 0.0f) {
+                const f3 f = eval_brdf(m, sh.n, V, L);
+                const f3 rad = scale(mk(lt.color[0], lt.color[1], lt.color[2]), (float)lt.intensity);
+                contrib = scale(mul(rad, f), NdotL);
+                lit = true;
+                const f3 toL = sub(lpos, sh.p);
+                dist = sqrtf(dot(toL, toL));
+                if (dist > 0.0f) {
+                    need = true;
+                    so = add(sh.p, scale(N, RT_EPS));
+                    sd = divf(toL, dist);
+                }
+            }
+            thr_p = thr;
+            Lo_p = Lo;
+            Lo_lit_p = add(Lo, contrib);
+            lit_p = lit;
+            pend = true;
+            // bounce (query.h:193-216)
+            if (depth + 1 < max_depth) {
+                const float kd = m.kd, kr = m.kr, total = kd + kr;
+                if (total <= 0.0f) {
+                    alive = false;
+                } else {
+                    const f3 Nb = unit(sh.n);
+                    const float xi = rng_next(rng);
+                    if (P.diffuse_bounce && xi < kd / total) {
+                        f3 dd = random_unit_vector(rng);
+                        if (!(dot(dd, Nb) > 0.0f)) dd = mk(-dd.x, -dd.y, -dd.z);
+                        ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), dd, scene_bmax(sc));
+                        const float nl = fmaxf(dot(Nb, dd), 0.0f);
+                        thr = mul(thr, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 2.0f * nl));
+                    } else {
+                        const f3 I = unit(ray.d);
+                        const f3 refl = sub(I, scale(Nb, 2.0f * dot(I, Nb)));
+                        ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), refl, scene_bmax(sc));
+                        thr = mul(thr, scale(mk(m.spec[0], m.spec[1], m.spec[2]), kr));
+                    }
+                    if (thr.x < 1e-4f && thr.y < 1e-4f && thr.z < 1e-4f) alive = false;
+                }
+            } else {
+                alive = false;
+            }
+        }
+        // the shadow ray to the partner lane (every lane shuffles: converged)
+        const uint64_t needm = ballot(need);
+        const float ox = __shfl_xor(so.x, 32), oy = __shfl_xor(so.y, 32), oz = __shfl_xor(so.z, 32);
+        const float dx = __shfl_xor(sd.x, 32), dy = __shfl_xor(sd.y, 32), dz = __shfl_xor(sd.z, 32);
+        const float dd = __shfl_xor(dist, 32);
+        if (upper) {
+            need_up = lane_in(needm << 32);
+            dist_up = dd;
+            if (need_up) ray = make_ray(mk(ox, oy, oz), mk(dx, dy, dz), scene_bmax(sc));
+        }
+        // (a depth's Lo may wait with no shadow ray to trace: NdotL <= 0 or a zero distance)
+        if (ballot(alive || need_up || pend) == 0) break;
+        traverse_lane<W>(sc, ray, alive || need_up, upper, dist_up, hs, reinterpret_cast<uint32_t*>(park));
+#ifdef RT_LANE_ITERS
+        lane_iters_note((alive || need_up) ? hs.iters : 0u);
+#endif
+        // IsInShadow's answer (shader.h:44-62) of the upper lanes, read by their lower partners
+        const uint64_t occ = ballot(need_up && hs.slot >= 0 && hs.bestT < dist_up);
+        if (pend) {
+            const bool occluded = lane_in(occ >> 32);
+            radiance = add(radiance, mul(thr_p, (lit_p && !occluded) ? Lo_lit_p : Lo_p));
+            pend = false;
+        }
+    }
+}
+
 // One camera sample through TraceRayIterative (query.h:156-220) + ShadeDirect (shader.h).
 // All lanes of a wave call it; `valid` marks lanes owning a sample.  D1: max_depth == 1 (no
 // bounce; the configuration the benchmarks run).
-template <int MODE, bool D1>
+template <int MODE, bool D1, bool PAIR = false>
 // The primary-hit AOV (P.hit_idx / P.hit_t at element aov, when aov >= 0) is written as soon as
 // the camera ray's traversal ends, so nothing of it stays live across the shading.
 // park: the lane's own LDS slot (slot k of the lane at park[k * BLOCK]).
+// PAIR (half waves): the camera ray's shading on in paired_bounces when the scene has one light.
 __device__ __forceinline__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int64_t aov,
                                           float* park) {
     const SceneView& sc = P.sc;
@@ -1030,6 +1167,24 @@ __device__ __forceinline__ f3 trace_sample(const RenderParams& P, bool valid, in
     f3 thr = mk(1.f, 1.f, 1.f);
     const int max_depth = P.max_depth;
     bool alive = valid && max_depth > 0;
+    bool paired = false;
+    if constexpr (PAIR && MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0)
+        paired = sc.num_lights == 1 && lane_ok<(MODE & MODE_WIDE) != 0>(sc);
+    if constexpr (PAIR && MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0) {
+        if (paired) {
+            // depth 0's camera ray takes the wave traversal; its shadow ray and every later ray
+            // go to paired_bounces' per-lane traversals
+            HitState hs;
+            traverse<MODE>(sc, ray, alive, false, 0.0f, hs);
+            if (valid && aov >= 0) {
+                const bool hit = alive && hs.slot >= 0;
+                P.hit_idx[aov] = hit ? leaf_tri<false>(sc, hs.slot) : -1;
+                P.hit_t[aov] = hit ? hs.bestT : -1.0f;
+            }
+            paired_bounces<MODE>(P, ray, alive, thr, radiance, rng, park, hs);
+            return clamp01(radiance);
+        }
+    }
     for (int depth = 0; depth < max_depth; ++depth) {
         if (ballot(alive) == 0) break;
         HitState hs;
@@ -1621,7 +1776,7 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, ui
         // it, or addresses made from it, live (and spilled) across the shading.
         if (s == 0) kpix[t >> P.spp_log2] = pix;
         const int64_t aov = valid && P.hit_idx ? (int64_t)pix * P.spp + s : -1;
-        const f3 c = trace_sample<MODE, D1>(P, valid, x, y, s, aov, park + t);
+        const f3 c = trace_sample<MODE, D1, LS == 1>(P, valid, x, y, s, aov, park + t);
         RT_PHASE(P, x, r, 1);
         // The thread index again, from the wave's index and a lane id the compiler cannot
         // merge with the first one (mbcnt of a zero read back from LDS): keeping t itself live

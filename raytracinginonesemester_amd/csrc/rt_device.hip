@@ -1876,6 +1876,14 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, uin
 #ifndef RT_BOUNCE_WAVES
 #define RT_BOUNCE_WAVES 3
 #endif
+// Scenes whose data (records, leaves, normals) exceed kBigSceneBytes do not stay in the L2s and
+// MALL: their depth-1 wave kernels run 8 waves per SIMD (64 VGPRs, a few spills outside the
+// traversal loops), more waves to hide the record loads' latency (c5, 345 MB: DESIGN.md §4.2).
+// RT_BIG_SCENE_BYTES overrides the threshold (A/B).
+#ifndef RT_RENDER_WAVES_BIG
+#define RT_RENDER_WAVES_BIG 8
+#endif
+constexpr size_t kBigSceneBytes = size_t(64) << 20;
 // Heavy-first dispatch: the queues hand out the heavy lists first; the waves record their
 // items' costs.
 template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0>
@@ -2886,6 +2894,7 @@ struct Launch {
     hipStream_t st;
     hipEvent_t start, stop;
     int cus;
+    bool big;  // scene data beyond kBigSceneBytes: the depth-1 wave kernels at RT_RENDER_WAVES_BIG
 };
 template <auto KERNEL>
 void launch_render(const RenderParams& P, const Launch& L) {
@@ -2907,6 +2916,12 @@ void launch_mode(const RenderParams& P, const Launch& L) {
         if constexpr (SAMPLES) {
             if (P.half_waves) {
                 launch_render<render_tiles_kernel<D1_MODE, SAMPLES, true, RT_RENDER_WAVES, 1>>(P, L);
+                return;
+            }
+        }
+        if constexpr ((MODE & (MODE_DEEP | RT_KERNEL_LANE)) == 0) {
+            if (L.big) {
+                launch_render<render_tiles_kernel<D1_MODE, SAMPLES, true, RT_RENDER_WAVES_BIG>>(P, L);
                 return;
             }
         }
@@ -3214,7 +3229,11 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
-        const Launch L{st, s->evm[slot], s->ev1[slot], s->cus};
+        static const size_t big_bytes = [] {
+            const char* e = std::getenv("RT_BIG_SCENE_BYTES");
+            return e ? (size_t)std::strtoull(e, nullptr, 10) : kBigSceneBytes;
+        }();
+        const Launch L{st, s->evm[slot], s->ev1[slot], s->cus, s->bytes > big_bytes};
         if (s->deep) launch<MODE_DEEP>(P, samples, L);
         else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, L);
         else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, L);

@@ -172,6 +172,29 @@ def test_bounce_paths_per_lane_traversal(name, flags):
     _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
 
 
+@pytest.mark.parametrize("name", ["c3b_small", "frog_bounce", "sphere_single"])
+@pytest.mark.parametrize("flags", [0, rt._lib.RT_FLAG_BINARY])
+@pytest.mark.parametrize("half", ["0", "1"])
+def test_one_light_bounce_loops_parity(name, flags, half, monkeypatch):
+    """One-light multi-bounce frames through both bounce loops: half waves (the default) pair a
+    path's lane with a shadow lane (paired_bounces: a depth's Lo add waits for its shadow ray's
+    answer, traced beside the next bounce ray); RT_HALF_WAVES=0 forces full waves and the
+    unpaired loop.  The reference's outputs bit for bit, AOVs included."""
+    monkeypatch.setenv("RT_HALF_WAVES", half)
+    meta = golden_meta(name)
+    assert meta["max_depth"] > 1 and meta["num_lights"] == 1
+    scene = G_SCENES[name]
+    hs = host_scene(scene)
+    cam = hs.camera(meta["width"], meta["height"])
+    rgb, hi, ht = _device_scene(scene).render(cam, spp=meta["spp"], max_depth=meta["max_depth"],
+                                              diffuse_bounce=bool(meta["diffuse_bounce"]),
+                                              miss_color=hexv(meta["miss_color"]), aov=True, flags=flags)
+    assert np.array_equal(hi.reshape(-1), golden_array(name, "hits.i32.gz", np.int32))
+    assert np.array_equal(ht.reshape(-1).view(np.uint32),
+                          golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
+    _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
+
+
 def test_c3b_full_frame_matches_reference():
     """c3b: frog.json as shipped (max_bounces 8, diffuse bounces) at 1920x1080x16 against the
     reference's own full-size outputs (hit AOVs by sha256, float frame, P6 file)."""

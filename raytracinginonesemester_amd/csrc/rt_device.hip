@@ -110,6 +110,7 @@ struct RenderParams {
     int32_t tile_w, tile_h, tiles_x, tiles_total;     // pixel tile per block
     int32_t lane_samples;                             // 1: one sample per lane; else pixel loop
     int32_t half_waves;                               // samples kernel: lanes >= 64 >> half_waves idle
+    int32_t paired_only;                              // multi-bounce, half waves, one light: LS = 3 kernels
     int32_t tile_order;                               // RT_TILES_*
     int32_t spp_log2, tile_w_log2;                    // samples kernel: both powers of two
     int32_t cull;                                     // tile culling against the root box
@@ -1131,11 +1132,12 @@ __device__ __forceinline__ void paired_bounces(const RenderParams& P, RayPre& ra
 // One camera sample through TraceRayIterative (query.h:156-220) + ShadeDirect (shader.h).
 // All lanes of a wave call it; `valid` marks lanes owning a sample.  D1: max_depth == 1 (no
 // bounce; the configuration the benchmarks run).
-template <int MODE, bool D1, bool PAIR = false>
+template <int MODE, bool D1, int PAIR = 0>
 // The primary-hit AOV (P.hit_idx / P.hit_t at element aov, when aov >= 0) is written as soon as
 // the camera ray's traversal ends, so nothing of it stays live across the shading.
 // park: the lane's own LDS slot (slot k of the lane at park[k * BLOCK]).
-// PAIR (half waves): the camera ray's shading on in paired_bounces when the scene has one light.
+// PAIR (half waves): 1, the camera ray's shading on in paired_bounces when the scene has one
+// light; 2, always (the paired-only kernels, LS = 3: no unpaired loop in the kernel).
 __device__ __forceinline__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int64_t aov,
                                           float* park) {
     const SceneView& sc = P.sc;
@@ -1167,11 +1169,11 @@ __device__ __forceinline__ f3 trace_sample(const RenderParams& P, bool valid, in
     f3 thr = mk(1.f, 1.f, 1.f);
     const int max_depth = P.max_depth;
     bool alive = valid && max_depth > 0;
-    bool paired = false;
-    if constexpr (PAIR && MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0)
+    bool paired = PAIR == 2;
+    if constexpr (PAIR == 1 && MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0)
         paired = sc.num_lights == 1 && lane_ok<(MODE & MODE_WIDE) != 0>(sc);
-    if constexpr (PAIR && MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0) {
-        if (paired) {
+    if constexpr (PAIR != 0 && MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0) {
+        if (PAIR == 2 || paired) {
             // depth 0's camera ray takes the wave traversal; its shadow ray and every later ray
             // go to paired_bounces' per-lane traversals
             HitState hs;
@@ -1745,7 +1747,7 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, ui
     // samples in its low lanes, so a tile's longest wave, which bounds a short kernel, has half
     // the rays' path union; lt is the sample's index in the (half-size) tile.  A template
     // parameter: a run-time flag here cost the full-wave c3 kernel 0.8 % (register allocation).
-    constexpr int wl = 64 >> LS;  // lanes that trace
+    constexpr int wl = LS != 0 ? 32 : 64;  // lanes that trace
     const bool on = (t & 63) < wl;
     const int lt = ((int)qw * wl) | (t & (wl - 1));
     {
@@ -1776,7 +1778,7 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, ui
         // it, or addresses made from it, live (and spilled) across the shading.
         if (s == 0) kpix[t >> P.spp_log2] = pix;
         const int64_t aov = valid && P.hit_idx ? (int64_t)pix * P.spp + s : -1;
-        const f3 c = trace_sample<MODE, D1, LS == 1>(P, valid, x, y, s, aov, park + t);
+        const f3 c = trace_sample<MODE, D1, LS == 3 ? 2 : (LS == 1 ? 1 : 0)>(P, valid, x, y, s, aov, park + t);
         RT_PHASE(P, x, r, 1);
         // The thread index again, from the wave's index and a lane id the compiler cannot
         // merge with the first one (mbcnt of a zero read back from LDS): keeping t itself live
@@ -1880,6 +1882,10 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, uin
 // MALL: their depth-1 wave kernels run 8 waves per SIMD (64 VGPRs, a few spills outside the
 // traversal loops), more waves to hide the record loads' latency (c5, 345 MB: DESIGN.md §4.2).
 // RT_BIG_SCENE_BYTES overrides the threshold (A/B).
+// The paired-only bounce kernels (one light, half waves: paired_bounces and nothing else).
+#ifndef RT_PAIRED_WAVES
+#define RT_PAIRED_WAVES 4
+#endif
 #ifndef RT_RENDER_WAVES_BIG
 #define RT_RENDER_WAVES_BIG 8
 #endif
@@ -2927,6 +2933,12 @@ void launch_mode(const RenderParams& P, const Launch& L) {
         }
         launch_render<render_tiles_kernel<D1_MODE, SAMPLES, true>>(P, L);
     } else {
+        if constexpr (SAMPLES && (MODE & (MODE_DEEP | RT_KERNEL_LANE)) == 0) {
+            if (P.half_waves && P.paired_only) {
+                launch_render<render_tiles_kernel<MODE, SAMPLES, false, RT_PAIRED_WAVES, 3>>(P, L);
+                return;
+            }
+        }
         if constexpr (SAMPLES) {
             if (P.half_waves) {
                 launch_render<render_tiles_kernel<MODE, SAMPLES, false, RT_BOUNCE_WAVES, 1>>(P, L);
@@ -3079,6 +3091,14 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     if (const char* e = std::getenv("RT_HALF_WAVES")) half = std::clamp(std::atoi(e), 0, 1);
     if (!samples || o->spp > (64 >> half)) half = 0;
     P.half_waves = half;
+    // One light and a tree whose DFS fits the per-lane LDS stacks: the bounce kernels that hold
+    // only the paired loop (paired_bounces), fewer live registers than the kernels that also
+    // carry the unpaired one.  RT_PAIRED_ONLY=0 turns them off (A/B).
+    P.paired_only = half && o->max_depth > 1 && s->nlights == 1 && !s->deep && o->kernel != RT_KERNEL_LANE &&
+                            (P.sc.wide ? s->lane_wide : s->lane_stack)
+                        ? 1
+                        : 0;
+    if (const char* e = std::getenv("RT_PAIRED_ONLY")) P.paired_only = P.paired_only && std::atoi(e) != 0;
     int ppb = samples ? (BLOCK >> half) / o->spp : BLOCK;  // pixels per block
     int tw = 1;
     while (tw * tw < ppb) tw <<= 1;                // square-ish power-of-two tile

@@ -2490,6 +2490,7 @@ struct rt_scene {
     bool caller_ordered = false;
     hipStream_t prep = nullptr;
     uint64_t launches = 0;
+    uint64_t est_next = 0;  // the oldest frame not yet seen finished (heavy-threshold estimate)
     size_t bytes = 0;
     // Work buffers rotate over kSets per frame (frame k: set k % 3; its cull pass zeroes the
     // counters of set k+1, last used by frame k-2).  A frame launched on another stream than
@@ -3142,22 +3143,30 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     const uint64_t k = s->launches;
     auto ev1_of = [&](uint64_t f) { return s->ev1[f % rt_scene::kRing]; };
     // The latest finished frame's render-kernel time sets the heavy threshold (non-blocking
-    // queries; none finished yet: the previous estimate, or no heavy lists).
+    // queries; none finished yet: the previous estimate, or no heavy lists).  The frames are
+    // scanned forward from the oldest one not yet seen finished (amortised one query per
+    // frame), so a caller that submits many frames ahead of the GPU still gets an estimate once
+    // its first frames finish (a look-back over the last three frames found none: all in flight).
     bool cost_reset = false;
     if (costs) {
-        for (uint64_t back = 1; back <= 3 && back <= k; ++back) {
-            const int f = int((k - back) % rt_scene::kRing);
-            if (hipEventQuery(s->ev1[f]) != hipSuccess) continue;
+        uint64_t f = std::max<uint64_t>(s->est_next, k >= uint64_t(rt_scene::kRing) ? k - (rt_scene::kRing - 1) : 0);
+        int64_t last = -1;
+        for (; f < k; ++f) {
+            if (hipEventQuery(s->ev1[f % rt_scene::kRing]) != hipSuccess) break;
+            last = int64_t(f);
+        }
+        s->est_next = f;
+        if (last >= 0) {
+            const int fl = int(uint64_t(last) % rt_scene::kRing);
             // the render kernel's time, or the frame period when shorter (overlapping frames:
             // RT_FLAG_OVERLAP starts a kernel while the previous one still runs)
             float ms = 0.f, period = 0.f;
-            if (hipEventElapsedTime(&ms, s->evm[f], s->ev1[f]) == hipSuccess) {
-                const int f0 = int((k - back - 1) % rt_scene::kRing);
-                if (k - back >= 1 && hipEventElapsedTime(&period, s->ev1[f0], s->ev1[f]) == hipSuccess && period > 0.f)
+            if (hipEventElapsedTime(&ms, s->evm[fl], s->ev1[fl]) == hipSuccess) {
+                const int f0 = int(uint64_t(last - 1) % rt_scene::kRing);
+                if (last >= 1 && hipEventElapsedTime(&period, s->ev1[f0], s->ev1[fl]) == hipSuccess && period > 0.f)
                     ms = std::min(ms, period);
                 s->kernel_ms_est = ms;
             }
-            break;
         }
         (void)hipGetLastError();  // a not-ready query is not an error of this call
         // 10 ns ticks (wall_clock64 runs at 100 MHz)

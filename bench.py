@@ -428,7 +428,13 @@ def band_shards(hs, cam, cfg, local, steps=20):
         for r in range(n):
             o, _j = ds.make_opts(spp=cfg["spp"], max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"],
                                  band_rows=BAND_ROWS, band_index=r, band_count=n)
-            for _ in range(3 + steps):
+            # warm-up frames waited for one by one: heavy-first takes its threshold from a
+            # finished frame of this shard, as a rank's own pipelined frames give it (submitted
+            # back to back, every frame of the loop ran before any had finished: no heavy lists)
+            for _ in range(4):
+                ds.render_device(cam, o, 0, stream=None, p6_dev_ptr=p6.data_ptr())
+                torch.cuda.synchronize()
+            for _ in range(steps):
                 ds.render_device(cam, o, 0, stream=None, p6_dev_ptr=p6.data_ptr())
             torch.cuda.synchronize()
             per.append((float(ds.frame_times(steps).mean()), float(ds.kernel_times(steps).mean())))

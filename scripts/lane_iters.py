@@ -27,6 +27,7 @@ from raytracinginonesemester_amd import _lib, configs  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3b")
 ap.add_argument("--out", default=str(REPO / "gpurun_out" / "lane_iters.json"))
+ap.add_argument("--band", default="", help="band shard r/n (8-row bands): only that rank's rows")
 a = ap.parse_args()
 cfg = configs.G_CONFIGS[a.config]
 sp = configs.scene_path(cfg["scene"])
@@ -37,7 +38,11 @@ lib = _lib.lib()
 lib.rt_debug_wave_times_set.argtypes = [C.c_void_p, C.c_void_p]
 lib.rt_debug_lane_iters_set.argtypes = [C.c_void_p, C.c_void_p]
 ds = rt.DeviceScene.from_host(hs)
-opts, _j = ds.make_opts(spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"])
+kw = {}
+if a.band:
+    r, n = (int(v) for v in a.band.split("/"))
+    kw = {"band_rows": 8, "band_index": r, "band_count": n}
+opts, _j = ds.make_opts(spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"], **kw)
 items = (W * H + 7) // 8 * 4  # bound for any tile shape (>= 8 pixels per tile), 4 waves per tile
 times = torch.zeros(items * 2, dtype=torch.int64, device="cuda")
 cuts = torch.full((items,), -1, dtype=torch.int32, device="cuda")
@@ -47,9 +52,9 @@ rgb = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
 assert lib.rt_debug_wave_times_set(C.c_void_p(times.data_ptr()), C.c_void_p(cuts.data_ptr())) == 0
 assert lib.rt_debug_lane_iters_set(C.c_void_p(iters.data_ptr()), C.c_void_p(acc.data_ptr())) == 0
 st = torch.cuda.current_stream().cuda_stream
-for _ in range(5):  # heavy-first costs settle
+for _ in range(5):  # heavy-first costs settle (each frame waited for: the threshold needs a finished one)
     ds.render_device(cam, opts, rgb.data_ptr(), stream=st)
-torch.cuda.synchronize()
+    torch.cuda.synchronize()
 times.zero_()
 iters.zero_()
 ds.render_device(cam, opts, rgb.data_ptr(), stream=st)
@@ -63,7 +68,7 @@ d = (e - s) * 10e-3  # us
 wsum, lmax, lsum, calls = it[live, 0], it[live, 1], it[live, 2], it[live, 3]
 order = np.argsort(-d)
 res = {
-    "config": a.config, "kernel_ms_event": kms, "items": int(len(live)),
+    "config": a.config, "band": a.band, "kernel_ms_event": kms, "heavy_tiles": ds.heavy_tiles(), "items": int(len(live)),
     "dur_us_pct": {p: round(float(np.percentile(d, p)), 1) for p in (50, 90, 99, 100)},
     "total_wsum": int(wsum.sum()), "total_lmax": int(lmax.sum()), "total_lsum": int(lsum.sum()),
     "corr_dur_wsum": round(float(np.corrcoef(d, wsum)[0, 1]), 3),

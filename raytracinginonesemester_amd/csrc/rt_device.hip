@@ -1013,6 +1013,235 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, con
 }
 
 
+// The paired-only kernels resume their per-lane traversals across calls (paired_bounces_resume;
+// c3b 1.425 vs 1.467 ms and 1.422 vs 1.501 in one process, frames identical).  -DRT_NO_RESUME
+// builds the plain paired loop into them for A/B.
+#ifndef RT_NO_RESUME
+#define RT_RESUME 1
+#endif
+#ifdef RT_RESUME
+#ifndef RT_RESUME_SHIFT
+#define RT_RESUME_SHIFT 2
+#endif
+// A per-lane DFS over the 4-ary records that a call can leave with lanes still
+// mid-traversal: their state stays in LaneDfs (and the LDS stack) and the next call resumes it.
+struct LaneDfs {
+    uint32_t ref;
+    int sp, stale;
+    bool retest, run;
+};
+__device__ __forceinline__ void dfs_start(const SceneView& sc, const RayPre& r, bool go, HitState& hs, LaneDfs& d) {
+    if (go) {
+        hs.bestT = FLT_MAX;
+        hs.slot = -1;
+        d.run = box_hit(r, own_box(sc, sc.root_ref, true), kRayTMin, FLT_MAX);  // the root's pop-time test
+        d.ref = sc.root_ref;
+        d.sp = 0;
+        d.stale = 0;
+        d.retest = false;
+    }
+}
+// Runs the lanes with d.run until at most `quota` of them still run (traverse_lane_lds_wide's
+// visits, one load batch each; the same tests in the same order: exact).
+__device__ __forceinline__ void dfs_run(const SceneView& sc, const RayPre& r, bool any_hit, float any_hit_dist,
+                                        HitState& hs, LaneDfs& d, uint32_t* stk, uint32_t quota) {
+    for (uint32_t guard = 0; guard < (1u << 22); ++guard) {
+        if ((uint32_t)__popcll(ballot(d.run)) <= quota) break;
+        if (d.run) {
+            RT_LI_STEP(hs);
+            const uint32_t ref = d.ref;
+            const bool leaf = (ref & LEAF_BIT) != 0;
+            const uint32_t idx = ref & ~LEAF_BIT;
+            const float4* R = leaf ? sc.leaf + 4 * (size_t)idx : sc.wnode + 8 * (size_t)idx;
+            const float4 w0 = R[0], w1 = R[1], w2 = R[2], w3 = R[3];
+            float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f), w5 = w4, w6 = w4;
+            if (!leaf) {
+                w4 = R[4];
+                w5 = R[5];
+                w6 = R[6];
+            }
+            const float* bp = leaf ? reinterpret_cast<const float*>(R + 2) + 2 : reinterpret_cast<const float*>(sc.ibox + 2 * (size_t)idx);
+            v2f bx = {0.f, 0.f}, by = bx, bz = bx;
+            if (d.retest) {
+                bx = *reinterpret_cast<const v2f*>(bp);
+                by = *reinterpret_cast<const v2f*>(bp + 2);
+                bz = *reinterpret_cast<const v2f*>(bp + 4);
+            }
+            const bool go = !d.retest || box_hit(r, BoxP{bx, by, bz}, kRayTMin, hs.bestT);
+            uint32_t next = NO_REF;
+            bool stop = false;
+            if (go) {
+                if (leaf) {
+                    float t, u, v;
+                    if (mt_g(r, mk(w0.x, w0.y, w0.z), mk(w1.x, w1.y, w1.z), mk(w1.w, w2.x, w2.y), kRayTMin, hs.bestT, t, u,
+                             v)) {
+                        hs.bestT = t;
+                        hs.slot = (int32_t)idx;
+                        d.stale = d.sp;
+                        if (any_hit && t < any_hit_dist) stop = true;
+                    }
+                } else {
+                    const float4 wv[7] = {w0, w1, w2, w3, w4, w5, w6};
+                    const uint32_t refs[4] = {__float_as_uint(w6.x), __float_as_uint(w6.y), __float_as_uint(w6.z),
+                                              __float_as_uint(w6.w)};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (refs[k] == NO_REF) continue;
+                        const float4 p = wv[(3 * k) / 2], q = wv[(3 * k) / 2 + 1];
+                        const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
+                        if (box_hit(r, bk, kRayTMin, hs.bestT)) {
+                            if (next != NO_REF) {
+                                stk[d.sp * BLOCK] = next;
+                                ++d.sp;
+                            }
+                            next = refs[k];
+                        }
+                    }
+                }
+            }
+            if (stop) {
+                d.run = false;
+            } else if (next != NO_REF) {
+                d.ref = next;
+                d.retest = false;
+            } else if (d.sp == 0) {
+                d.run = false;
+            } else {
+                --d.sp;
+                d.ref = stk[d.sp * BLOCK];
+                d.retest = d.sp < d.stale;
+                if (d.retest) d.stale = d.sp;
+            }
+        }
+    }
+}
+
+// paired_bounces with resumable per-lane traversals: a call returns once three quarters of its
+// running lanes are done; a pair (path lane l, shadow lane l + 32) whose two traversals have
+// ended is shaded and sent on at once, while the others resume in the next call.  Per sample the
+// same rays, tests, arithmetic and order of radiance adds as paired_bounces: exact.
+template <int MODE>
+__device__ __forceinline__ void paired_bounces_resume(const RenderParams& P, RayPre& ray, bool alive, f3& thr,
+                                                      f3& radiance, uint32_t& rng, float* park, HitState hs) {
+    const SceneView& sc = P.sc;
+    const bool upper = lane_id() >= 32;
+    const int max_depth = P.max_depth;
+    uint32_t* stk = reinterpret_cast<uint32_t*>(park);
+    LaneDfs d;
+    d.run = false;
+    d.ref = 0;
+    d.sp = d.stale = 0;
+    d.retest = false;
+    int depth = 0;                   // lower lanes: the depth of the path result in hs
+    bool unproc = !upper;            // lower lanes: hs holds a path result not yet shaded
+    bool need_up = false;            // upper lanes: tracing (or holding the answer of) a shadow ray
+    float dist_up = 0.f;
+    bool pend = false, lit_p = false;
+    f3 thr_p = mk(0.f, 0.f, 0.f), Lo_p = thr_p, Lo_lit_p = thr_p;
+    for (uint32_t guard = 0; guard < (1u << 16); ++guard) {
+        const uint64_t runm = ballot(d.run);
+        const bool ready = !upper && !d.run && !lane_in(runm >> 32);
+        const uint64_t readym = ballot(ready);
+        const bool pready = upper && lane_in(readym << 32);
+        // IsInShadow's answer (shader.h:44-62) of the upper lanes whose pair is ready
+        const uint64_t occ = ballot(pready && need_up && hs.slot >= 0 && hs.bestT < dist_up);
+        if (ready && pend) {
+            const bool occluded = lane_in(occ >> 32);
+            radiance = add(radiance, mul(thr_p, (lit_p && !occluded) ? Lo_lit_p : Lo_p));
+            pend = false;
+        }
+        if (pready) need_up = false;
+        bool need = false;
+        float dist = 0.f;
+        f3 so = mk(0.f, 0.f, 0.f), sd = so;
+        bool launch = false;  // lower lanes: a new path ray to trace
+        if (ready && unproc) {
+            unproc = false;
+            const bool hit = alive && hs.slot >= 0;
+            if (alive && !hit) {
+                radiance = add(radiance, mul(thr, P.miss));
+                alive = false;
+            }
+            if (hit) {
+                const SurfHit sh = resolve_hit<false>(sc, ray, hs.slot);
+                const DevMaterial m = material_of(sc, sh.tri);
+                const f3 N = unit(sh.n);
+                const f3 V = unit(sub(ray.o, sh.p));
+                f3 Lo = mk(0.f, 0.f, 0.f);
+                Lo = add(Lo, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 0.05f));
+                Lo = add(Lo, mk(m.emission[0], m.emission[1], m.emission[2]));
+                const DevLight& lt = sc.lights[0];
+                const f3 lpos = mk(lt.pos[0], lt.pos[1], lt.pos[2]);
+                f3 contrib = mk(0.f, 0.f, 0.f);
+                bool lit = false;
+                const f3 L = unit(sub(lpos, sh.p));
+                const float NdotL = fmaxf(dot(N, L), 0.0f);
+                if (NdotL > 0.0f) {
+                    const f3 f = eval_brdf(m, sh.n, V, L);
+                    const f3 rad = scale(mk(lt.color[0], lt.color[1], lt.color[2]), (float)lt.intensity);
+                    contrib = scale(mul(rad, f), NdotL);
+                    lit = true;
+                    const f3 toL = sub(lpos, sh.p);
+                    dist = sqrtf(dot(toL, toL));
+                    if (dist > 0.0f) {
+                        need = true;
+                        so = add(sh.p, scale(N, RT_EPS));
+                        sd = divf(toL, dist);
+                    }
+                }
+                thr_p = thr;
+                Lo_p = Lo;
+                Lo_lit_p = add(Lo, contrib);
+                lit_p = lit;
+                pend = true;
+                if (depth + 1 < max_depth) {
+                    const float kd = m.kd, kr = m.kr, total = kd + kr;
+                    if (total <= 0.0f) {
+                        alive = false;
+                    } else {
+                        const f3 Nb = unit(sh.n);
+                        const float xi = rng_next(rng);
+                        if (P.diffuse_bounce && xi < kd / total) {
+                            f3 dd = random_unit_vector(rng);
+                            if (!(dot(dd, Nb) > 0.0f)) dd = mk(-dd.x, -dd.y, -dd.z);
+                            ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), dd, scene_bmax(sc));
+                            const float nl = fmaxf(dot(Nb, dd), 0.0f);
+                            thr = mul(thr, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 2.0f * nl));
+                        } else {
+                            const f3 I = unit(ray.d);
+                            const f3 refl = sub(I, scale(Nb, 2.0f * dot(I, Nb)));
+                            ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), refl, scene_bmax(sc));
+                            thr = mul(thr, scale(mk(m.spec[0], m.spec[1], m.spec[2]), kr));
+                        }
+                        if (thr.x < 1e-4f && thr.y < 1e-4f && thr.z < 1e-4f) alive = false;
+                    }
+                    ++depth;
+                } else {
+                    alive = false;
+                }
+            }
+            launch = alive;
+        }
+        const uint64_t needm = ballot(need);
+        const float ox = __shfl_xor(so.x, 32), oy = __shfl_xor(so.y, 32), oz = __shfl_xor(so.z, 32);
+        const float dx = __shfl_xor(sd.x, 32), dy = __shfl_xor(sd.y, 32), dz = __shfl_xor(sd.z, 32);
+        const float dd = __shfl_xor(dist, 32);
+        bool go = launch;
+        if (pready) {
+            need_up = lane_in(needm << 32);
+            dist_up = dd;
+            if (need_up) ray = make_ray(mk(ox, oy, oz), mk(dx, dy, dz), scene_bmax(sc));
+            go = need_up;
+        }
+        dfs_start(sc, ray, go, hs, d);
+        if (launch) unproc = true;
+        if (ballot(d.run || pend || unproc) == 0) break;
+        const uint32_t quota = (uint32_t)__popcll(ballot(d.run)) >> RT_RESUME_SHIFT;
+        dfs_run(sc, ray, upper, dist_up, hs, d, stk, quota);
+    }
+}
+#endif
+
 // TraceRayIterative (query.h:156-220) from the camera ray's hit on, for half waves over one
 // light, the lanes in pairs: a sample's path lives in lane l < 32 (the lanes that trace in a half
 // wave), and lane l + 32, otherwise idle, traces that path's shadow rays.  The bounce direction
@@ -1183,7 +1412,12 @@ __device__ __forceinline__ f3 trace_sample(const RenderParams& P, bool valid, in
                 P.hit_idx[aov] = hit ? leaf_tri<false>(sc, hs.slot) : -1;
                 P.hit_t[aov] = hit ? hs.bestT : -1.0f;
             }
-            paired_bounces<MODE>(P, ray, alive, thr, radiance, rng, park, hs);
+#ifdef RT_RESUME
+            if constexpr ((MODE & MODE_WIDE) != 0 && PAIR == 2)
+                paired_bounces_resume<MODE>(P, ray, alive, thr, radiance, rng, park, hs);
+            else
+#endif
+                paired_bounces<MODE>(P, ray, alive, thr, radiance, rng, park, hs);
             return clamp01(radiance);
         }
     }

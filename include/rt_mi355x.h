@@ -431,6 +431,10 @@ int rt_heavy_tiles(const rt_scene* s, int64_t* heavy);
 int rt_device_count(int* n);
 const char* rt_last_error(void);
 int rt_abi_version(void);
+/* sha256 (hex) of the csrc/ and include/ sources and compile flags this library was built from
+ * (raytracinginonesemester_amd/build.py: source_build_id), so a caller can prove which sources
+ * the loaded binary came from. */
+const char* rt_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -172,6 +172,7 @@ SIGNATURES = {
     "rt_device_count": (I, [P]),
     "rt_last_error": (C.c_char_p, []),
     "rt_abi_version": (I, []),
+    "rt_build_id": (C.c_char_p, []),
 }
 
 _lib = None

@@ -1042,7 +1042,8 @@ __device__ __forceinline__ void dfs_start(const SceneView& sc, const RayPre& r, 
     }
 }
 // Runs the lanes with d.run until at most `quota` of them still run (traverse_lane_lds_wide's
-// visits, one load batch each; the same tests in the same order: exact).
+// visits, one load batch each; the same tests in the same order: exact).  The guard only ends a
+// call, never a traversal: lanes still running resume in the caller's next call.
 __device__ __forceinline__ void dfs_run(const SceneView& sc, const RayPre& r, bool any_hit, float any_hit_dist,
                                         HitState& hs, LaneDfs& d, uint32_t* stk, uint32_t quota) {
     for (uint32_t guard = 0; guard < (1u << 22); ++guard) {
@@ -1138,6 +1139,10 @@ __device__ __forceinline__ void paired_bounces_resume(const RenderParams& P, Ray
     float dist_up = 0.f;
     bool pend = false, lit_p = false;
     f3 thr_p = mk(0.f, 0.f, 0.f), Lo_p = thr_p, Lo_lit_p = thr_p;
+    // Every call ends at least one lane's traversal and a path has at most max_depth rays, so
+    // the loop ends long before the guard; should the guard ever run out, the sample is
+    // poisoned (NaN) rather than silently truncated, so no parity test can pass over it.
+    bool finished = false;
     for (uint32_t guard = 0; guard < (1u << 16); ++guard) {
         const uint64_t runm = ballot(d.run);
         const bool ready = !upper && !d.run && !lane_in(runm >> 32);
@@ -1235,10 +1240,14 @@ __device__ __forceinline__ void paired_bounces_resume(const RenderParams& P, Ray
         }
         dfs_start(sc, ray, go, hs, d);
         if (launch) unproc = true;
-        if (ballot(d.run || pend || unproc) == 0) break;
+        if (ballot(d.run || pend || unproc) == 0) {
+            finished = true;
+            break;
+        }
         const uint32_t quota = (uint32_t)__popcll(ballot(d.run)) >> RT_RESUME_SHIFT;
         dfs_run(sc, ray, upper, dist_up, hs, d, stk, quota);
     }
+    if (!finished) radiance = mk(__int_as_float(0x7fc00000), 0.f, 0.f);
 }
 #endif
 

@@ -350,6 +350,16 @@ struct rt_renderer {
     RankPool pool;  // in-process renderers over several GPUs: per-rank submission threads
 
     ~rt_renderer() { release(); }
+    // HOST_SHARED, after this process's copy streams were synchronised: publish every frame its
+    // ranks copied, so rank 0 never waits on a frame whose "done" word only a wait would write
+    // (a rank that resizes or closes without waiting its last tickets).
+    void publish_copied() {
+        if (!shared) return;
+        uint64_t last = 0;
+        for (uint64_t t : slot_ticket) last = std::max(last, t);
+        if (last == 0) return;
+        for (const LocalRank& L : ranks) SharedFrames::raise_to(shared->done(L.rank), last);
+    }
     void release_buffers() {
         if (!shared) {
             for (void* h : host)
@@ -372,6 +382,7 @@ struct rt_renderer {
             if (L.comm) (void)hipStreamSynchronize(L.comm);
             if (L.copy) (void)hipStreamSynchronize(L.copy);
         }
+        publish_copied();
         release_buffers();
         for (LocalRank& L : ranks) {
             DeviceGuard g(L.device);
@@ -547,6 +558,7 @@ int ensure_geometry(rt_renderer* r, int W, int H) {
         HIP_TRY(hipStreamSynchronize(L.comm));
         HIP_TRY(hipStreamSynchronize(L.copy));
     }
+    r->publish_copied();
     r->release_buffers();
     r->first_valid = r->next;
     r->W = W;
@@ -640,12 +652,17 @@ extern "C" int rt_renderer_create(size_t P, const rt_bvh_node* nodes, const rt_a
     const bool named = o->host_frame_name && o->host_frame_name[0];
     int gather = o->gather;
     if (gather == RT_GATHER_AUTO) {
-        if (world == n) gather = RT_GATHER_DIRECT;
+        // one process over distinct GPUs delivering into rank 0's HBM: RCCL over xGMI rather
+        // than cross-device 2-D copies
+        if (world == n) gather = (o->deliver == RT_DELIVER_DEVICE && n > 1 && distinct) ? RT_GATHER_RCCL : RT_GATHER_DIRECT;
         else gather = named ? RT_GATHER_HOST_SHARED : RT_GATHER_RCCL;
     }
     if ((o->flags & RT_RENDERER_SELF_SEND) && o->gather == RT_GATHER_AUTO) gather = RT_GATHER_RCCL;
     if (gather == RT_GATHER_DIRECT && world > n)
         return set_error(RT_ERR_UNSUPPORTED, "RT_GATHER_DIRECT needs every rank in this process");
+    if (gather == RT_GATHER_RCCL && world > n && !o->unique_id)
+        return set_error(RT_ERR_ARG, "RCCL across processes needs unique_id (rt_comm_unique_id on rank 0, shared with "
+                                     "every process); or name a host_frame_name for RT_GATHER_HOST_SHARED");
     if (gather == RT_GATHER_RCCL && !distinct)
         return set_error(RT_ERR_UNSUPPORTED, "RCCL needs one rank per device; use RT_GATHER_DIRECT for repeated ids");
     if (gather == RT_GATHER_HOST_SHARED) {
@@ -681,9 +698,6 @@ extern "C" int rt_renderer_create(size_t P, const rt_bvh_node* nodes, const rt_a
         if (i == 0) rc = rt_scene_create(L.device, P, nodes, aabbs, tris, objids, mats, nmat, lights, nlights, &L.scene);
         else rc = rt_scene_clone(r->ranks[0].scene, L.device, &L.scene);
         if (rc != RT_OK) return rc;
-        // the renderer waits for buffer reuse on the host: its frames skip the scene's wait for
-        // work queued before them on the compute stream (there is none but its own frames)
-        rt::scene_set_caller_ordered(L.scene, true);
         HIP_TRY(hipStreamCreateWithFlags(&L.compute, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&L.comm, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking));
@@ -761,8 +775,13 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
             o.band_index = L.rank;
             o.band_count = r->world;
             void* buf = L.strip[s].p;
+            // the renderer waits for buffer reuse on the host: its own frames skip the scene's
+            // wait for work queued before them on the compute stream (there is none but its
+            // frames).  Only for this call: a borrowed view (rt_renderer_scene) stays stream-ordered.
+            rt::scene_set_caller_ordered(L.scene, true);
             int q = rt_render_device_p6(L.scene, cam, &o, f32 ? static_cast<float*>(buf) : nullptr, nullptr, nullptr,
                                         f32 ? nullptr : static_cast<uint8_t*>(buf), L.compute);
+            rt::scene_set_caller_ordered(L.scene, false);
             if (q != RT_OK) return q;
             hipEvent_t first = nullptr;
             rt::scene_frame_events(L.scene, &first, &L.rendered[s]);

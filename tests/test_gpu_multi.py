@@ -117,7 +117,7 @@ def test_bench_failed_rccl_is_not_silent():
 
 
 # ---- the shared host frame between processes ----------------------------------------------
-def _shared_worker(rank, world, port, name, depth, q):
+def _shared_worker(rank, world, port, name, depth, q, others_wait=True):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RT_PEER_TIMEOUT_S="60")
@@ -137,6 +137,8 @@ def _shared_worker(rank, world, port, name, depth, q):
             last = k + 1 == len(seq) or seq[k + 1] // 2 != c // 2
             while pend and (len(pend) >= depth or last):
                 kk, t = pend.pop(0)
+                if rank != 0 and not others_wait:
+                    continue  # rank 1 never waits: its resize and close must publish its copies
                 addr, n = r.wait(t)
                 if rank == 0:
                     got.append((kk, bytes((C.c_uint8 * n).from_address(addr))))
@@ -148,8 +150,11 @@ def _shared_worker(rank, world, port, name, depth, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("depth", [2, 3])
-def test_shared_host_frame_two_processes(depth):
+@pytest.mark.parametrize("depth,others_wait", [(2, True), (3, True), (2, False)])
+def test_shared_host_frame_two_processes(depth, others_wait):
+    """Two processes, one rank each, into the shared host frame.  others_wait=False: rank 1
+    never calls wait (the header gives non-zero ranks nothing to wait for); its copies reach
+    rank 0 through the slot reuse, the resize and close alone."""
     hs = host_scene("frog.json")
     ds = rt.DeviceScene.from_host(hs, device=0)
     cams = [hs.camera(W, H), _moved(hs.camera(W, H)), hs.camera(320, 180)]
@@ -161,8 +166,8 @@ def test_shared_host_frame_two_processes(depth):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    name = f"/rt_test_{os.getpid()}_{depth}"
-    procs = [ctx.Process(target=_shared_worker, args=(rk, 2, port, name, depth, q)) for rk in range(2)]
+    name = f"/rt_test_{os.getpid()}_{depth}_{int(others_wait)}"
+    procs = [ctx.Process(target=_shared_worker, args=(rk, 2, port, name, depth, q, others_wait)) for rk in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=300)

@@ -174,13 +174,38 @@ def test_reference_signature_multi_gpu(frog, golden):
     rt.render(frog.num_triangles, W, H, cam, frog.settings["miss_color"], 1, SPP, frog.nodes, frog.aabbs,
               frog.triangles, frog.tri_object_ids, mats, len(mats), frog.lights, len(frog.lights), True, out)
     assert out.view(np.uint32).tobytes() == golden[0].view(np.uint32).tobytes()
+
+
+def test_reference_signature_distinct_gpus(frog, golden):
+    """rt_render_reference_gpus over up to 8 distinct GPUs (RCCL-free direct delivery, one
+    process) equals the reference frame.  Skipped, visibly, on a box with one GPU."""
     dev = rt.device_count()
-    if dev >= 2:
-        out2 = np.zeros_like(out)
-        rt.render(frog.num_triangles, W, H, cam, frog.settings["miss_color"], 1, SPP, frog.nodes, frog.aabbs,
-                  frog.triangles, frog.tri_object_ids, mats, len(mats), frog.lights, len(frog.lights), True, out2,
-                  n_gpus=min(dev, 8))
-        assert out2.view(np.uint32).tobytes() == out.view(np.uint32).tobytes()
+    if dev < 2:
+        pytest.skip("needs >= 2 GPUs (this box has %d)" % dev)
+    cam = frog.camera(W, H)
+    mats = frog.materials
+    out = np.zeros(W * H * 3, np.float32)
+    rt.render(frog.num_triangles, W, H, cam, frog.settings["miss_color"], 1, SPP, frog.nodes, frog.aabbs,
+              frog.triangles, frog.tri_object_ids, mats, len(mats), frog.lights, len(frog.lights), True, out,
+              n_gpus=min(dev, 8))
+    assert out.view(np.uint32).tobytes() == golden[0].view(np.uint32).tobytes()
+
+
+def test_rccl_gather_distinct_gpus(frog, golden):
+    """The RCCL strip gather over xGMI between distinct GPUs of one process (ncclCommInitAll),
+    P6 and device delivery: the reference frame.  Skipped, visibly, on a box with one GPU."""
+    dev = rt.device_count()
+    if dev < 2:
+        pytest.skip("needs >= 2 GPUs (this box has %d)" % dev)
+    cam = frog.camera(W, H)
+    for deliver, want in ((rt.RT_DELIVER_F32, golden[0]), (rt.RT_DELIVER_P6, golden[1]),
+                          (rt.RT_DELIVER_DEVICE, golden[1])):
+        r = rt.Renderer.from_host(frog, devices=tuple(range(min(dev, 8))), gather=rt.RT_GATHER_RCCL, deliver=deliver)
+        try:
+            got = r.render(cam, spp=SPP, max_depth=1, miss_color=frog.settings["miss_color"])
+            assert np.asarray(got).tobytes() == want.tobytes(), deliver
+        finally:
+            r.close()
 
 
 def test_scene_frames_on_two_streams(frog, golden):

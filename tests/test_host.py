@@ -195,3 +195,23 @@ def test_p6_header_matches_writer_and_device_epilogue_checks_arguments():
         rt.unpermute_strips_device(16, 2, 60, 16, 8, 4, 0)
     with pytest.raises(rt.RTError):  # 16 rows over 4 ranks of 4-row bands need 4 rows per strip
         rt.unpermute_strips_device(16, 3, 60, 16, 4, 4, 32)
+
+
+def test_renderer_multiprocess_rccl_needs_unique_id():
+    """A multi-process renderer that resolves to RCCL (explicitly, or AUTO without a shared host
+    frame name) but has no unique_id is refused with RT_ERR_ARG before any device is touched
+    (it used to read the id through a null pointer)."""
+    hs = host_scene("frog.json")
+    for gather in (rt.RT_GATHER_RCCL, rt.RT_GATHER_AUTO):
+        with pytest.raises(rt.RTError, match="unique_id") as e:
+            rt.Renderer.from_host(hs, devices=(0,), world_size=2, rank0=1, gather=gather)
+        assert e.value.code == -1
+
+
+def test_loaded_library_is_built_from_these_sources():
+    """rt_build_id() of the loaded librt_mi355x.so is the sha256 of csrc/ + include/ + flags:
+    a stale prebuilt library cannot pass for the current sources."""
+    from raytracinginonesemester_amd import build as b
+
+    lib = _lib.lib()
+    assert lib.rt_build_id().decode() == b.source_build_id() == b.library_build_id()

@@ -355,6 +355,7 @@ def native(a, hs, cam, cfg, ctx):
     sc = r.scene(0)
     res = {"elapsed": elapsed, "kernel_ms": max(kts), "frame_ms": max(fts), "prepass_ms": max(pts),
            "kernel_ms_local": kts, "live_tiles": list(sc.live_tiles()), "heavy_tiles": sc.heavy_tiles(),
+           "kernel_instance": sc.kernel_name(),
            "gather_path": GATHER_NAMES[gather], "warmup_frames_run": warm_run, "gather_note": gather_note}
     if ctx.rank == 0:
         g, d, f = (r.times(k, a.steps) for k in (rt.RT_TIME_GATHER, rt.RT_TIME_DELIVER, rt.RT_TIME_FRAME))
@@ -523,11 +524,15 @@ def torch_path(a, hs, cam, cfg, world, rank, local, dev):
     return res
 
 
-def load_traffic(path: Path, config: str):
+def load_traffic(path: Path, config: str, instance: str):
+    """The measured per-launch traffic of this config's render kernel, only if it was profiled on
+    the same kernel instantiation the timed frames launched (profiles/traffic.json records the
+    instantiation rocprofv3 named); otherwise None: a line never cites another kernel's bytes."""
     try:
-        return json.loads(path.read_text()).get(config)
+        tr = json.loads(path.read_text()).get(config)
     except Exception:
         return None
+    return tr if tr and instance and tr.get("kernel_instance") == instance else None
 
 
 def primary_hit_parity(ds, cam, cfg, hs, golden: str) -> dict:
@@ -619,6 +624,12 @@ def main():
         vals.append(res["other_payload"]["s"])
     m = ctx.max(vals)
     elapsed, kernel_ms, frame_ms = m[0], m[1], m[2]
+    per_rank = None
+    if ctx.multiproc:  # every rank's own kernel / frame ms, to set beside the one-GPU shard estimates
+        mine = {"rank": rank, "device": ctx.devices[0], "kernel_ms": round(res["kernel_ms"], 4),
+                "frame_ms": round(res["frame_ms"], 4), "elapsed_s": round(res["elapsed"], 6)}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     shards = lbvh = None
     if world == 1 and not a.no_extras and comm == "native":
         shards = band_shards(hs, cam, cfg, ctx.devices[0])
@@ -662,10 +673,12 @@ def main():
         line["config"]["gather_note"] = res["gather_note"]
     per_gpu_samples = samples / world
     bps = configs.BYTES_PER_SAMPLE.get(a.config)
-    tr = load_traffic(Path(a.traffic_file), a.config) if world == 1 else None
+    instance = res.get("kernel_instance")
+    tr = load_traffic(Path(a.traffic_file), a.config, instance) if world == 1 else None
     traffic = tr.get("bytes_per_launch") if tr else None
     roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": traffic,
-            "kernel": "render_tiles_kernel", "kernel_ms": round(kernel_ms, 4), "frame_ms": round(frame_ms, 4)}
+            "kernel": instance or "render_tiles_kernel", "kernel_ms": round(kernel_ms, 4),
+            "frame_ms": round(frame_ms, 4)}
     if traffic:
         ach = traffic / (kernel_ms / 1e3) / 1e9
         roof.update(achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
@@ -675,7 +688,8 @@ def main():
             roof["compulsory_bytes_per_launch"] = tr["compulsory_bytes_per_launch"]
             roof["compulsory_GBps"] = round(tr["compulsory_bytes_per_launch"] / (kernel_ms / 1e3) / 1e9, 2)
     else:
-        roof.update(achieved=None, frac=None, achieved_from="no PMC traffic for this launch shape")
+        roof.update(achieved=None, frac=None,
+                    achieved_from=f"no PMC traffic profiled for {instance} on {a.config} (profiles/traffic.json)")
     if bps:
         roof["reference_equivalent_GBps"] = round(bps * per_gpu_samples / (kernel_ms / 1e3) / 1e9, 2)
         roof["reference_equivalent_note"] = (f"SURVEY.md §8(d) reference-layout model, {bps:.2f} B/sample: the "
@@ -712,6 +726,8 @@ def main():
             extra[k] = round(res[k], 4)
     if len(res.get("kernel_ms_local", [])) > 1:
         extra["kernel_ms_per_local_rank"] = [round(x, 4) for x in res["kernel_ms_local"]]
+    if per_rank:
+        extra["per_rank"] = per_rank
     if "render_only_s" in res:
         extra["render_only_value"] = round(samples * a.steps / m[3] / 1e6, 3)
         op = res["other_payload"]

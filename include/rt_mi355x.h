@@ -427,6 +427,10 @@ int rt_live_tiles(const rt_scene* s, int64_t* live, int64_t* total);
  * dispatch: tiles whose waves took >= 1/4 of the previous finished frame's render kernel in the
  * last frame that rendered them; their order only, never their pixels).  Waits for that call. */
 int rt_heavy_tiles(const rt_scene* s, int64_t* heavy);
+/* The render kernel instantiation the most recent rt_render_device call launched, as rocprofv3
+ * names it ("render_tiles_kernel<49, true, true, 7, 0>"; "" before the first frame): bench.py
+ * keys its measured per-launch HBM traffic by it. */
+const char* rt_scene_kernel_name(const rt_scene* s);
 
 int rt_device_count(int* n);
 const char* rt_last_error(void);

@@ -169,6 +169,7 @@ SIGNATURES = {
     "rt_prepass_times": (I, [P, P, I, P]),
     "rt_live_tiles": (I, [P, P, P]),
     "rt_heavy_tiles": (I, [P, P]),
+    "rt_scene_kernel_name": (C.c_char_p, [P]),
     "rt_device_count": (I, [P]),
     "rt_last_error": (C.c_char_p, []),
     "rt_abi_version": (I, []),

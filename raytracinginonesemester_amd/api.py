@@ -302,6 +302,10 @@ class DeviceScene:
         check(lib().rt_live_tiles(self._handle(), C.byref(live), C.byref(total)))
         return live.value, total.value
 
+    def kernel_name(self) -> str:
+        """The render kernel instantiation of the most recent frame, as rocprofv3 names it."""
+        return lib().rt_scene_kernel_name(self._handle()).decode()
+
     def heavy_tiles(self) -> int:
         """Tiles the most recent render dispatched first (heavy-first order, speed only)."""
         n = C.c_int64()

@@ -2694,6 +2694,7 @@ using rt::DeviceGuard;
 
 struct rt_scene {
     int device = 0;
+    const char* last_kernel = nullptr;  // the render kernel instantiation of the latest frame
     size_t P = 0;
     int nmat = 0, nlights = 0;
     uint32_t root_ref = 0;
@@ -3145,14 +3146,20 @@ struct Launch {
     hipEvent_t start, stop;
     int cus;
     bool big;  // scene data beyond kBigSceneBytes: the depth-1 wave kernels at RT_RENDER_WAVES_BIG
+    const char** name;  // out: the launched instantiation, as rocprofv3 names it (rt_scene_kernel_name)
 };
-template <auto KERNEL>
+template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0>
 void launch_render(const RenderParams& P, const Launch& L) {
+    constexpr auto KERNEL = render_tiles_kernel<MODE, SAMPLES, D1, WAVES, LS>;
     static const int per_cu = [] {
         int n = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, KERNEL, BLOCK, 0) != hipSuccess || n < 1) n = 1;
         return n;
     }();
+    static const std::string name = "render_tiles_kernel<" + std::to_string(MODE) + (SAMPLES ? ", true" : ", false") +
+                                    (D1 ? ", true, " : ", false, ") + std::to_string(WAVES) + ", " +
+                                    std::to_string(LS) + ">";
+    if (L.name) *L.name = name.c_str();
     const int tiles8 = (P.tiles_total + 7) / 8 * 8;
     const dim3 grid((unsigned)std::max(8, std::min(tiles8, L.cus * per_cu / 8 * 8)));
     hipExtLaunchKernelGGL(KERNEL, grid, dim3(BLOCK), 0, L.st, L.start, L.stop, 0, P);
@@ -3165,31 +3172,31 @@ void launch_mode(const RenderParams& P, const Launch& L) {
     if (P.max_depth == 1) {
         if constexpr (SAMPLES) {
             if (P.half_waves) {
-                launch_render<render_tiles_kernel<D1_MODE, SAMPLES, true, RT_RENDER_WAVES, 1>>(P, L);
+                launch_render<D1_MODE, SAMPLES, true, RT_RENDER_WAVES, 1>(P, L);
                 return;
             }
         }
         if constexpr ((MODE & (MODE_DEEP | RT_KERNEL_LANE)) == 0) {
             if (L.big) {
-                launch_render<render_tiles_kernel<D1_MODE, SAMPLES, true, RT_RENDER_WAVES_BIG>>(P, L);
+                launch_render<D1_MODE, SAMPLES, true, RT_RENDER_WAVES_BIG>(P, L);
                 return;
             }
         }
-        launch_render<render_tiles_kernel<D1_MODE, SAMPLES, true>>(P, L);
+        launch_render<D1_MODE, SAMPLES, true>(P, L);
     } else {
         if constexpr (SAMPLES && (MODE & (MODE_DEEP | RT_KERNEL_LANE)) == 0) {
             if (P.half_waves && P.paired_only) {
-                launch_render<render_tiles_kernel<MODE, SAMPLES, false, RT_PAIRED_WAVES, 3>>(P, L);
+                launch_render<MODE, SAMPLES, false, RT_PAIRED_WAVES, 3>(P, L);
                 return;
             }
         }
         if constexpr (SAMPLES) {
             if (P.half_waves) {
-                launch_render<render_tiles_kernel<MODE, SAMPLES, false, RT_BOUNCE_WAVES, 1>>(P, L);
+                launch_render<MODE, SAMPLES, false, RT_BOUNCE_WAVES, 1>(P, L);
                 return;
             }
         }
-        launch_render<render_tiles_kernel<MODE, SAMPLES, false, RT_BOUNCE_WAVES>>(P, L);
+        launch_render<MODE, SAMPLES, false, RT_BOUNCE_WAVES>(P, L);
     }
 }
 
@@ -3505,7 +3512,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             const char* e = std::getenv("RT_BIG_SCENE_BYTES");
             return e ? (size_t)std::strtoull(e, nullptr, 10) : kBigSceneBytes;
         }();
-        const Launch L{st, s->evm[slot], s->ev1[slot], s->cus, s->bytes > big_bytes};
+        const Launch L{st, s->evm[slot], s->ev1[slot], s->cus, s->bytes > big_bytes, &s->last_kernel};
         if (s->deep) launch<MODE_DEEP>(P, samples, L);
         else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, L);
         else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, L);
@@ -3585,6 +3592,10 @@ int live_tiles(const rt_scene* s, int64_t* live, int64_t* heavy, int64_t* total)
 
 extern "C" int rt_live_tiles(const rt_scene* s, int64_t* live, int64_t* total) {
     return live_tiles(s, live, nullptr, total);
+}
+
+extern "C" const char* rt_scene_kernel_name(const rt_scene* s) {
+    return (s && s->last_kernel) ? s->last_kernel : "";
 }
 
 extern "C" int rt_heavy_tiles(const rt_scene* s, int64_t* heavy) {

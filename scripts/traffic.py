@@ -35,11 +35,17 @@ def short(name):
     return name[:40]
 
 
+import re
+
+instances = collections.Counter()  # render-kernel instantiations seen in the profile (launches)
 pmc = collections.defaultdict(lambda: collections.defaultdict(list))
 for p in sorted(glob.glob(os.path.join(a.prof, "*", "*counter_collection.csv"))):
     per = collections.defaultdict(lambda: collections.defaultdict(float))  # (kernel, dispatch) -> counter sums
     for r in csv.DictReader(open(p)):
         per[(short(r["Kernel_Name"]), int(r["Dispatch_Id"]))][r["Counter_Name"]] += float(r["Counter_Value"])
+        m = re.search(re.escape(a.kernel) + r"<[^>]*>", r["Kernel_Name"])
+        if m:
+            instances[(m.group(0), int(r["Dispatch_Id"]))] += 1
     seen = collections.Counter()
     for (kn, _d), cs in sorted(per.items(), key=lambda kv: kv[0][1]):
         seen[kn] += 1
@@ -119,12 +125,16 @@ def binding(i):
             f"rate before the stack's v_readlane/v_writelane, which share it), VALU issue "
             f"{i['valu_issue']:.2f}; waves waiting {i['wait_any']:.2f} of their cycles at "
             f"{i['waves_per_simd']:.1f} waves/SIMD")
+names = {n for n, _ in instances}
+if len(names) > 1:
+    raise SystemExit(f"{a.prof}: several {a.kernel} instantiations {sorted(names)}: profile one per run")
+instance = names.pop() if names else None
 if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
     fetch = 2 * k["FETCH_SIZE"] * 1024
     write = k["WRITE_SIZE"] * 1024
     tf = REPO / "profiles" / "traffic.json"
     data = json.loads(tf.read_text()) if tf.exists() else {}
-    data[a.config] = {"kernel": a.kernel, "bytes_per_launch": round(fetch + write),
+    data[a.config] = {"kernel": a.kernel, "kernel_instance": instance, "bytes_per_launch": round(fetch + write),
                       "fetch_bytes": round(fetch), "write_bytes": round(write),
                       "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
                                 f"{os.path.basename(a.prof.rstrip('/'))}; FETCH_SIZE x2 (gfx950), KiB->B"}

@@ -3482,12 +3482,20 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.heavy_tiles = reinterpret_cast<int32_t*>(lists + list_bytes + cut_bytes);
     const int slot = int(k % rt_scene::kRing);
     // From the cull launch on, a failure leaves the counter sets unknown (counters_dirty).
+    static const bool same_stream = [] {
+        const char* e = std::getenv("RT_PREP_SAME_STREAM");
+        return e && std::atoi(e) != 0;
+    }();
+    static const int cut_per_cu = [] {
+        const char* e = std::getenv("RT_CUT_BLOCKS_PER_CU");
+        return e ? std::max(1, std::atoi(e)) : 4;
+    }();
     auto frame = [&]() -> int {
-        hipStream_t pp = s->prep;
+        hipStream_t pp = same_stream ? st : s->prep;
         // set k was last read by frame k-3, set k+1 (zeroed by this cull pass) by frame k-2
-        if (k >= 2) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 2), 0));
-        if (k >= 1 && overlap) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 1), 0));
-        if (!s->caller_ordered) {  // stream order for the caller's buffers (see rt_scene::evq)
+        if (k >= 2 && !same_stream) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 2), 0));
+        if (k >= 1 && overlap && !same_stream) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 1), 0));
+        if (!s->caller_ordered && !same_stream) {  // stream order for the caller's buffers (see rt_scene::evq)
             HIP_TRY(hipEventRecord(s->evq[slot], st));
             HIP_TRY(hipStreamWaitEvent(pp, s->evq[slot], 0));
         }
@@ -3503,11 +3511,11 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         HIP_TRY(hipGetLastError());
         if (cut) {
             // 16 waves per CU; each takes (list, group) pairs grid-stride (c3: about one each)
-            const int cut_blocks = 4 * s->cus;
+            const int cut_blocks = cut_per_cu * s->cus;
             hipExtLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, pp, nullptr, s->pdone[slot], 0, P);
             HIP_TRY(hipGetLastError());
         }
-        HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
+        if (!same_stream) HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
         static const size_t big_bytes = [] {
             const char* e = std::getenv("RT_BIG_SCENE_BYTES");
             return e ? (size_t)std::strtoull(e, nullptr, 10) : kBigSceneBytes;

@@ -18,6 +18,6 @@ fi
     -mcode-object-version=5 -Wno-unused-function "$@" -I"$ROOT/include" -I"$ROOT/raytracinginonesemester_amd/csrc" \
     -c -x hip "$SRC" -o "$OUT/rt_device.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$ROOT/build/obj/rt_host.o" "$OUT/rt_device.o" \
-    "$ROOT/build/obj/rt_frame.o" "$ROOT/build/obj/rt_lbvh.o" "$ROOT/build/obj/rt_renderer.o" \
+    "$ROOT/build/obj/rt_frame.o" "$ROOT/build/obj/rt_lbvh.o" "$ROOT/build/obj/rt_renderer.o" "$ROOT/build/obj/rt_build_id.o" \
     -o "$OUT/librt_mi355x.so"
 echo "$OUT/librt_mi355x.so"

@@ -411,7 +411,7 @@ def rccl_leg(a, hs, cam, cfg, ctx) -> dict:
             if dl == rt.RT_DELIVER_P6 and a.config in GOLDEN_FULL:
                 addr, n = last
                 body = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_uint8 * n).from_address(addr)).tobytes()
-                d["ppm_identical"] = rt.p6_header(cam.pixel_width, cam.pixel_height) + body == golden_ppm(a.config)
+                d["ppm_identical"] = ppm_matches_golden(a.config, rt.p6_header(cam.pixel_width, cam.pixel_height) + body)
         rr.close()
         out[name] = d
     return out
@@ -550,11 +550,23 @@ def primary_hit_parity(ds, cam, cfg, hs, golden: str) -> dict:
             "samples_hit": int((hi >= 0).sum())}
 
 
-GOLDEN_FULL = {"c3": "c3_full", "c3b": "c3b_full"}  # reference outputs of the full bench frame
+# reference outputs of the full bench frame (sphere, sphere_single: sha256 of the outputs only)
+GOLDEN_FULL = {"c3": "c3_full", "c3b": "c3b_full", "sphere": "sphere_full", "sphere_single": "sphere_single_full"}
 
 
-def golden_ppm(config: str) -> bytes:
-    return gzip.open(REPO / "tests" / "golden" / "scenes" / GOLDEN_FULL[config] / "image.ppm.gz").read()
+def golden_ppm(config: str) -> bytes | None:
+    p = REPO / "tests" / "golden" / "scenes" / GOLDEN_FULL[config] / "image.ppm.gz"
+    return gzip.open(p).read() if p.exists() else None
+
+
+def golden_ppm_sha(config: str) -> str:
+    meta = json.loads((REPO / "tests" / "golden" / "scenes" / GOLDEN_FULL[config] / "meta.json").read_text())
+    return meta["sha256"]["image.ppm"]
+
+
+def ppm_matches_golden(config: str, ppm: bytes) -> bool:
+    g = golden_ppm(config)
+    return ppm == g if g is not None else hashlib.sha256(ppm).hexdigest() == golden_ppm_sha(config)
 
 
 def lbvh_times(hs, device: int, reps: int = 5) -> dict:
@@ -650,14 +662,18 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32+f64",
-        "data": "synthetic=false: frog.obj scene (reference asset), camera/light from frog.json"
-                if a.config in ("c3", "c3b") else "synthetic seeded 1,048,576-triangle heightfield",
+        "data": ("synthetic seeded 1,048,576-triangle heightfield" if a.config == "c5" else
+                 "synthetic=false: this repo's two-light scene over the reference's cornellbox.obj"
+                 if a.config == "cornell" else
+                 f"synthetic=false: {cfg['scene']} as the reference ships it (meshes and scene JSON are reference assets)"),
     }
     gpath = res["gather_path"]
     line["config"] = {
         "workload": f"{a.config if world == 1 or a.config != 'c3' else 'c4'}: {cfg['scene']} {W}x{H}x{spp}spp "
-                    f"max_bounces={cfg['max_depth']}" + (", diffuse bounces" if cfg["max_depth"] > 1 else "")
-                    + ", Lambert/Blinn-Phong + 1 hard shadow ray per light",
+                    f"max_bounces={cfg['max_depth']}"
+                    + ((", diffuse bounces" if hs.settings["diffuse_bounce"] else ", mirror bounces")
+                       if cfg["max_depth"] > 1 else "")
+                    + f", Lambert/Blinn-Phong + 1 hard shadow ray per light ({len(hs.lights)} light(s))",
         "triangles": hs.num_triangles, "bands": f"{BAND_ROWS}-row bands round-robin over {world} GPU(s)",
         "processes": world if ctx.multiproc else 1,
         "devices": "one per process" if ctx.multiproc else list(ctx.devices),
@@ -746,17 +762,24 @@ def main():
 
     if not a.no_parity and a.config in GOLDEN_FULL and rank == 0:
         gdir = REPO / "tests" / "golden" / "scenes" / GOLDEN_FULL[a.config]
-        ref = np.frombuffer(gzip.open(gdir / "fb.f32.gz").read(), np.float32).reshape(H, W, 3)
+        gmeta = json.loads((gdir / "meta.json").read_text())
+        ref = (np.frombuffer(gzip.open(gdir / "fb.f32.gz").read(), np.float32).reshape(H, W, 3)
+               if (gdir / "fb.f32.gz").exists() else None)
         ppm_ref = golden_ppm(a.config)
-        par = {"vs": f"reference CPU render() output (tests/golden/scenes/{GOLDEN_FULL[a.config]})"}
+        par = {"vs": f"reference CPU render() output (tests/golden/scenes/{GOLDEN_FULL[a.config]}"
+                     + ("" if ref is not None else ": sha256 of the float frame and P6 file") + ")"}
 
         def p6_check(body: bytes, tag: str):
-            got = np.frombuffer(body, np.uint8).astype(int)
-            want = np.frombuffer(ppm_ref[17:], np.uint8).astype(int)
-            par[f"{tag}ppm_maxabs"] = int(np.abs(got - want).max())
-            par[f"{tag}ppm_identical"] = rt.p6_header(W, H) + body == ppm_ref
+            if ppm_ref is not None:
+                got = np.frombuffer(body, np.uint8).astype(int)
+                want = np.frombuffer(ppm_ref[len(rt.p6_header(W, H)):], np.uint8).astype(int)
+                par[f"{tag}ppm_maxabs"] = int(np.abs(got - want).max())
+            par[f"{tag}ppm_identical"] = ppm_matches_golden(a.config, rt.p6_header(W, H) + body)
 
         def f32_check(body: bytes, tag: str):
+            if ref is None:
+                par[f"{tag}rgb_sha256_equal"] = hashlib.sha256(body).hexdigest() == gmeta["sha256"]["fb.f32"]
+                return
             fr = np.frombuffer(body, np.float32).reshape(H, W, 3)
             par[f"{tag}rgb_maxabs"] = float(np.abs(fr - ref).max())
             par[f"{tag}rgb_bitexact_frac"] = float((fr.view(np.uint32) == ref.view(np.uint32)).mean())

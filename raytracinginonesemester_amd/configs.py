@@ -41,6 +41,13 @@ G_CONFIGS = {
     # default workload (G/assets/json_files/frog.json:3, G/include/scene.h:15-19)
     "c3b": dict(scene="frog.json", width=1920, height=1080, spp=16, max_depth=8),
     "c5": dict(scene="heightfield_c5.json", width=3840, height=2160, spp=64, max_depth=1),
+    # the reference's other shipped scenes at their shipped settings (G/assets/json_files/):
+    # sphere.json (128 spp: whole-tile work items, 4 bounces, mirrors, no diffuse bounce) and
+    # sphere_single.json (64 spp, 4 diffuse bounces)
+    "sphere": dict(scene="sphere.json", width=1920, height=1080, spp=128, max_depth=4),
+    "sphere_single": dict(scene="sphere_single.json", width=1920, height=1080, spp=64, max_depth=4),
+    # a multi-light bounce scene (two lights: the unpaired bounce loop, G/include/shader.h:87-94)
+    "cornell": dict(scene="cornell.json", width=1920, height=1080, spp=16, max_depth=3),
 }
 
 # Algorithmic bytes per camera sample (SURVEY.md §8(d) traffic model: 24 B per AABB fetched

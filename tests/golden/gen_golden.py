@@ -28,7 +28,8 @@ from raytracinginonesemester_amd import configs  # noqa: E402
 
 REF = REPO / "oracle" / "_ref"
 
-# G/ scene fixtures: name -> (scene json, W, H, spp, max_depth, keep raw hits)
+# G/ scene fixtures: name -> (scene json, W, H, spp, max_depth, keep raw hits); keep None: sha256
+# of the outputs only (full-size frames too large to commit)
 G_FIXTURES = {
     "c3_small": ("frog.json", 192, 108, 16, 1, True),
     "c3_full": ("frog.json", 1920, 1080, 16, 1, False),
@@ -39,6 +40,13 @@ G_FIXTURES = {
     # c3b: frog.json's own max_bounces 8 (diffuse bounce), 16 spp (bench config c3b)
     "c3b_small": ("frog.json", 192, 108, 16, 0, True),
     "c3b_full": ("frog.json", 1920, 1080, 16, 0, False),
+    # sphere.json as shipped (G/assets/json_files/sphere.json): five scaled sphere instances and a
+    # plane, mirrors kr 0.35/0.95/0.5, shininess up to 100000, 128 spp (spp > 64: whole-tile
+    # work items), 4 bounces, diffuse_bounce false
+    "sphere": ("sphere.json", 192, 108, 128, 0, False),
+    "sphere_full": ("sphere.json", 1920, 1080, 128, 0, None),
+    # sphere_single.json at its shipped 1920x1080x64, 4 diffuse bounces
+    "sphere_single_full": ("sphere_single.json", 1920, 1080, 64, 0, None),
 }
 # HW1 fixtures: name -> (config, W, H)
 HW1_FIXTURES = {
@@ -113,12 +121,16 @@ def gen_g(name: str) -> None:
         meta["sha256"] = {k: sha256(t / k) for k in
                           ("nodes.bin", "aabbs.bin", "tris.bin", "triobj.bin", "mats.bin",
                            "lights.bin", "fb.f32", "hits.i32", "hitt.f32")}
-        gz(t / "fb.f32", dst / "fb.f32.gz")
+        if keep_hits is not None:
+            gz(t / "fb.f32", dst / "fb.f32.gz")
         if keep_hits:
             gz(t / "hits.i32", dst / "hits.i32.gz")
             gz(t / "hitt.f32", dst / "hitt.f32.gz")
         if name in PPM_OF:
             ppm(t / "fb.f32", meta["width"], meta["height"], dst / "image.ppm.gz")
+        if keep_hits is None:  # the P6 file write_p6 makes of the frame, by sha256
+            run([REF / "ref_ppm", t / "fb.f32", meta["width"], meta["height"], t / "image.ppm"])
+            meta["sha256"]["image.ppm"] = sha256(t / "image.ppm")
         (dst / "meta.json").write_text(json.dumps(meta, indent=1) + "\n")
 
 

@@ -209,6 +209,42 @@ def test_c3b_full_frame_matches_reference():
     assert rt.encode_p6(rgb) == gzip.open(GOLDEN / "scenes" / "c3b_full" / "image.ppm.gz").read()
 
 
+@pytest.mark.parametrize("flags", [0, rt._lib.RT_FLAG_BINARY])
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_sphere_scene_parity(kernel, flags):
+    """sphere.json as shipped (G/assets/json_files/sphere.json: scaled sphere instances, mirrors
+    with kr up to 0.95, shininess up to 100000, 128 spp, 4 bounces, no diffuse bounce) at 192x108
+    against the reference's own render(): float frame bit for bit, hit AOVs by sha256."""
+    meta = golden_meta("sphere")
+    assert meta["spp"] == 128 and meta["max_depth"] == 4 and meta["diffuse_bounce"] == 0
+    hs = host_scene("sphere.json")
+    cam = hs.camera(meta["width"], meta["height"])
+    rgb, hi, ht = _device_scene("sphere.json").render(cam, spp=128, max_depth=4, diffuse_bounce=False,
+                                                      miss_color=hexv(meta["miss_color"]), aov=True,
+                                                      kernel=kernel, flags=flags)
+    assert hashlib.sha256(hi.tobytes()).hexdigest() == meta["sha256"]["hits.i32"]
+    assert hashlib.sha256(ht.tobytes()).hexdigest() == meta["sha256"]["hitt.f32"]
+    _check_fb(rgb, golden_array("sphere", "fb.f32.gz", np.float32))
+
+
+@pytest.mark.parametrize("name,scene", [("sphere_full", "sphere.json"), ("sphere_single_full", "sphere_single.json")])
+def test_shipped_scene_full_frames(name, scene):
+    """The reference's other shipped scenes at their shipped size (1920x1080; sphere.json 128 spp
+    4 mirror bounces, sphere_single.json 64 spp 4 diffuse bounces): the float frame and both
+    hit AOVs equal the reference's own full-size outputs (sha256 of each)."""
+    meta = golden_meta(name)
+    hs = host_scene(scene)
+    assert (meta["width"], meta["height"], meta["spp"]) == (1920, 1080, hs.settings["spp"])
+    cam = hs.camera(1920, 1080)
+    rgb, hi, ht = _device_scene(scene).render(cam, spp=meta["spp"], max_depth=meta["max_depth"],
+                                              diffuse_bounce=bool(meta["diffuse_bounce"]),
+                                              miss_color=hexv(meta["miss_color"]), aov=True)
+    assert np.isfinite(rgb).all()
+    assert hashlib.sha256(np.ascontiguousarray(rgb, np.float32).tobytes()).hexdigest() == meta["sha256"]["fb.f32"]
+    assert hashlib.sha256(hi.tobytes()).hexdigest() == meta["sha256"]["hits.i32"]
+    assert hashlib.sha256(ht.tobytes()).hexdigest() == meta["sha256"]["hitt.f32"]
+
+
 @pytest.mark.parametrize("env", [{}, {"RT_HEAVY_CAP": "8"}, {"RT_HEAVY_FRAC": "0.0001"}])
 def test_heavy_first_dispatch_changes_nothing(env, monkeypatch):
     """Heavy-first dispatch (the previous frames' per-tile costs order the render blocks; full

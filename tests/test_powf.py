@@ -23,7 +23,9 @@ def _inputs(n_grid=1 << 16, n_rand=1 << 15, seed=3):
     rng = np.random.default_rng(seed)
     xs, ys = [], []
     grid = np.linspace(0, 0x3F800000, n_grid, dtype=np.uint64).astype(np.uint32).view(np.float32)
-    for y in (1.0, 2.0, 16.0, 32.0, 64.0, 128.0, 7.3, 0.5):
+    # the shipped scenes' shininess values (frog/sphere_single/cornell, sphere.json: 128, 256,
+    # 1000, 100000) and others
+    for y in (1.0, 2.0, 16.0, 32.0, 64.0, 128.0, 256.0, 1000.0, 100000.0, 7.3, 0.5):
         xs.append(grid)
         ys.append(np.full_like(grid, y))
     r = rng.integers(0, 2 ** 32, size=(2, n_rand), dtype=np.uint64).astype(np.uint32).view(np.float32)

@@ -408,6 +408,15 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
     uint32_t st_ref = 0, st_mlo = 0, st_mhi = 0;  // lane k holds entry k
     int sp = 0;
     int stale = 0;  // entries [0, stale) take the pop-time re-test
+    // The record arrays' bases, held in SGPRs for the whole traversal.  Left to itself the
+    // compiler re-reads them from the kernel arguments at every pop (they are cheap to
+    // rematerialise), which puts a dependent scalar load before each record load.
+    const char* leaf_b = reinterpret_cast<const char*>(sc.leaf);
+    const char* wnode_b = reinterpret_cast<const char*>(sc.wnode);
+    const char* ibox_b = reinterpret_cast<const char*>(sc.ibox);
+#ifdef RT_EXP_HOIST_BASE
+    asm volatile("" : "+s"(leaf_b), "+s"(wnode_b), "+s"(ibox_b));
+#endif
     while (true) {
         RT_STAT(2 + so, 1);
 #ifdef RT_STATS
@@ -420,7 +429,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
             if (ref & LEAF_BIT) {
                 RT_STAT(10 + so, 1);
                 const uint32_t slot = ref & ~LEAF_BIT;
-                const float4* L = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.leaf) + (slot << 6));
+                const float4* L = reinterpret_cast<const float4*>(leaf_b + (slot << 6));
                 const bool act = lane_in(mask);
                 const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
                 float t, u, v;
@@ -441,7 +450,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                     // 4-ary record in one round trip: the seven 16-byte scalar loads are issued
                     // together and waited for once (the empty asm keeps the compiler from sinking
                     // each load next to its entry's test), addressed by 32-bit byte offset
-                    const float4* W = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.wnode) + (ref << 7));
+                    const float4* W = reinterpret_cast<const float4*>(wnode_b + (ref << 7));
                     vf4 wq[7];
 #pragma unroll
                     for (int k = 0; k < 7; ++k) wq[k] = ldc_v(W + k);
@@ -512,12 +521,11 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                 RT_STAT(6 + so, 1);
                 BoxP ob;
                 if (ref & LEAF_BIT) {
-                    const float4* L = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.leaf) +
-                                                                      ((ref & ~LEAF_BIT) << 6));
+                    const float4* L = reinterpret_cast<const float4*>(leaf_b + ((ref & ~LEAF_BIT) << 6));
                     const float4 c = ldc(L + 2), d = ldc(L + 3);
                     ob = BoxP{hi2(c), lo2(d), hi2(d)};
                 } else {
-                    const float4* B = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(sc.ibox) + (ref << 5));
+                    const float4* B = reinterpret_cast<const float4*>(ibox_b + (ref << 5));
                     const float4 p = ldc(B), q = ldc(B + 1);
                     ob = BoxP{lo2(p), hi2(p), lo2(q)};
                 }

@@ -111,6 +111,7 @@ struct RenderParams {
     int32_t lane_samples;                             // 1: one sample per lane; else pixel loop
     int32_t half_waves;                               // samples kernel: lanes >= 64 >> half_waves idle
     int32_t paired_only;                              // multi-bounce, half waves, one light: LS = 3 kernels
+    int32_t regen;                                    // ... with path regeneration: LS = 4 kernels (full-wave items)
     int32_t tile_order;                               // RT_TILES_*
     int32_t spp_log2, tile_w_log2;                    // samples kernel: both powers of two
     int32_t cull;                                     // tile culling against the root box
@@ -1986,6 +1987,267 @@ __device__ __forceinline__ uint32_t dequeue(uint32_t* head, uint32_t lane) {
     return uni(v);
 }
 
+// Pixel and sample of lane-sample lt of a tile in the samples layout (Z-ordered pixels in a
+// square tile, spp consecutive samples per pixel; samples_tile's mapping).
+struct SampleAt {
+    int x, r, y, s, pix;
+    bool valid;
+};
+__device__ __forceinline__ SampleAt sample_at(const RenderParams& P, int tile, int lt) {
+    SampleAt a;
+    a.s = lt & (P.spp - 1);
+    const int pit = lt >> P.spp_log2;
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    int px, py;
+    if (P.tile_w == P.tile_h) {
+        px = (pit & 1) | ((pit >> 1) & 2) | ((pit >> 2) & 4) | ((pit >> 3) & 8);
+        py = ((pit >> 1) & 1) | ((pit >> 2) & 2) | ((pit >> 3) & 4) | ((pit >> 4) & 8);
+    } else {
+        px = pit & (P.tile_w - 1);
+        py = pit >> P.tile_w_log2;
+    }
+    a.x = tx * P.tile_w + px;
+    a.r = ty * P.tile_h + py;
+    a.valid = a.x < P.W && a.r < P.rows;
+    a.y = a.valid ? global_row(P, a.r) : 0;
+    a.pix = a.valid ? a.r * P.W + a.x : -1;
+    return a;
+}
+
+#ifdef RT_RESUME
+// Path regeneration over the resumable paired traversals (one light): a wave owns 64 samples
+// (a 2x2-pixel quad x 16 spp), whose camera rays all 64 lanes trace with the wave DFS first
+// (coherent rays keep the wave-shared stack); each camera hit (bestT, slot) waits in the
+// sample's colour slot of LDS.  Then lanes 0-31 carry paths and lanes 32-63 their shadow rays
+// (paired_bounces_resume): a path lane whose sample has ended writes the sample's colour and
+// takes the wave's next sample, so the path lanes stay busy until the wave's pool is drained,
+// instead of one sample per lane and the wave waiting for its longest path.  Per sample the
+// same rays, tests, arithmetic and order of radiance adds: exact.
+// col: the block's colour slots (3 floats per sample); wbase: this wave's first slot; tile, qw:
+// the work item (its 64 samples are lane-samples qw*64 + k).
+template <int MODE>
+__device__ __forceinline__ void paired_bounces_regen(const RenderParams& P, int tile, uint32_t qw, int wbase,
+                                                     float* col, float* park) {
+    const SceneView& sc = P.sc;
+    const bool upper = lane_id() >= 32;
+    const int max_depth = P.max_depth;
+    uint32_t* stk = reinterpret_cast<uint32_t*>(park);
+    LaneDfs d;
+    d.run = false;
+    d.ref = 0;
+    d.sp = d.stale = 0;
+    d.retest = false;
+    RayPre ray;
+    HitState hs;
+    hs.bestT = FLT_MAX;
+    hs.slot = -1;
+    f3 radiance = mk(0.f, 0.f, 0.f), thr = radiance;
+    uint32_t rng = 0;
+    bool alive = false;
+    int cur = -1;                    // lower lanes: the pool sample this lane's path belongs to
+    int depth = 0;                   // lower lanes: the depth of the path result in hs
+    bool unproc = false;             // lower lanes: hs holds a path result not yet shaded
+    bool need_up = false;            // upper lanes: tracing (or holding the answer of) a shadow ray
+    float dist_up = 0.f;
+    bool pend = false, lit_p = false;
+    f3 thr_p = mk(0.f, 0.f, 0.f), Lo_p = thr_p, Lo_lit_p = thr_p;
+    int taken = 0;  // wave-uniform: pool samples handed out
+    bool finished = false;
+    for (uint32_t guard = 0; guard < (1u << 16); ++guard) {
+        const uint64_t runm = ballot(d.run);
+        const bool ready = !upper && !d.run && !lane_in(runm >> 32);
+        const uint64_t readym = ballot(ready);
+        const bool pready = upper && lane_in(readym << 32);
+        // IsInShadow's answer (shader.h:44-62) of the upper lanes whose pair is ready
+        const uint64_t occ = ballot(pready && need_up && hs.slot >= 0 && hs.bestT < dist_up);
+        if (ready && pend) {
+            const bool occluded = lane_in(occ >> 32);
+            radiance = add(radiance, mul(thr_p, (lit_p && !occluded) ? Lo_lit_p : Lo_p));
+            pend = false;
+        }
+        if (pready) need_up = false;
+        // a path that has ended: its sample's colour (TraceRayIterative's clamp) to its slot
+        if (ready && cur >= 0 && !pend && !unproc && !alive) {
+            const f3 c = clamp01(radiance);
+            float* o = col + 3 * (wbase + cur);
+            o[0] = c.x;
+            o[1] = c.y;
+            o[2] = c.z;
+            cur = -1;
+        }
+        // free path lanes take the pool's next samples, in lane order
+        const bool want = ready && cur < 0;
+        const uint64_t wantm = ballot(want);
+        if (wantm != 0 && taken < 64) {
+            const int k = taken + (int)__popcll(wantm & ((1ull << lane_id()) - 1));
+            if (want && k < 64) {
+                const SampleAt a = sample_at(P, tile, (int)qw * 64 + k);
+                const float* h = col + 3 * (wbase + k);
+                hs.bestT = h[0];
+                hs.slot = __float_as_int(h[1]);
+                ray = camera_ray(P, a.valid, a.x, a.y, a.s);
+                rng = make_rng_seed(a.x, a.y, a.s);
+                thr = mk(1.f, 1.f, 1.f);
+                radiance = mk(0.f, 0.f, 0.f);
+                alive = a.valid && max_depth > 0;
+                depth = 0;
+                unproc = true;
+                cur = k;
+            }
+            taken = min(64, taken + (int)__popcll(wantm));
+        }
+        bool need = false;
+        float dist = 0.f;
+        f3 so = mk(0.f, 0.f, 0.f), sd = so;
+        bool launch = false;  // lower lanes: a new path ray to trace
+        if (ready && unproc) {
+            unproc = false;
+            const bool hit = alive && hs.slot >= 0;
+            if (alive && !hit) {
+                radiance = add(radiance, mul(thr, P.miss));
+                alive = false;
+            }
+            if (hit) {
+                const SurfHit sh = resolve_hit<false>(sc, ray, hs.slot);
+                const DevMaterial m = material_of(sc, sh.tri);
+                const f3 N = unit(sh.n);
+                const f3 V = unit(sub(ray.o, sh.p));
+                f3 Lo = mk(0.f, 0.f, 0.f);
+                Lo = add(Lo, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 0.05f));
+                Lo = add(Lo, mk(m.emission[0], m.emission[1], m.emission[2]));
+                const DevLight& lt = sc.lights[0];
+                const f3 lpos = mk(lt.pos[0], lt.pos[1], lt.pos[2]);
+                f3 contrib = mk(0.f, 0.f, 0.f);
+                bool lit = false;
+                const f3 L = unit(sub(lpos, sh.p));
+                const float NdotL = fmaxf(dot(N, L), 0.0f);
+                if (NdotL > 0.0f) {
+                    const f3 f = eval_brdf(m, sh.n, V, L);
+                    const f3 rad = scale(mk(lt.color[0], lt.color[1], lt.color[2]), (float)lt.intensity);
+                    contrib = scale(mul(rad, f), NdotL);
+                    lit = true;
+                    const f3 toL = sub(lpos, sh.p);
+                    dist = sqrtf(dot(toL, toL));
+                    if (dist > 0.0f) {
+                        need = true;
+                        so = add(sh.p, scale(N, RT_EPS));
+                        sd = divf(toL, dist);
+                    }
+                }
+                thr_p = thr;
+                Lo_p = Lo;
+                Lo_lit_p = add(Lo, contrib);
+                lit_p = lit;
+                pend = true;
+                if (depth + 1 < max_depth) {
+                    const float kd = m.kd, kr = m.kr, total = kd + kr;
+                    if (total <= 0.0f) {
+                        alive = false;
+                    } else {
+                        const f3 Nb = unit(sh.n);
+                        const float xi = rng_next(rng);
+                        if (P.diffuse_bounce && xi < kd / total) {
+                            f3 dd = random_unit_vector(rng);
+                            if (!(dot(dd, Nb) > 0.0f)) dd = mk(-dd.x, -dd.y, -dd.z);
+                            ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), dd, scene_bmax(sc));
+                            const float nl = fmaxf(dot(Nb, dd), 0.0f);
+                            thr = mul(thr, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 2.0f * nl));
+                        } else {
+                            const f3 I = unit(ray.d);
+                            const f3 refl = sub(I, scale(Nb, 2.0f * dot(I, Nb)));
+                            ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), refl, scene_bmax(sc));
+                            thr = mul(thr, scale(mk(m.spec[0], m.spec[1], m.spec[2]), kr));
+                        }
+                        if (thr.x < 1e-4f && thr.y < 1e-4f && thr.z < 1e-4f) alive = false;
+                    }
+                    ++depth;
+                } else {
+                    alive = false;
+                }
+            }
+            launch = alive;
+        }
+        const uint64_t needm = ballot(need);
+        const float ox = __shfl_xor(so.x, 32), oy = __shfl_xor(so.y, 32), oz = __shfl_xor(so.z, 32);
+        const float dx = __shfl_xor(sd.x, 32), dy = __shfl_xor(sd.y, 32), dz = __shfl_xor(sd.z, 32);
+        const float dd = __shfl_xor(dist, 32);
+        bool go = launch;
+        if (pready) {
+            need_up = lane_in(needm << 32);
+            dist_up = dd;
+            if (need_up) ray = make_ray(mk(ox, oy, oz), mk(dx, dy, dz), scene_bmax(sc));
+            go = need_up;
+        }
+        dfs_start(sc, ray, go, hs, d);
+        if (launch) unproc = true;
+        if (ballot(d.run || pend || unproc || cur >= 0) == 0 && taken >= 64) {
+            finished = true;
+            break;
+        }
+        const uint32_t quota = (uint32_t)__popcll(ballot(d.run)) >> RT_RESUME_SHIFT;
+        dfs_run(sc, ray, upper, dist_up, hs, d, stk, quota);
+    }
+    // the guard cannot run out (every iteration ends a traversal or a sample); if it ever did,
+    // the wave's samples are poisoned rather than silently truncated
+    if (!finished && !upper) col[3 * (wbase + (int)lane_id())] = __int_as_float(0x7fc00000);
+}
+
+// One wave item of the regeneration kernels (LS = 4): the camera rays of its 64 samples through
+// the wave DFS, their hits parked in the samples' colour slots, then paired_bounces_regen, then
+// the per-pixel sums in sample order (samples_tile's epilogue).
+template <int MODE>
+__device__ __forceinline__ void regen_tile(const RenderParams& P, int tile, uint32_t qw, int t, float* col, int* kpix,
+                                           float* park, const int* lds_zero) {
+    const uint32_t wv = uni((uint32_t)t) >> 6;
+    const int wbase = (int)(wv << 6);
+    {
+        const SampleAt a = sample_at(P, tile, (int)qw * 64 + (t & 63));
+        if (a.s == 0) kpix[t >> P.spp_log2] = a.pix;
+        const RayPre ray = camera_ray(P, a.valid, a.x, a.y, a.s);
+        HitState hs;
+        traverse<MODE>(P.sc, ray, a.valid && P.max_depth > 0, false, 0.0f, hs);
+        if (a.valid && P.hit_idx) {
+            const int64_t aov = (int64_t)a.pix * P.spp + a.s;
+            const bool hit = P.max_depth > 0 && hs.slot >= 0;
+            P.hit_idx[aov] = hit ? leaf_tri<false>(P.sc, hs.slot) : -1;
+            P.hit_t[aov] = hit ? hs.bestT : -1.0f;
+        }
+        col[3 * t] = hs.bestT;
+        col[3 * t + 1] = __int_as_float(hs.slot);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    paired_bounces_regen<MODE>(P, tile, qw, wbase, col, park + t);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int t2 = (int)((wv << 6) | __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(
+                                             ~0u, (uint32_t)*(const volatile int*)lds_zero)));
+    if ((t2 & (P.spp - 1)) == 0) {
+        const int pix = kpix[t2 >> P.spp_log2];
+        if (pix >= 0) {
+            f3 acc = mk(0.f, 0.f, 0.f);
+            for (int k = 0; k < P.spp; ++k)
+                acc = add(acc, mk(col[3 * (t2 + k)], col[3 * (t2 + k) + 1], col[3 * (t2 + k) + 2]));
+            const float rs = 1.0f / (float)P.spp;
+            const size_t k = (size_t)pix * 3;
+            const f3 px = mk(acc.x * rs, acc.y * rs, acc.z * rs);
+            if (P.rgb) {
+                P.rgb[k] = px.x;
+                P.rgb[k + 1] = px.y;
+                P.rgb[k + 2] = px.z;
+            }
+            if (P.p6) {
+                P.p6[k] = rtp::p6_default_sample(px.x);
+                P.p6[k + 1] = rtp::p6_default_sample(px.y);
+                P.p6[k + 2] = rtp::p6_default_sample(px.z);
+            }
+        }
+    }
+}
+#endif
+
 // One sample per lane: a block covers a tile_w x tile_h pixel tile x spp samples (spp a power
 // of two <= 256, tile_w*tile_h*spp == BLOCK); per-pixel sums run in sample order from LDS.
 template <int MODE, bool D1, int LS = 0>
@@ -2217,6 +2479,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
             t_start[wv] = (uint32_t)wall_clock64();
             t_item[wv] = (uint32_t)tile * WPT + qw;
         }
+#ifdef RT_RESUME
+        if constexpr (SAMPLES && LS == 4) regen_tile<MODE>(R, tile, qw, tid, col, kpix, park, &lds_zero);
+        else
+#endif
         if constexpr (SAMPLES) samples_tile<MODE, D1, LS>(R, tile, qw, tid, col, kpix, park, &lds_zero);
         else pixels_tile<MODE, D1>(R, tile, qw, tid, park);
         if (R.tile_cost && fresh_lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
@@ -3192,6 +3458,14 @@ void launch_mode(const RenderParams& P, const Launch& L) {
         }
         launch_render<D1_MODE, SAMPLES, true>(P, L);
     } else {
+#ifdef RT_RESUME
+        if constexpr (SAMPLES && (MODE & MODE_WIDE) != 0 && (MODE & (MODE_DEEP | RT_KERNEL_LANE)) == 0) {
+            if (P.regen) {
+                launch_render<MODE, SAMPLES, false, RT_PAIRED_WAVES, 4>(P, L);
+                return;
+            }
+        }
+#endif
         if constexpr (SAMPLES && (MODE & (MODE_DEEP | RT_KERNEL_LANE)) == 0) {
             if (P.half_waves && P.paired_only) {
                 launch_render<MODE, SAMPLES, false, RT_PAIRED_WAVES, 3>(P, L);
@@ -3358,6 +3632,12 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
                         ? 1
                         : 0;
     if (const char* e = std::getenv("RT_PAIRED_ONLY")) P.paired_only = P.paired_only && std::atoi(e) != 0;
+    // Path regeneration (paired_bounces_regen): the paired-only case over 4-ary records with
+    // full-wave items (64 samples per wave, 2 x 2 pixels x 16 spp).  RT_REGEN=1 selects it (A/B).
+    P.regen = 0;
+    if (const char* e = std::getenv("RT_REGEN"))
+        P.regen = P.paired_only && P.sc.wide && s->lane_wide && o->spp <= 64 && std::atoi(e) != 0 ? 1 : 0;
+    if (P.regen) half = P.half_waves = 0;
     int ppb = samples ? (BLOCK >> half) / o->spp : BLOCK;  // pixels per block
     int tw = 1;
     while (tw * tw < ppb) tw <<= 1;                // square-ish power-of-two tile

@@ -432,6 +432,21 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                 const uint32_t slot = ref & ~LEAF_BIT;
                 const float4* L = reinterpret_cast<const float4*>(leaf_b + (slot << 6));
                 const bool act = lane_in(mask);
+#ifdef RT_EXP_PREFETCH
+                // A leaf pushes nothing: the entry processed next is the stack top.  Touch its
+                // record (one dword per 64-byte line) with the leaf's loads, so its own load in
+                // the next iteration finds the scalar cache warm; the values are consumed (no
+                // wait) at the end of this iteration.
+                uint32_t pf0 = 0, pf1 = 0;
+                if (sp > 0) {
+                    const uint32_t nref = rdlane(st_ref, sp - 1);
+                    const uint32_t* np = (nref & LEAF_BIT)
+                                             ? reinterpret_cast<const uint32_t*>(leaf_b + ((nref & ~LEAF_BIT) << 6))
+                                             : reinterpret_cast<const uint32_t*>(wnode_b + (nref << 7));
+                    pf0 = ldc_u32(np);
+                    pf1 = (nref & LEAF_BIT) ? 0u : ldc_u32(np + 16);
+                }
+#endif
                 const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
                 float t, u, v;
                 const bool h = act && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin,
@@ -445,6 +460,9 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                     stale = sp;
                     if (any_hit) alive &= ~ballot(h && t < any_hit_dist);
                 }
+#ifdef RT_EXP_PREFETCH
+                asm volatile("" ::"s"(pf0), "s"(pf1));
+#endif
             } else {
                 RT_STAT(8 + so, 1);
                 if constexpr (WIDE) {

@@ -976,7 +976,9 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, con
         Lo = add(Lo, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 0.05f));
         Lo = add(Lo, mk(m.emission[0], m.emission[1], m.emission[2]));
     }
-    for (int li = 0; li < sc.num_lights; ++li) {
+    // One light (frog, sphere scenes): the body straight, no loop -- as a loop, values the
+    // compiler carried between iterations (the unset shadow ray of lanes without one) spilled.
+    auto light = [&](int li) {
         const DevLight& lt = sc.lights[li];
         const f3 lpos = mk(lt.pos[0], lt.pos[1], lt.pos[2]);
         float dist = 0.f;
@@ -1035,6 +1037,11 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, con
         Lo = take ? mk(pk.get(7), pk.get(8), pk.get(9)) : mk(pk.get(4), pk.get(5), pk.get(6));
         slot = __float_as_int(pk.get(3));
         cray.d = mk(pk.get(0), pk.get(1), pk.get(2));
+    };
+    if (sc.num_lights == 1) {
+        light(0);
+    } else {
+        for (int li = 0; li < sc.num_lights; ++li) light(li);
     }
     return radiance_of(Lo);
 }

@@ -128,7 +128,20 @@ __host__ __device__ inline bool box_hit_exact(const RayPre& r, const BoxP& b, do
     // double(o) and 1/double(d) out of the traversal loops) measured no faster and, in the 6-wave
     // build, exposed a miscompile of the bounce and binary-record kernels (golden parity failures;
     // DESIGN.md §7).
+#if defined(__HIP_DEVICE_COMPILE__) && defined(RT_EXACT_LOCAL)
+    // Hoisted out of a traversal loop, double(o) and 1/double(d) hold 12 VGPRs across the whole
+    // loop for a test only ambiguous lanes reach (a few % of box tests).  An opaque SGPR zero,
+    // made here (inside the wave-uniform branch that calls this), ORed into the float bits ties
+    // them to this call, so they are recomputed per exact test instead.
+    uint32_t oz = 0;
+    asm volatile("" : "+s"(oz));
+    const float o[3] = {__uint_as_float(__float_as_uint(r.o.x) | oz), __uint_as_float(__float_as_uint(r.o.y) | oz),
+                        __uint_as_float(__float_as_uint(r.o.z) | oz)};
+    const float d[3] = {__uint_as_float(__float_as_uint(r.d.x) | oz), __uint_as_float(__float_as_uint(r.d.y) | oz),
+                        __uint_as_float(__float_as_uint(r.d.z) | oz)};
+#else
     const float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+#endif
     const float mn[3] = {b.x.x, b.y.x, b.z.x}, mx[3] = {b.x.y, b.y.y, b.z.y};
     bool ok = true;
 #pragma unroll

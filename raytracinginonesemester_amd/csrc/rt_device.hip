@@ -62,6 +62,9 @@ constexpr int MODE_PK = 32;  // the wave traversal's box tests in packed FMAs (b
 // Trees whose DFS needs more than STACK_CAP entries: SearchBVH literally, per lane, with the
 // reference's 512-entry stack, its overflow rule and brute-force completion (traverse_deep).
 constexpr int MODE_DEEP = 64;
+// The depth-1 kernels' one-light form: the scene has exactly one light, so shade_d1 has no light
+// loop (whose loop-carried values spilled in the big-scene 8-wave build).
+constexpr int MODE_1L = 128;
 constexpr int REF_STACK = 512;                // query.h:245
 constexpr uint32_t INV_LEAF = 0xFFFFFFFEu;    // deep stack entry: a leaf naming no triangle (query.h:263)
 constexpr uint32_t BRUTE_BIT = 0x40000000u;   // HitState::slot of a brute-force hit: BRUTE_BIT | triangle
@@ -1038,7 +1041,9 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, con
         slot = __float_as_int(pk.get(3));
         cray.d = mk(pk.get(0), pk.get(1), pk.get(2));
     };
-    if (sc.num_lights == 1) {
+    if ((MODE & MODE_1L) != 0) {
+        light(0);
+    } else if (sc.num_lights == 1) {
         light(0);
     } else {
         for (int li = 0; li < sc.num_lights; ++li) light(li);
@@ -3477,7 +3482,8 @@ void launch_mode(const RenderParams& P, const Launch& L) {
         }
         if constexpr ((MODE & (MODE_DEEP | RT_KERNEL_LANE)) == 0) {
             if (L.big) {
-                launch_render<D1_MODE, SAMPLES, true, RT_RENDER_WAVES_BIG>(P, L);
+                if (P.sc.num_lights == 1) launch_render<D1_MODE | MODE_1L, SAMPLES, true, RT_RENDER_WAVES_BIG>(P, L);
+                else launch_render<D1_MODE, SAMPLES, true, RT_RENDER_WAVES_BIG>(P, L);
                 return;
             }
         }

@@ -294,7 +294,7 @@ __device__ __forceinline__ BoxP leaf_box(const NodeRec& r) {
 // box_hit for the lanes in `act` (a wave mask; all lanes call it), as the mask of lanes that
 // pass: the float pre-classification for everyone, the exact double test only behind a
 // wave-uniform branch taken when some lane is ambiguous.
-template <bool PK = false>
+template <bool PK = false, bool XL = false>
 __device__ __forceinline__ uint64_t box_hit_mask(const RayPre& r, const BoxP& b, float tmax, uint64_t act) {
     AxisEnds e;
     if constexpr (PK) e = box_ends_pk(r, b);
@@ -312,7 +312,7 @@ __device__ __forceinline__ uint64_t box_hit_mask(const RayPre& r, const BoxP& b,
     RT_KF64(tmin_d, (double)kRayTMin)
     RT_KF64(fltmax_d, (double)FLT_MAX)
     const double tmax_d = tmax == FLT_MAX ? fltmax_d : (double)tmax;
-    return hit | (ballot(box_hit_exact(r, b, tmin_d, tmax_d)) & amb);
+    return hit | (ballot(box_hit_exact<XL>(r, b, tmin_d, tmax_d)) & amb);
 }
 
 // rt_count_rays: one wave-aggregated add of the lanes where `c` holds into ray class `cls`.
@@ -388,7 +388,7 @@ __device__ __forceinline__ void lane_iters_note(uint32_t it) {
 // - records addressed by 32-bit byte offsets, which the scalar loads take as their SGPR offset
 //   (rt_scene_create sends larger trees to MODE_DEEP);
 // - the camera ray's query skips the `alive` AND (only a shadow query's lanes leave early).
-template <bool WIDE, bool PK = false>
+template <bool WIDE, bool PK = false, bool XL = false>
 __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const RayPre& r, bool active,
                                                   bool any_hit, float any_hit_dist, HitState& hs) {
     uint64_t alive = ballot(active);
@@ -403,7 +403,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
     RT_STAT(13 + so, __popcll(alive));
     // The root's pop-time test (SearchBVH tests every popped node, query.h:252-254) is made
     // here with the initial bestT; the root is then the first entry in hand.
-    uint64_t mask = box_hit_mask<PK>(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
+    uint64_t mask = box_hit_mask<PK, XL>(r, own_box(sc, sc.root_ref, true), hs.bestT, alive);
     if (mask == 0) {
         if (!any_hit) RT_STAT(17, 1);
         return;
@@ -487,7 +487,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                         if (refs[k] == NO_REF) continue;
                         const float4 p = wv[(3 * k) / 2], q = wv[(3 * k) / 2 + 1];
                         const BoxP bk = (k & 1) ? BoxP{hi2(p), lo2(q), hi2(q)} : BoxP{lo2(p), hi2(p), lo2(q)};
-                        const uint64_t mk_ = box_hit_mask<PK>(r, bk, hs.bestT, mask);
+                        const uint64_t mk_ = box_hit_mask<PK, XL>(r, bk, hs.bestT, mask);
                         if (mk_ != 0) {
                             if (pmask != 0) {  // the previous passing entry goes to the stack
                                 st_ref = wrlane(pref, sp, st_ref);
@@ -505,14 +505,14 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                     const uint4 q3 = ldc_u(N + 3);
                     const uint32_t lref = q3.x, rref = q3.y;
                     if (lref != NO_REF) {
-                        const uint64_t ml = box_hit_mask<PK>(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
+                        const uint64_t ml = box_hit_mask<PK, XL>(r, BoxP{lo2(q0), hi2(q0), lo2(q1)}, hs.bestT, mask);
                         if (ml != 0) {
                             pref = lref;
                             pmask = ml;
                         }
                     }
                     if (rref != NO_REF) {
-                        const uint64_t mr = box_hit_mask<PK>(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
+                        const uint64_t mr = box_hit_mask<PK, XL>(r, BoxP{hi2(q1), lo2(q2), hi2(q2)}, hs.bestT, mask);
                         if (mr != 0) {
                             if (pmask != 0) {
                                 st_ref = wrlane(pref, sp, st_ref);
@@ -551,7 +551,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                     const float4 p = ldc(B), q = ldc(B + 1);
                     ob = BoxP{lo2(p), hi2(p), lo2(q)};
                 }
-                mask = box_hit_mask<PK>(r, ob, hs.bestT, mask);
+                mask = box_hit_mask<PK, XL>(r, ob, hs.bestT, mask);
             }
         }
     }
@@ -841,7 +841,8 @@ __device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, b
                                          float any_hit_dist, HitState& hs) {
     if constexpr ((MODE & MODE_DEEP) != 0) traverse_deep(sc, r, active, any_hit, any_hit_dist, hs);
     else if constexpr (MODE == RT_KERNEL_LANE) traverse_lane(sc, r, active, any_hit, any_hit_dist, hs);
-    else traverse_wave_split<(MODE & MODE_WIDE) != 0, (MODE & MODE_PK) != 0>(sc, r, active, any_hit, any_hit_dist, hs);
+    else traverse_wave_split<(MODE & MODE_WIDE) != 0, (MODE & MODE_PK) != 0, (MODE & MODE_PK) != 0 && (MODE & MODE_1L) == 0>(
+        sc, r, active, any_hit, any_hit_dist, hs);
 }
 
 // The traversal of a ray at bounce depth `depth` (wave-uniform): camera rays (depth 0) and their
@@ -942,11 +943,18 @@ __device__ __forceinline__ RayPre camera_ray(const RenderParams& P, bool valid, 
 // of arrays with stride BLOCK): the traversal needs every VGPR the kernel's occupancy allows, and
 // values kept live across it were spilled to scratch (private memory through L2/HBM); LDS is a
 // few tens of cycles away and otherwise unused by the render kernels.
-constexpr int PARK_SLOTS = 12;
+constexpr int PARK_SLOTS = 14;
 struct Park {
-    float* p;  // this lane's slot 0 (LDS)
-    __device__ __forceinline__ void put(int k, float v) const { p[k * BLOCK] = v; }
-    __device__ __forceinline__ float get(int k) const { return p[k * BLOCK]; }
+    // the wave's slot 0 (LDS, wave-uniform); a lane's slot is found afresh at every access (a
+    // per-lane pointer kept across the traversals was itself spilled in the 64-VGPR build)
+    float* p;
+    __device__ __forceinline__ uint32_t lane() const {
+        uint32_t z = 0;
+        asm volatile("" : "+s"(z));
+        return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, z));
+    }
+    __device__ __forceinline__ void put(int k, float v) const { p[k * BLOCK + lane()] = v; }
+    __device__ __forceinline__ float get(int k) const { return p[k * BLOCK + lane()]; }
     // The traversal between put and get writes no LDS, so without this the compiler would
     // forward the stored values and keep them in registers after all.
     __device__ __forceinline__ static void fence() { asm volatile("" ::: "memory"); }
@@ -954,9 +962,9 @@ struct Park {
 
 template <int MODE>
 __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, const RayPre& ray, const HitState& hs,
-                                       float* park_lds) {
+                                       float* park_wave) {
     const SceneView& sc = P.sc;
-    const Park pk{park_lds};
+    const Park pk{park_wave};
     bool valid = valid_in;
     bool hit = valid && hs.slot >= 0;
     // radiance = 0 + (1,1,1) * missColor on a miss (query.h:181-183), 0 + (1,1,1) * Lo on a hit:
@@ -969,6 +977,9 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, con
     };
     if (ballot(hit) == 0) return radiance_of(mk(0.f, 0.f, 0.f));
     int32_t slot = hs.slot;
+    // valid and hit go to LDS at once (slot 10; lit, known later, to slot 11): kept live
+    // across the shading, the lane's valid bit was spilled to scratch in the 64-VGPR build
+    pk.put(10, __int_as_float((valid ? 1 : 0) | (hit ? 2 : 0)));
     // The camera ray's origin is the (uniform) camera centre; only its direction is per lane.
     RayPre cray;
     cray.o = ray.o;
@@ -1025,7 +1036,7 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, con
         pk.put(7, Lo_lit.x);
         pk.put(8, Lo_lit.y);
         pk.put(9, Lo_lit.z);
-        pk.put(10, __int_as_float((valid ? 1 : 0) | (hit ? 2 : 0) | (lit ? 4 : 0)));
+        pk.put(11, lit ? 1.0f : 0.0f);
         Park::fence();
         HitState shs;
         count_rays<MODE>(P.ray_count, 1, need);
@@ -1035,7 +1046,7 @@ __device__ __forceinline__ f3 shade_d1(const RenderParams& P, bool valid_in, con
         const int fl = __float_as_int(pk.get(10));
         valid = (fl & 1) != 0;
         hit = (fl & 2) != 0;
-        lit = (fl & 4) != 0;
+        lit = pk.get(11) != 0.0f;
         const bool take = lit && !occluded;
         Lo = take ? mk(pk.get(7), pk.get(8), pk.get(9)) : mk(pk.get(4), pk.get(5), pk.get(6));
         slot = __float_as_int(pk.get(3));
@@ -1416,13 +1427,21 @@ template <int MODE, bool D1, int PAIR = 0>
 // PAIR (half waves): 1, the camera ray's shading on in paired_bounces when the scene has one
 // light; 2, always (the paired-only kernels, LS = 3: no unpaired loop in the kernel).
 __device__ __forceinline__ f3 trace_sample(const RenderParams& P, bool valid, int x, int y, int s, int64_t aov,
-                                          float* park) {
+                                          float* park, float* park_wave) {
     const SceneView& sc = P.sc;
     RayPre ray = camera_ray(P, valid, x, y, s);
     count_rays<MODE>(P.ray_count, 3, valid && P.max_depth > 0);  // camera rays that reach traversal
     if constexpr (D1) {
+        // the AOV index waits in LDS across the traversal (PARK slots 12-13; kept in registers
+        // it was spilled to scratch in the 64-VGPR build)
+        const Park pk{park_wave};
+        pk.put(12, __int_as_float((int32_t)aov));
+        pk.put(13, __int_as_float((int32_t)(aov >> 32)));
+        Park::fence();
         HitState hs;
         traverse<MODE>(sc, ray, valid, false, 0.0f, hs);
+        Park::fence();
+        aov = (int64_t)(uint32_t)__float_as_int(pk.get(12)) | ((int64_t)__float_as_int(pk.get(13)) << 32);
         RT_PHASE(P, x, y, 0);
 #ifdef RT_STATS
         if constexpr (MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0) {
@@ -1438,7 +1457,7 @@ __device__ __forceinline__ f3 trace_sample(const RenderParams& P, bool valid, in
                 P.hit_t[aov] = hs.slot >= 0 ? hs.bestT : -1.0f;
             }
         }
-        return shade_d1<MODE>(P, valid, ray, hs, park);
+        return shade_d1<MODE>(P, valid, ray, hs, park_wave);
     }
     uint32_t rng = make_rng_seed(x, y, s);
 
@@ -2321,7 +2340,8 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, ui
         // it, or addresses made from it, live (and spilled) across the shading.
         if (s == 0) kpix[t >> P.spp_log2] = pix;
         const int64_t aov = valid && P.hit_idx ? (int64_t)pix * P.spp + s : -1;
-        const f3 c = trace_sample<MODE, D1, LS == 3 ? 2 : (LS == 1 ? 1 : 0)>(P, valid, x, y, s, aov, park + t);
+        const f3 c = trace_sample<MODE, D1, LS == 3 ? 2 : (LS == 1 ? 1 : 0)>(P, valid, x, y, s, aov, park + t,
+                                                                             park + (wv << 6));
         RT_PHASE(P, x, r, 1);
         // The thread index again, from the wave's index and a lane id the compiler cannot
         // merge with the first one (mbcnt of a zero read back from LDS): keeping t itself live
@@ -2383,7 +2403,7 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, uin
     f3 acc = mk(0.f, 0.f, 0.f);
     for (int s = 0; s < P.spp; ++s) {
         const int64_t aov = valid && P.hit_idx ? ((int64_t)r * P.W + x) * P.spp + s : -1;
-        acc = add(acc, trace_sample<MODE, D1>(P, valid, x, y, s, aov, park + tid));
+        acc = add(acc, trace_sample<MODE, D1>(P, valid, x, y, s, aov, park + tid, park + (uni((uint32_t)tid) & ~63u)));
     }
     if (valid) {
         const float fs = (float)P.spp;

@@ -122,19 +122,21 @@ __host__ __device__ __forceinline__ RayPre make_ray_mt(f3 o, f3 d) { return make
 // per axis inv = 1.0/double(dir), tNear/tFar = (double(bound) - double(orig)) * inv,
 // reference compare/swap order.  The boolean equals the reference's early-return form
 // because t0 only grows and t1 only shrinks.
+template <bool LOCAL = false>
 __host__ __device__ inline bool box_hit_exact(const RayPre& r, const BoxP& b, double tmin, double tmax) {
     double t0 = tmin, t1 = tmax;
     // No register-pinning asm here: an empty asm "+v" on o/d (to keep the compiler from hoisting
     // double(o) and 1/double(d) out of the traversal loops) measured no faster and, in the 6-wave
     // build, exposed a miscompile of the bounce and binary-record kernels (golden parity failures;
     // DESIGN.md §7).
-#if defined(__HIP_DEVICE_COMPILE__) && defined(RT_EXACT_LOCAL)
-    // Hoisted out of a traversal loop, double(o) and 1/double(d) hold 12 VGPRs across the whole
-    // loop for a test only ambiguous lanes reach (a few % of box tests).  An opaque SGPR zero,
-    // made here (inside the wave-uniform branch that calls this), ORed into the float bits ties
-    // them to this call, so they are recomputed per exact test instead.
+    // LOCAL: hoisted out of a traversal loop, double(o) and 1/double(d) hold 12 VGPRs across
+    // the whole loop for a test only ambiguous lanes reach (a few % of box tests).  An opaque
+    // SGPR zero, made here (inside the wave-uniform branch that calls this), ORed into the float
+    // bits ties them to this call, so they are recomputed per exact test instead (the c3 kernel
+    // then has no scratch; c5's big-scene kernel, with 30x more exact tests, keeps the hoist).
+#if defined(__HIP_DEVICE_COMPILE__)
     uint32_t oz = 0;
-    asm volatile("" : "+s"(oz));
+    if constexpr (LOCAL) asm volatile("" : "+s"(oz));
     const float o[3] = {__uint_as_float(__float_as_uint(r.o.x) | oz), __uint_as_float(__float_as_uint(r.o.y) | oz),
                         __uint_as_float(__float_as_uint(r.o.z) | oz)};
     const float d[3] = {__uint_as_float(__float_as_uint(r.d.x) | oz), __uint_as_float(__float_as_uint(r.d.y) | oz),

@@ -115,6 +115,13 @@ struct RenderParams {
     int32_t half_waves;                               // samples kernel: lanes >= 64 >> half_waves idle
     int32_t paired_only;                              // multi-bounce, half waves, one light: LS = 3 kernels
     int32_t regen;                                    // ... with path regeneration: LS = 4 kernels (full-wave items)
+    // Fused frames (RT_FUSED): the render kernel runs the frame's cull and cut passes itself
+    // (fused_prepass), so a frame is one launch on one stream.  fclaim: per-unit claim words
+    // (a unit is taken by the wave whose atomic max raises its word to fepoch, this frame's
+    // number), fepoch > every earlier frame's.
+    int32_t fused;
+    uint32_t fepoch;
+    uint32_t* fclaim;
     int32_t tile_order;                               // RT_TILES_*
     int32_t spp_log2, tile_w_log2;                    // samples kernel: both powers of two
     int32_t cull;                                     // tile culling against the root box
@@ -1780,7 +1787,8 @@ constexpr int NCLASS_D1 = 3;
 constexpr int HEAVY_SLOT0 = 9;
 constexpr int CUT_SLOT0 = HEAVY_SLOT0 + 8 * NCLASS;  // then 8: lengths of the cut pass's survivor lists
 constexpr int HEAD_SLOT0 = CUT_SLOT0 + 8;  // then 8: the render kernel's work-queue heads (one per XCD)
-constexpr int COUNTER_SLOTS = HEAD_SLOT0 + 8;
+constexpr int FDONE_SLOT0 = HEAD_SLOT0 + 8;  // fused frames: 8 cull-done then 8 cut-done counters
+constexpr int COUNTER_SLOTS = FDONE_SLOT0 + 16;
 constexpr int COUNTER_SET_U32 = COUNTER_SLOTS * COUNTER_STRIDE;
 __host__ __device__ constexpr int heavy_counter(int k, int q) { return (HEAVY_SLOT0 + 8 * k + q) * COUNTER_STRIDE; }
 __device__ __forceinline__ int queue_of_tile(const RenderParams& P, int tile) {
@@ -1858,14 +1866,8 @@ __device__ __forceinline__ void append_live(const RenderParams& P, bool live, in
     }
 }
 
-// Pass 1, one lane per tile: the root test; the survivors go to the live lists.
-__global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
-    __builtin_amdgcn_s_setprio(3);  // ahead of the previous frame's render waves (see Launch)
-    const int tile = (int)(blockIdx.x * BLOCK + threadIdx.x);
-    // Counter sets rotate over three frames (no reset launch): this frame's set was zeroed by
-    // the previous frame's pass; zero the next frame's (its last user, frame k-2, has finished:
-    // the scene's prep stream waited for it).
-    if (blockIdx.x == 0 && threadIdx.x < COUNTER_SLOTS) P.next_count[threadIdx.x * COUNTER_STRIDE] = 0u;
+// The root test of one tile per lane (tiles past the end: no-ops); survivors to the live lists.
+__device__ __forceinline__ void cull_tiles(const RenderParams& P, int tile) {
     bool live = false;
     if (tile < P.tiles_total) {
         const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
@@ -1876,6 +1878,16 @@ __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
         else live = true;
     }
     append_live(P, live, tile);
+}
+
+// Pass 1, one lane per tile: the root test; the survivors go to the live lists.
+__global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
+    __builtin_amdgcn_s_setprio(3);  // ahead of the previous frame's render waves (see Launch)
+    // Counter sets rotate over three frames (no reset launch): this frame's set was zeroed by
+    // the previous frame's pass; zero the next frame's (its last user, frame k-2, has finished:
+    // the scene's prep stream waited for it).
+    if (blockIdx.x == 0 && threadIdx.x < COUNTER_SLOTS) P.next_count[threadIdx.x * COUNTER_STRIDE] = 0u;
+    cull_tiles(P, (int)(blockIdx.x * BLOCK + threadIdx.x));
 }
 
 // Pass 2 (sc.ncut > 0), one wave per CUT_GROUP consecutive slots of a live list, one lane
@@ -1890,11 +1902,10 @@ __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
 #define RT_CUT_GROUP 8
 #endif
 constexpr int CUT_GROUP = RT_CUT_GROUP;
-__global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
-    __builtin_amdgcn_s_setprio(3);
-    const uint32_t lane = lane_id();
-    const int waves = (int)(gridDim.x * (BLOCK / 64));
-    int n = 0, max_len = 0;
+// The cut pass's test condition and this lane's box of the cut (loaded once per wave).
+__device__ __forceinline__ bool cut_setup(const RenderParams& P, uint32_t lane, float* box, int& max_len) {
+    int n = 0;
+    max_len = 0;
     for (int k = 0; k < P.nqueues; ++k) {
         const int l = (int)ldc_u32(&P.live_count[k * COUNTER_STRIDE]);
         n += l;
@@ -1904,86 +1915,102 @@ __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
     // view and the cut rarely removes one (c5's heightfield: none of 739,248): flags 0, no
     // tests (a speed choice only: keeping a tile is always exact).
     const bool test = P.cut_force || 4 * (int64_t)n <= (int64_t)P.tiles_total;
-    // this lane's box of the cut, loaded once
-    float box[6] = {0.f, 0.f, 0.f, -1.f, -1.f, -1.f};
     if (test && (int)lane < P.sc.ncut) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) box[i] = P.sc.cut[6 * (size_t)lane + i];
     }
+    return test;
+}
+
+// One unit of the cut pass: group g (CUT_GROUP consecutive slots) of live list q; false when
+// the group is past the list's end.
+__device__ __forceinline__ bool cut_unit(const RenderParams& P, uint32_t lane, int q, int g, bool test,
+                                         const float* box) {
+    const int len = (int)ldc_u32(&P.live_count[q * COUNTER_STRIDE]);
+    if (CUT_GROUP * g >= len) return false;
+    const int m = min(CUT_GROUP, len - CUT_GROUP * g);
+    const size_t slot0 = (size_t)q * P.queue_cap + (size_t)(CUT_GROUP * g);
+    const int my_tile = (int)lane < m ? P.live_tiles[slot0 + lane] : -1;
+    // the tile's last render cost, loaded before the tests so the load overlaps them
+    uint2 cost = make_uint2(0u, 0u);
+    if (P.heavy_cap > 0 && (int)lane < m) cost = *reinterpret_cast<const uint2*>(P.tile_cost + 4 * (size_t)my_tile);
+    uint64_t culled = 0;
+    for (int j = 0; test && j < m; ++j) {
+        const int tile = (int)rdlane((uint32_t)my_tile, (uint32_t)j);
+        const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        const int xa = tx * P.tile_w, ra = ty * P.tile_h;
+        const int xb = min(xa + P.tile_w, P.W) - 1, rb = min(ra + P.tile_h, P.rows) - 1;
+        const TileDirsF T = tile_dirs_f(P, xa, xb, global_row(P, ra), global_row(P, rb));
+        const bool hit = (int)lane < P.sc.ncut && !tile_misses_box_f(T, box);
+#ifdef RT_WAVE_TIMES
+        {
+            const uint64_t hm = ballot(hit);
+            if (g_cut_counts && lane == 0) g_cut_counts[tile] = __popcll(hm);
+        }
+#endif
+        if (ballot(hit) == 0) {
+            write_culled_tile(P, tile, (int)lane, 64);
+            culled |= 1ull << j;
+        }
+    }
+    // Heavy-first: a surviving tile whose last render took >= heavy_ticks[c] goes to list q's
+    // class-c heavy list, the others to its survivor list (the render kernel's normal part).
+    // The appends take one vector atomic, lane k adding class k's count (lane NCLASS the
+    // survivors'), so a group pays one round trip for them.
+    int cls = -1;  // -1: no tile, or culled
+    if ((int)lane < m && !((culled >> lane) & 1ull)) {
+        cls = NCLASS;
+        if (P.heavy_cap > 0) {
+            const uint32_t mx = max(max(cost.x & 0xffffu, cost.x >> 16), max(cost.y & 0xffffu, cost.y >> 16));
+            for (int k = NCLASS - 1; k >= 0; --k)
+                if (mx >= P.heavy_ticks[k]) cls = k;
+        }
+    }
+    uint64_t cm[NCLASS + 1];
+    uint32_t add = 0;
+#pragma unroll
+    for (int k = 0; k <= NCLASS; ++k) {
+        cm[k] = ballot(cls == k);
+        if ((int)lane == k) add = (uint32_t)__popcll(cm[k]);
+    }
+    const uint64_t below = (1ull << lane) - 1;
+    if (ballot(add != 0) != 0) {
+        uint32_t base = 0;
+        if ((int)lane <= NCLASS && add != 0)
+            base = atomicAdd(&P.live_count[(int)lane < NCLASS ? heavy_counter((int)lane, q) : (CUT_SLOT0 + q) * COUNTER_STRIDE], add);
+        bool spill = false;  // a heavy tile past its list's capacity goes to the survivor list
+#pragma unroll
+        for (int k = 0; k <= NCLASS; ++k) {
+            const uint32_t idx = rdlane(base, (uint32_t)k) + (uint32_t)__popcll(cm[k] & below);
+            if (cls == k) {
+                if (k == NCLASS) P.cut_tiles[(size_t)q * P.queue_cap + idx] = my_tile;
+                else if (idx < (uint32_t)P.heavy_cap) P.heavy_tiles[((size_t)k * 8 + q) * P.heavy_cap + idx] = my_tile;
+                else spill = true;
+            }
+        }
+        const uint64_t sm = ballot(spill);
+        if (sm != 0) {  // rare: a full heavy list
+            const uint32_t leader = (uint32_t)__builtin_ctzll(sm);
+            uint32_t b2 = 0;
+            if (lane == leader) b2 = atomicAdd(&P.live_count[(CUT_SLOT0 + q) * COUNTER_STRIDE], (uint32_t)__popcll(sm));
+            if (spill) P.cut_tiles[(size_t)q * P.queue_cap + rdlane(b2, leader) + (uint32_t)__popcll(sm & below)] = my_tile;
+        }
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t lane = lane_id();
+    const int waves = (int)(gridDim.x * (BLOCK / 64));
+    float box[6] = {0.f, 0.f, 0.f, -1.f, -1.f, -1.f};
+    int max_len;
+    const bool test = cut_setup(P, lane, box, max_len);
     // (list q, group g) pairs, lists interleaved, each wave from its own index on
     for (int p = (int)(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64);; p += waves) {
         const int q = p % P.nqueues, g = p / P.nqueues;
         if (CUT_GROUP * g >= max_len) break;
-        const int len = (int)ldc_u32(&P.live_count[q * COUNTER_STRIDE]);
-        if (CUT_GROUP * g >= len) continue;
-        const int m = min(CUT_GROUP, len - CUT_GROUP * g);
-        const size_t slot0 = (size_t)q * P.queue_cap + (size_t)(CUT_GROUP * g);
-        const int my_tile = (int)lane < m ? P.live_tiles[slot0 + lane] : -1;
-        // the tile's last render cost, loaded before the tests so the load overlaps them
-        uint2 cost = make_uint2(0u, 0u);
-        if (P.heavy_cap > 0 && (int)lane < m) cost = *reinterpret_cast<const uint2*>(P.tile_cost + 4 * (size_t)my_tile);
-        uint64_t culled = 0;
-        for (int j = 0; test && j < m; ++j) {
-            const int tile = (int)rdlane((uint32_t)my_tile, (uint32_t)j);
-            const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-            const int xa = tx * P.tile_w, ra = ty * P.tile_h;
-            const int xb = min(xa + P.tile_w, P.W) - 1, rb = min(ra + P.tile_h, P.rows) - 1;
-            const TileDirsF T = tile_dirs_f(P, xa, xb, global_row(P, ra), global_row(P, rb));
-            const bool hit = (int)lane < P.sc.ncut && !tile_misses_box_f(T, box);
-#ifdef RT_WAVE_TIMES
-            {
-                const uint64_t hm = ballot(hit);
-                if (g_cut_counts && lane == 0) g_cut_counts[tile] = __popcll(hm);
-            }
-#endif
-            if (ballot(hit) == 0) {
-                write_culled_tile(P, tile, (int)lane, 64);
-                culled |= 1ull << j;
-            }
-        }
-        // Heavy-first: a surviving tile whose last render took >= heavy_ticks[c] goes to list q's
-        // class-c heavy list, the others to its survivor list (the render kernel's normal part).
-        // The appends take one vector atomic, lane k adding class k's count (lane NCLASS the
-        // survivors'), so a group pays one round trip for them.
-        int cls = -1;  // -1: no tile, or culled
-        if ((int)lane < m && !((culled >> lane) & 1ull)) {
-            cls = NCLASS;
-            if (P.heavy_cap > 0) {
-                const uint32_t mx = max(max(cost.x & 0xffffu, cost.x >> 16), max(cost.y & 0xffffu, cost.y >> 16));
-                for (int k = NCLASS - 1; k >= 0; --k)
-                    if (mx >= P.heavy_ticks[k]) cls = k;
-            }
-        }
-        uint64_t cm[NCLASS + 1];
-        uint32_t add = 0;
-#pragma unroll
-        for (int k = 0; k <= NCLASS; ++k) {
-            cm[k] = ballot(cls == k);
-            if ((int)lane == k) add = (uint32_t)__popcll(cm[k]);
-        }
-        const uint64_t below = (1ull << lane) - 1;
-        if (ballot(add != 0) != 0) {
-            uint32_t base = 0;
-            if ((int)lane <= NCLASS && add != 0)
-                base = atomicAdd(&P.live_count[(int)lane < NCLASS ? heavy_counter((int)lane, q) : (CUT_SLOT0 + q) * COUNTER_STRIDE], add);
-            bool spill = false;  // a heavy tile past its list's capacity goes to the survivor list
-#pragma unroll
-            for (int k = 0; k <= NCLASS; ++k) {
-                const uint32_t idx = rdlane(base, (uint32_t)k) + (uint32_t)__popcll(cm[k] & below);
-                if (cls == k) {
-                    if (k == NCLASS) P.cut_tiles[(size_t)q * P.queue_cap + idx] = my_tile;
-                    else if (idx < (uint32_t)P.heavy_cap) P.heavy_tiles[((size_t)k * 8 + q) * P.heavy_cap + idx] = my_tile;
-                    else spill = true;
-                }
-            }
-            const uint64_t sm = ballot(spill);
-            if (sm != 0) {  // rare: a full heavy list
-                const uint32_t leader = (uint32_t)__builtin_ctzll(sm);
-                uint32_t b2 = 0;
-                if (lane == leader) b2 = atomicAdd(&P.live_count[(CUT_SLOT0 + q) * COUNTER_STRIDE], (uint32_t)__popcll(sm));
-                if (spill) P.cut_tiles[(size_t)q * P.queue_cap + rdlane(b2, leader) + (uint32_t)__popcll(sm & below)] = my_tile;
-            }
-        }
+        (void)cut_unit(P, lane, q, g, test, box);
     }
 }
 
@@ -2422,6 +2449,86 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, uin
     }
 }
 
+// ---- fused frames: the pre-passes inside the render kernel ----------------------------
+// A frame is one launch: every wave of the persistent grid first takes units of the cull pass
+// (64 tiles, one per lane), then, once all are done, units of the cut pass (a group of one
+// live list), then renders.  Units are claimed (fclaim) so any running wave can take a unit
+// another has not started: the waits depend only on units held by running waves, never on a
+// block that is not resident (a grid barrier would hang when the grid is not all resident,
+// e.g. two processes sharing a GPU).  Completion: per-unit adds to 8 counters (unit & 7), a
+// release before each add and an acquire after the wait (the lists are written and read on
+// different XCDs; the render phase reads them with scalar loads no wave made before the wait).
+__device__ __forceinline__ bool fused_claim(const RenderParams& P, uint32_t u, uint32_t lane) {
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_max(P.fclaim + u, P.fepoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return uni(old) < P.fepoch;
+}
+__device__ __forceinline__ void fused_done(const RenderParams& P, int slot0, uint32_t u, uint32_t lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (lane == 0)
+        __hip_atomic_fetch_add(P.live_count + (slot0 + (int)(u & 7u)) * COUNTER_STRIDE, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wait until `n` units of the phase counted at slot0 are done; meanwhile (after a few polls)
+// take any unit [0, nunits) nobody has claimed (claim words at base).  Bounded: a frame whose
+// wait ran out would be wrong, never a hung GPU.
+template <typename F>
+__device__ __forceinline__ void fused_wait(const RenderParams& P, int slot0, uint32_t n, uint32_t nunits,
+                                           uint32_t base, uint32_t lane, F work) {
+    for (uint32_t it = 0; it < (1u << 22); ++it) {
+        uint32_t sum = 0;
+        if (lane == 0)
+            for (int i = 0; i < 8; ++i)
+                sum += __hip_atomic_load(P.live_count + (slot0 + i) * COUNTER_STRIDE, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+        if (uni(sum) >= n) break;
+        if (it >= 16 && (it & 255) == 16) {  // rescue: units still unclaimed
+            for (uint32_t u0 = 0; u0 < nunits; u0 += 64) {
+                const uint32_t u = u0 + lane;
+                const bool open = u < nunits && __hip_atomic_load(P.fclaim + base + u, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT) < P.fepoch;
+                for (uint64_t m = ballot(open); m != 0; m &= m - 1) {
+                    const uint32_t v = u0 + (uint32_t)__builtin_ctzll(m);
+                    if (fused_claim(P, base + v, lane)) work(v);
+                }
+            }
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+__device__ __forceinline__ void fused_prepass(const RenderParams& P) {
+    const uint32_t lane = lane_id();
+    const uint32_t W = gridDim.x * (BLOCK / 64);
+    const uint32_t w = blockIdx.x * (BLOCK / 64) + (uni((uint32_t)threadIdx.x) >> 6);
+    // the next frame's counters (its previous user, frame k-2, has finished: same stream)
+    if (blockIdx.x == 0 && threadIdx.x < COUNTER_SLOTS) P.next_count[threadIdx.x * COUNTER_STRIDE] = 0u;
+    const uint32_t nC = (uint32_t)(P.tiles_total + 63) / 64u;
+    auto cull_u = [&](uint32_t u) {
+        cull_tiles(P, (int)(u * 64u + lane));
+        fused_done(P, FDONE_SLOT0, u, lane);
+    };
+    for (uint32_t u = w; u < nC; u += W)
+        if (fused_claim(P, u, lane)) cull_u(u);
+    fused_wait(P, FDONE_SLOT0, nC, nC, 0u, lane, cull_u);
+    if (P.sc.ncut > 0) {
+        float box[6] = {0.f, 0.f, 0.f, -1.f, -1.f, -1.f};
+        int max_len;
+        const bool test = cut_setup(P, lane, box, max_len);
+        const uint32_t nq = (uint32_t)P.nqueues;
+        const uint32_t nU = nq * (uint32_t)((max_len + CUT_GROUP - 1) / CUT_GROUP);
+        uint32_t nK = 0;  // the groups that exist (a list shorter than max_len has holes)
+        for (int q = 0; q < P.nqueues; ++q)
+            nK += ((uint32_t)ldc_u32(&P.live_count[q * COUNTER_STRIDE]) + CUT_GROUP - 1) / CUT_GROUP;
+        auto cut_u = [&](uint32_t p) {
+            if (cut_unit(P, lane, (int)(p % nq), (int)(p / nq), test, box)) fused_done(P, FDONE_SLOT0 + 8, p, lane);
+        };
+        for (uint32_t p = w; p < nU; p += W)
+            if (fused_claim(P, nC + p, lane)) cut_u(p);
+        fused_wait(P, FDONE_SLOT0 + 8, nK, nU, nC, lane, cut_u);
+    }
+}
+
 // A persistent grid (the blocks one dispatch keeps resident) over per-XCD work queues: block b
 // serves queue g = b % 8 (dispatch deals blocks round-robin over the XCDs, so queue g is served
 // on XCD g and list g's tiles share an L2).  With 8 lists queue g is list g; with one list
@@ -2471,6 +2578,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
     // the wave's index in the block as a uniform value (threadIdx.x itself, kept live to the
     // tile-cost write at the end, was spilled to scratch)
     const uint32_t wv = uni((uint32_t)threadIdx.x) >> 6;
+#ifdef RT_EXP_FUSED
+    if (P.fused) fused_prepass(P);
+#endif
     // The first item of each wave (block) is its place in the grid, the rest come from the
     // queue after those: 900 dequeues per head at once when the grid starts took ~10 us to serve.
     for (bool first = true;; first = false) {
@@ -3050,6 +3160,10 @@ struct rt_scene {
     // so frame k's pre-passes overlap frame k-1's render kernel (its tail leaves CUs idle).
     static constexpr int kRing = 256;
     hipEvent_t ev0[kRing] = {}, evm[kRing] = {}, ev1[kRing] = {}, pdone[kRing] = {};
+    // fused frames (RT_FUSED): one launch, timed ev0 -> ev1 (no evm / pdone); claim words
+    bool fused[kRing] = {};
+    DevBuf fclaim;
+    uint32_t fepoch = 0;
     // evq: recorded on the caller's stream at the start of a frame; the prep stream waits for it
     // so the pre-passes (which write the culled tiles' pixels into the caller's buffers) come
     // after everything the caller queued on that stream before the call.  A caller that orders
@@ -3750,7 +3864,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             // the render kernel's time, or the frame period when shorter (overlapping frames:
             // RT_FLAG_OVERLAP starts a kernel while the previous one still runs)
             float ms = 0.f, period = 0.f;
-            if (hipEventElapsedTime(&ms, s->evm[fl], s->ev1[fl]) == hipSuccess) {
+            if (hipEventElapsedTime(&ms, s->fused[fl] ? s->ev0[fl] : s->evm[fl], s->ev1[fl]) == hipSuccess) {
                 const int f0 = int(uint64_t(last - 1) % rt_scene::kRing);
                 if (last >= 1 && hipEventElapsedTime(&period, s->ev1[f0], s->ev1[fl]) == hipSuccess && period > 0.f)
                     ms = std::min(ms, period);
@@ -3829,7 +3943,44 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         const char* e = std::getenv("RT_CUT_BLOCKS_PER_CU");
         return e ? std::max(1, std::atoi(e)) : 4;
     }();
+    // Fused frames (A/B, RT_FUSED=1): the render kernel runs the cull and cut passes itself
+    // (fused_prepass): one launch per frame on the caller's stream, no prep stream, no
+    // cross-stream wait.
+    bool fused = false;
+#ifdef RT_EXP_FUSED
+    if (const char* e = std::getenv("RT_FUSED")) fused = std::atoi(e) != 0 && !s->deep;
+#endif
+    if (fused) {
+        const size_t nC = (size_t(P.tiles_total) + 63) / 64;
+        const size_t need = (nC + size_t(P.nqueues) * ((size_t(P.queue_cap) + CUT_GROUP - 1) / CUT_GROUP)) * sizeof(uint32_t);
+        if (s->fclaim.n < need) {
+            if (k > 0) HIP_TRY(hipEventSynchronize(ev1_of(k - 1)));
+            if ((rc = s->fclaim.alloc(need)) != RT_OK) return rc;
+            HIP_TRY(hipMemset(s->fclaim.p, 0, need));
+        }
+        P.fused = 1;
+        P.fepoch = ++s->fepoch;
+        P.fclaim = static_cast<uint32_t*>(s->fclaim.p);
+    }
+    s->fused[slot] = fused;
     auto frame = [&]() -> int {
+        if (fused) {
+            if (s->counters_dirty) {
+                HIP_TRY(hipMemsetAsync(base, 0, rt_scene::kSets * kCounterBytes, st));
+                s->counters_dirty = false;
+            }
+            if (cost_reset) HIP_TRY(hipMemsetAsync(s->cost.p, 0, s->cost.n, st));
+            static const size_t big_bytes_f = [] {
+                const char* e = std::getenv("RT_BIG_SCENE_BYTES");
+                return e ? (size_t)std::strtoull(e, nullptr, 10) : kBigSceneBytes;
+            }();
+            const Launch L{st, s->ev0[slot], s->ev1[slot], s->cus, s->bytes > big_bytes_f, &s->last_kernel};
+            if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, L);
+            else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, L);
+            else launch<RT_KERNEL_WAVE>(P, samples, L);
+            HIP_TRY(hipGetLastError());
+            return RT_OK;
+        }
         hipStream_t pp = same_stream ? st : s->prep;
         // set k was last read by frame k-3, set k+1 (zeroed by this cull pass) by frame k-2
         if (k >= 2 && !same_stream) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 2), 0));
@@ -3903,8 +4054,12 @@ int event_times(const rt_scene* s, int what, float* ms_out, int max, int* n_out)
         const int slot = int((s->launches - uint64_t(n) + uint64_t(k)) % rt_scene::kRing);
         HIP_TRY(hipEventSynchronize(s->ev1[slot]));
         float kern = 0.f, prep = 0.f;
-        if (what != 1) HIP_TRY(hipEventElapsedTime(&kern, s->evm[slot], s->ev1[slot]));
-        if (what != 0) HIP_TRY(hipEventElapsedTime(&prep, s->ev0[slot], s->pdone[slot]));
+        if (s->fused[slot]) {  // one launch: its span is the kernel and the frame, no separate pre-pass
+            if (what != 1) HIP_TRY(hipEventElapsedTime(&kern, s->ev0[slot], s->ev1[slot]));
+        } else {
+            if (what != 1) HIP_TRY(hipEventElapsedTime(&kern, s->evm[slot], s->ev1[slot]));
+            if (what != 0) HIP_TRY(hipEventElapsedTime(&prep, s->ev0[slot], s->pdone[slot]));
+        }
         ms_out[k] = kern + prep;
     }
     if (n_out) *n_out = n;

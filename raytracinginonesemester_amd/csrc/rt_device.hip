@@ -1787,8 +1787,9 @@ constexpr int NCLASS_D1 = 3;
 constexpr int HEAVY_SLOT0 = 9;
 constexpr int CUT_SLOT0 = HEAVY_SLOT0 + 8 * NCLASS;  // then 8: lengths of the cut pass's survivor lists
 constexpr int HEAD_SLOT0 = CUT_SLOT0 + 8;  // then 8: the render kernel's work-queue heads (one per XCD)
-constexpr int FDONE_SLOT0 = HEAD_SLOT0 + 8;  // fused frames: 8 cull-done then 8 cut-done counters
-constexpr int COUNTER_SLOTS = FDONE_SLOT0 + 16;
+// fused frames: per phase (cull, then cut) 8 unit counters, a counter of completed ones, a flag
+constexpr int FDONE_SLOT0 = HEAD_SLOT0 + 8;
+constexpr int COUNTER_SLOTS = FDONE_SLOT0 + 20;
 constexpr int COUNTER_SET_U32 = COUNTER_SLOTS * COUNTER_STRIDE;
 __host__ __device__ constexpr int heavy_counter(int k, int q) { return (HEAVY_SLOT0 + 8 * k + q) * COUNTER_STRIDE; }
 __device__ __forceinline__ int queue_of_tile(const RenderParams& P, int tile) {
@@ -2463,26 +2464,38 @@ __device__ __forceinline__ bool fused_claim(const RenderParams& P, uint32_t u, u
     if (lane == 0) old = __hip_atomic_fetch_max(P.fclaim + u, P.fepoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return uni(old) < P.fepoch;
 }
-__device__ __forceinline__ void fused_done(const RenderParams& P, int slot0, uint32_t u, uint32_t lane) {
+// A unit is done: a release, then one add to counter (unit & 7) of the phase; the wave whose add
+// completes its counter (all units u with u & 7 == i) adds to the phase's ninth counter, and the
+// wave completing that one raises the phase flag.  Waiters poll the flag word only.
+// expect: the units counter (u & 7) receives in this phase; nz: the counters that receive any.
+__device__ __forceinline__ void fused_done(const RenderParams& P, int slot0, uint32_t u, uint32_t expect, uint32_t nz,
+                                           uint32_t lane) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    if (lane == 0)
-        __hip_atomic_fetch_add(P.live_count + (slot0 + (int)(u & 7u)) * COUNTER_STRIDE, 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+        const uint32_t i = u & 7u;
+        const uint32_t c = __hip_atomic_fetch_add(P.live_count + (slot0 + (int)i) * COUNTER_STRIDE, 1u, __ATOMIC_ACQ_REL,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        if (c + 1u == expect) {
+            const uint32_t d = __hip_atomic_fetch_add(P.live_count + (slot0 + 8) * COUNTER_STRIDE, 1u, __ATOMIC_ACQ_REL,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            if (d + 1u == nz)
+                __hip_atomic_store(P.live_count + (slot0 + 9) * COUNTER_STRIDE, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
-// Wait until `n` units of the phase counted at slot0 are done; meanwhile (after a few polls)
-// take any unit [0, nunits) nobody has claimed (claim words at base).  Bounded: a frame whose
-// wait ran out would be wrong, never a hung GPU.
+// Wait for the phase flag at slot0 + 9; a phase of n == 0 units is done at once.  After a long
+// wait (a grid not all resident: its unclaimed units), take any unit [0, nunits) nobody has
+// claimed (claim words at base).  Bounded: a frame whose wait ran out would be wrong, never a
+// hung GPU.
 template <typename F>
 __device__ __forceinline__ void fused_wait(const RenderParams& P, int slot0, uint32_t n, uint32_t nunits,
                                            uint32_t base, uint32_t lane, F work) {
-    for (uint32_t it = 0; it < (1u << 22); ++it) {
-        uint32_t sum = 0;
+    for (uint32_t it = 0; n > 0 && it < (1u << 20); ++it) {
+        uint32_t f = 0;
         if (lane == 0)
-            for (int i = 0; i < 8; ++i)
-                sum += __hip_atomic_load(P.live_count + (slot0 + i) * COUNTER_STRIDE, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-        if (uni(sum) >= n) break;
-        if (it >= 16 && (it & 255) == 16) {  // rescue: units still unclaimed
+            f = __hip_atomic_load(P.live_count + (slot0 + 9) * COUNTER_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (uni(f) != 0) break;
+        if (it >= 512 && (it & 511) == 0) {  // rescue (not reached when the grid is all resident)
             for (uint32_t u0 = 0; u0 < nunits; u0 += 64) {
                 const uint32_t u = u0 + lane;
                 const bool open = u < nunits && __hip_atomic_load(P.fclaim + base + u, __ATOMIC_RELAXED,
@@ -2493,7 +2506,7 @@ __device__ __forceinline__ void fused_wait(const RenderParams& P, int slot0, uin
                 }
             }
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(8);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
@@ -2506,7 +2519,7 @@ __device__ __forceinline__ void fused_prepass(const RenderParams& P) {
     const uint32_t nC = (uint32_t)(P.tiles_total + 63) / 64u;
     auto cull_u = [&](uint32_t u) {
         cull_tiles(P, (int)(u * 64u + lane));
-        fused_done(P, FDONE_SLOT0, u, lane);
+        fused_done(P, FDONE_SLOT0, u, nC / 8u + ((u & 7u) < nC % 8u ? 1u : 0u), nC < 8u ? nC : 8u, lane);
     };
     for (uint32_t u = w; u < nC; u += W)
         if (fused_claim(P, u, lane)) cull_u(u);
@@ -2520,12 +2533,25 @@ __device__ __forceinline__ void fused_prepass(const RenderParams& P) {
         uint32_t nK = 0;  // the groups that exist (a list shorter than max_len has holes)
         for (int q = 0; q < P.nqueues; ++q)
             nK += ((uint32_t)ldc_u32(&P.live_count[q * COUNTER_STRIDE]) + CUT_GROUP - 1) / CUT_GROUP;
+        // completion counter p & 7: with 8 lists that is list p % 8 (its groups), with one list
+        // the groups g = p spread evenly
+        uint32_t nzK = 0;
+        if (nq == 8) {
+            for (int q = 0; q < 8; ++q) nzK += ldc_u32(&P.live_count[q * COUNTER_STRIDE]) > 0 ? 1u : 0u;
+        } else {
+            nzK = nK < 8u ? nK : 8u;
+        }
         auto cut_u = [&](uint32_t p) {
-            if (cut_unit(P, lane, (int)(p % nq), (int)(p / nq), test, box)) fused_done(P, FDONE_SLOT0 + 8, p, lane);
+            if (cut_unit(P, lane, (int)(p % nq), (int)(p / nq), test, box)) {
+                const uint32_t i = p & 7u;
+                const uint32_t expect = nq == 8 ? ((uint32_t)ldc_u32(&P.live_count[(int)i * COUNTER_STRIDE]) + CUT_GROUP - 1) / CUT_GROUP
+                                                : nK / 8u + (i < nK % 8u ? 1u : 0u);
+                fused_done(P, FDONE_SLOT0 + 10, p, expect, nzK, lane);
+            }
         };
         for (uint32_t p = w; p < nU; p += W)
             if (fused_claim(P, nC + p, lane)) cut_u(p);
-        fused_wait(P, FDONE_SLOT0 + 8, nK, nU, nC, lane, cut_u);
+        fused_wait(P, FDONE_SLOT0 + 10, nK, nU, nC, lane, cut_u);
     }
 }
 

@@ -114,14 +114,6 @@ struct RenderParams {
     int32_t lane_samples;                             // 1: one sample per lane; else pixel loop
     int32_t half_waves;                               // samples kernel: lanes >= 64 >> half_waves idle
     int32_t paired_only;                              // multi-bounce, half waves, one light: LS = 3 kernels
-    int32_t regen;                                    // ... with path regeneration: LS = 4 kernels (full-wave items)
-    // Fused frames (RT_FUSED): the render kernel runs the frame's cull and cut passes itself
-    // (fused_prepass), so a frame is one launch on one stream.  fclaim: per-unit claim words
-    // (a unit is taken by the wave whose atomic max raises its word to fepoch, this frame's
-    // number), fepoch > every earlier frame's.
-    int32_t fused;
-    uint32_t fepoch;
-    uint32_t* fclaim;
     int32_t tile_order;                               // RT_TILES_*
     int32_t spp_log2, tile_w_log2;                    // samples kernel: both powers of two
     int32_t cull;                                     // tile culling against the root box
@@ -419,15 +411,11 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
     uint32_t st_ref = 0, st_mlo = 0, st_mhi = 0;  // lane k holds entry k
     int sp = 0;
     int stale = 0;  // entries [0, stale) take the pop-time re-test
-    // The record arrays' bases, held in SGPRs for the whole traversal.  Left to itself the
-    // compiler re-reads them from the kernel arguments at every pop (they are cheap to
-    // rematerialise), which puts a dependent scalar load before each record load.
+    // The record arrays' bases (the compiler re-reads them from the kernel arguments at every
+    // pop; holding them in SGPRs measured no faster).
     const char* leaf_b = reinterpret_cast<const char*>(sc.leaf);
     const char* wnode_b = reinterpret_cast<const char*>(sc.wnode);
     const char* ibox_b = reinterpret_cast<const char*>(sc.ibox);
-#ifdef RT_EXP_HOIST_BASE
-    asm volatile("" : "+s"(leaf_b), "+s"(wnode_b), "+s"(ibox_b));
-#endif
     while (true) {
         RT_STAT(2 + so, 1);
 #ifdef RT_STATS
@@ -442,21 +430,6 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                 const uint32_t slot = ref & ~LEAF_BIT;
                 const float4* L = reinterpret_cast<const float4*>(leaf_b + (slot << 6));
                 const bool act = lane_in(mask);
-#ifdef RT_EXP_PREFETCH
-                // A leaf pushes nothing: the entry processed next is the stack top.  Touch its
-                // record (one dword per 64-byte line) with the leaf's loads, so its own load in
-                // the next iteration finds the scalar cache warm; the values are consumed (no
-                // wait) at the end of this iteration.
-                uint32_t pf0 = 0, pf1 = 0;
-                if (sp > 0) {
-                    const uint32_t nref = rdlane(st_ref, sp - 1);
-                    const uint32_t* np = (nref & LEAF_BIT)
-                                             ? reinterpret_cast<const uint32_t*>(leaf_b + ((nref & ~LEAF_BIT) << 6))
-                                             : reinterpret_cast<const uint32_t*>(wnode_b + (nref << 7));
-                    pf0 = ldc_u32(np);
-                    pf1 = (nref & LEAF_BIT) ? 0u : ldc_u32(np + 16);
-                }
-#endif
                 const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2);
                 float t, u, v;
                 const bool h = act && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin,
@@ -470,9 +443,6 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
                     stale = sp;
                     if (any_hit) alive &= ~ballot(h && t < any_hit_dist);
                 }
-#ifdef RT_EXP_PREFETCH
-                asm volatile("" ::"s"(pf0), "s"(pf1));
-#endif
             } else {
                 RT_STAT(8 + so, 1);
                 if constexpr (WIDE) {
@@ -1787,9 +1757,7 @@ constexpr int NCLASS_D1 = 3;
 constexpr int HEAVY_SLOT0 = 9;
 constexpr int CUT_SLOT0 = HEAVY_SLOT0 + 8 * NCLASS;  // then 8: lengths of the cut pass's survivor lists
 constexpr int HEAD_SLOT0 = CUT_SLOT0 + 8;  // then 8: the render kernel's work-queue heads (one per XCD)
-// fused frames: per phase (cull, then cut) 8 unit counters, a counter of completed ones, a flag
-constexpr int FDONE_SLOT0 = HEAD_SLOT0 + 8;
-constexpr int COUNTER_SLOTS = FDONE_SLOT0 + 20;
+constexpr int COUNTER_SLOTS = HEAD_SLOT0 + 8;
 constexpr int COUNTER_SET_U32 = COUNTER_SLOTS * COUNTER_STRIDE;
 __host__ __device__ constexpr int heavy_counter(int k, int q) { return (HEAVY_SLOT0 + 8 * k + q) * COUNTER_STRIDE; }
 __device__ __forceinline__ int queue_of_tile(const RenderParams& P, int tile) {
@@ -2064,267 +2032,6 @@ __device__ __forceinline__ uint32_t dequeue(uint32_t* head, uint32_t lane) {
     return uni(v);
 }
 
-// Pixel and sample of lane-sample lt of a tile in the samples layout (Z-ordered pixels in a
-// square tile, spp consecutive samples per pixel; samples_tile's mapping).
-struct SampleAt {
-    int x, r, y, s, pix;
-    bool valid;
-};
-__device__ __forceinline__ SampleAt sample_at(const RenderParams& P, int tile, int lt) {
-    SampleAt a;
-    a.s = lt & (P.spp - 1);
-    const int pit = lt >> P.spp_log2;
-    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-    int px, py;
-    if (P.tile_w == P.tile_h) {
-        px = (pit & 1) | ((pit >> 1) & 2) | ((pit >> 2) & 4) | ((pit >> 3) & 8);
-        py = ((pit >> 1) & 1) | ((pit >> 2) & 2) | ((pit >> 3) & 4) | ((pit >> 4) & 8);
-    } else {
-        px = pit & (P.tile_w - 1);
-        py = pit >> P.tile_w_log2;
-    }
-    a.x = tx * P.tile_w + px;
-    a.r = ty * P.tile_h + py;
-    a.valid = a.x < P.W && a.r < P.rows;
-    a.y = a.valid ? global_row(P, a.r) : 0;
-    a.pix = a.valid ? a.r * P.W + a.x : -1;
-    return a;
-}
-
-#ifdef RT_RESUME
-// Path regeneration over the resumable paired traversals (one light): a wave owns 64 samples
-// (a 2x2-pixel quad x 16 spp), whose camera rays all 64 lanes trace with the wave DFS first
-// (coherent rays keep the wave-shared stack); each camera hit (bestT, slot) waits in the
-// sample's colour slot of LDS.  Then lanes 0-31 carry paths and lanes 32-63 their shadow rays
-// (paired_bounces_resume): a path lane whose sample has ended writes the sample's colour and
-// takes the wave's next sample, so the path lanes stay busy until the wave's pool is drained,
-// instead of one sample per lane and the wave waiting for its longest path.  Per sample the
-// same rays, tests, arithmetic and order of radiance adds: exact.
-// col: the block's colour slots (3 floats per sample); wbase: this wave's first slot; tile, qw:
-// the work item (its 64 samples are lane-samples qw*64 + k).
-template <int MODE>
-__device__ __forceinline__ void paired_bounces_regen(const RenderParams& P, int tile, uint32_t qw, int wbase,
-                                                     float* col, float* park) {
-    const SceneView& sc = P.sc;
-    const bool upper = lane_id() >= 32;
-    const int max_depth = P.max_depth;
-    uint32_t* stk = reinterpret_cast<uint32_t*>(park);
-    LaneDfs d;
-    d.run = false;
-    d.ref = 0;
-    d.sp = d.stale = 0;
-    d.retest = false;
-    RayPre ray;
-    HitState hs;
-    hs.bestT = FLT_MAX;
-    hs.slot = -1;
-    f3 radiance = mk(0.f, 0.f, 0.f), thr = radiance;
-    uint32_t rng = 0;
-    bool alive = false;
-    int cur = -1;                    // lower lanes: the pool sample this lane's path belongs to
-    int depth = 0;                   // lower lanes: the depth of the path result in hs
-    bool unproc = false;             // lower lanes: hs holds a path result not yet shaded
-    bool need_up = false;            // upper lanes: tracing (or holding the answer of) a shadow ray
-    float dist_up = 0.f;
-    bool pend = false, lit_p = false;
-    f3 thr_p = mk(0.f, 0.f, 0.f), Lo_p = thr_p, Lo_lit_p = thr_p;
-    int taken = 0;  // wave-uniform: pool samples handed out
-    bool finished = false;
-    for (uint32_t guard = 0; guard < (1u << 16); ++guard) {
-        const uint64_t runm = ballot(d.run);
-        const bool ready = !upper && !d.run && !lane_in(runm >> 32);
-        const uint64_t readym = ballot(ready);
-        const bool pready = upper && lane_in(readym << 32);
-        // IsInShadow's answer (shader.h:44-62) of the upper lanes whose pair is ready
-        const uint64_t occ = ballot(pready && need_up && hs.slot >= 0 && hs.bestT < dist_up);
-        if (ready && pend) {
-            const bool occluded = lane_in(occ >> 32);
-            radiance = add(radiance, mul(thr_p, (lit_p && !occluded) ? Lo_lit_p : Lo_p));
-            pend = false;
-        }
-        if (pready) need_up = false;
-        // a path that has ended: its sample's colour (TraceRayIterative's clamp) to its slot
-        if (ready && cur >= 0 && !pend && !unproc && !alive) {
-            const f3 c = clamp01(radiance);
-            float* o = col + 3 * (wbase + cur);
-            o[0] = c.x;
-            o[1] = c.y;
-            o[2] = c.z;
-            cur = -1;
-        }
-        // free path lanes take the pool's next samples, in lane order
-        const bool want = ready && cur < 0;
-        const uint64_t wantm = ballot(want);
-        if (wantm != 0 && taken < 64) {
-            const int k = taken + (int)__popcll(wantm & ((1ull << lane_id()) - 1));
-            if (want && k < 64) {
-                const SampleAt a = sample_at(P, tile, (int)qw * 64 + k);
-                const float* h = col + 3 * (wbase + k);
-                hs.bestT = h[0];
-                hs.slot = __float_as_int(h[1]);
-                ray = camera_ray(P, a.valid, a.x, a.y, a.s);
-                rng = make_rng_seed(a.x, a.y, a.s);
-                thr = mk(1.f, 1.f, 1.f);
-                radiance = mk(0.f, 0.f, 0.f);
-                alive = a.valid && max_depth > 0;
-                depth = 0;
-                unproc = true;
-                cur = k;
-            }
-            taken = min(64, taken + (int)__popcll(wantm));
-        }
-        bool need = false;
-        float dist = 0.f;
-        f3 so = mk(0.f, 0.f, 0.f), sd = so;
-        bool launch = false;  // lower lanes: a new path ray to trace
-        if (ready && unproc) {
-            unproc = false;
-            const bool hit = alive && hs.slot >= 0;
-            if (alive && !hit) {
-                radiance = add(radiance, mul(thr, P.miss));
-                alive = false;
-            }
-            if (hit) {
-                const SurfHit sh = resolve_hit<false>(sc, ray, hs.slot);
-                const DevMaterial m = material_of(sc, sh.tri);
-                const f3 N = unit(sh.n);
-                const f3 V = unit(sub(ray.o, sh.p));
-                f3 Lo = mk(0.f, 0.f, 0.f);
-                Lo = add(Lo, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 0.05f));
-                Lo = add(Lo, mk(m.emission[0], m.emission[1], m.emission[2]));
-                const DevLight& lt = sc.lights[0];
-                const f3 lpos = mk(lt.pos[0], lt.pos[1], lt.pos[2]);
-                f3 contrib = mk(0.f, 0.f, 0.f);
-                bool lit = false;
-                const f3 L = unit(sub(lpos, sh.p));
-                const float NdotL = fmaxf(dot(N, L), 0.0f);
-                if (NdotL > 0.0f) {
-                    const f3 f = eval_brdf(m, sh.n, V, L);
-                    const f3 rad = scale(mk(lt.color[0], lt.color[1], lt.color[2]), (float)lt.intensity);
-                    contrib = scale(mul(rad, f), NdotL);
-                    lit = true;
-                    const f3 toL = sub(lpos, sh.p);
-                    dist = sqrtf(dot(toL, toL));
-                    if (dist > 0.0f) {
-                        need = true;
-                        so = add(sh.p, scale(N, RT_EPS));
-                        sd = divf(toL, dist);
-                    }
-                }
-                thr_p = thr;
-                Lo_p = Lo;
-                Lo_lit_p = add(Lo, contrib);
-                lit_p = lit;
-                pend = true;
-                if (depth + 1 < max_depth) {
-                    const float kd = m.kd, kr = m.kr, total = kd + kr;
-                    if (total <= 0.0f) {
-                        alive = false;
-                    } else {
-                        const f3 Nb = unit(sh.n);
-                        const float xi = rng_next(rng);
-                        if (P.diffuse_bounce && xi < kd / total) {
-                            f3 dd = random_unit_vector(rng);
-                            if (!(dot(dd, Nb) > 0.0f)) dd = mk(-dd.x, -dd.y, -dd.z);
-                            ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), dd, scene_bmax(sc));
-                            const float nl = fmaxf(dot(Nb, dd), 0.0f);
-                            thr = mul(thr, scale(mk(m.albedo[0], m.albedo[1], m.albedo[2]), 2.0f * nl));
-                        } else {
-                            const f3 I = unit(ray.d);
-                            const f3 refl = sub(I, scale(Nb, 2.0f * dot(I, Nb)));
-                            ray = make_ray(add(sh.p, scale(Nb, RT_EPS)), refl, scene_bmax(sc));
-                            thr = mul(thr, scale(mk(m.spec[0], m.spec[1], m.spec[2]), kr));
-                        }
-                        if (thr.x < 1e-4f && thr.y < 1e-4f && thr.z < 1e-4f) alive = false;
-                    }
-                    ++depth;
-                } else {
-                    alive = false;
-                }
-            }
-            launch = alive;
-        }
-        const uint64_t needm = ballot(need);
-        const float ox = __shfl_xor(so.x, 32), oy = __shfl_xor(so.y, 32), oz = __shfl_xor(so.z, 32);
-        const float dx = __shfl_xor(sd.x, 32), dy = __shfl_xor(sd.y, 32), dz = __shfl_xor(sd.z, 32);
-        const float dd = __shfl_xor(dist, 32);
-        bool go = launch;
-        if (pready) {
-            need_up = lane_in(needm << 32);
-            dist_up = dd;
-            if (need_up) ray = make_ray(mk(ox, oy, oz), mk(dx, dy, dz), scene_bmax(sc));
-            go = need_up;
-        }
-        dfs_start(sc, ray, go, hs, d);
-        if (launch) unproc = true;
-        if (ballot(d.run || pend || unproc || cur >= 0) == 0 && taken >= 64) {
-            finished = true;
-            break;
-        }
-        const uint32_t quota = (uint32_t)__popcll(ballot(d.run)) >> RT_RESUME_SHIFT;
-        dfs_run(sc, ray, upper, dist_up, hs, d, stk, quota);
-    }
-    // the guard cannot run out (every iteration ends a traversal or a sample); if it ever did,
-    // the wave's samples are poisoned rather than silently truncated
-    if (!finished && !upper) col[3 * (wbase + (int)lane_id())] = __int_as_float(0x7fc00000);
-}
-
-// One wave item of the regeneration kernels (LS = 4): the camera rays of its 64 samples through
-// the wave DFS, their hits parked in the samples' colour slots, then paired_bounces_regen, then
-// the per-pixel sums in sample order (samples_tile's epilogue).
-template <int MODE>
-__device__ __forceinline__ void regen_tile(const RenderParams& P, int tile, uint32_t qw, int t, float* col, int* kpix,
-                                           float* park, const int* lds_zero) {
-    const uint32_t wv = uni((uint32_t)t) >> 6;
-    const int wbase = (int)(wv << 6);
-    {
-        const SampleAt a = sample_at(P, tile, (int)qw * 64 + (t & 63));
-        if (a.s == 0) kpix[t >> P.spp_log2] = a.pix;
-        const RayPre ray = camera_ray(P, a.valid, a.x, a.y, a.s);
-        HitState hs;
-        traverse<MODE>(P.sc, ray, a.valid && P.max_depth > 0, false, 0.0f, hs);
-        if (a.valid && P.hit_idx) {
-            const int64_t aov = (int64_t)a.pix * P.spp + a.s;
-            const bool hit = P.max_depth > 0 && hs.slot >= 0;
-            P.hit_idx[aov] = hit ? leaf_tri<false>(P.sc, hs.slot) : -1;
-            P.hit_t[aov] = hit ? hs.bestT : -1.0f;
-        }
-        col[3 * t] = hs.bestT;
-        col[3 * t + 1] = __int_as_float(hs.slot);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    paired_bounces_regen<MODE>(P, tile, qw, wbase, col, park + t);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int t2 = (int)((wv << 6) | __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(
-                                             ~0u, (uint32_t)*(const volatile int*)lds_zero)));
-    if ((t2 & (P.spp - 1)) == 0) {
-        const int pix = kpix[t2 >> P.spp_log2];
-        if (pix >= 0) {
-            f3 acc = mk(0.f, 0.f, 0.f);
-            for (int k = 0; k < P.spp; ++k)
-                acc = add(acc, mk(col[3 * (t2 + k)], col[3 * (t2 + k) + 1], col[3 * (t2 + k) + 2]));
-            const float rs = 1.0f / (float)P.spp;
-            const size_t k = (size_t)pix * 3;
-            const f3 px = mk(acc.x * rs, acc.y * rs, acc.z * rs);
-            if (P.rgb) {
-                P.rgb[k] = px.x;
-                P.rgb[k + 1] = px.y;
-                P.rgb[k + 2] = px.z;
-            }
-            if (P.p6) {
-                P.p6[k] = rtp::p6_default_sample(px.x);
-                P.p6[k + 1] = rtp::p6_default_sample(px.y);
-                P.p6[k + 2] = rtp::p6_default_sample(px.z);
-            }
-        }
-    }
-}
-#endif
-
 // One sample per lane: a block covers a tile_w x tile_h pixel tile x spp samples (spp a power
 // of two <= 256, tile_w*tile_h*spp == BLOCK); per-pixel sums run in sample order from LDS.
 template <int MODE, bool D1, int LS = 0>
@@ -2450,111 +2157,6 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, uin
     }
 }
 
-// ---- fused frames: the pre-passes inside the render kernel ----------------------------
-// A frame is one launch: every wave of the persistent grid first takes units of the cull pass
-// (64 tiles, one per lane), then, once all are done, units of the cut pass (a group of one
-// live list), then renders.  Units are claimed (fclaim) so any running wave can take a unit
-// another has not started: the waits depend only on units held by running waves, never on a
-// block that is not resident (a grid barrier would hang when the grid is not all resident,
-// e.g. two processes sharing a GPU).  Completion: per-unit adds to 8 counters (unit & 7), a
-// release before each add and an acquire after the wait (the lists are written and read on
-// different XCDs; the render phase reads them with scalar loads no wave made before the wait).
-__device__ __forceinline__ bool fused_claim(const RenderParams& P, uint32_t u, uint32_t lane) {
-    uint32_t old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_max(P.fclaim + u, P.fepoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return uni(old) < P.fepoch;
-}
-// A unit is done: a release, then one add to counter (unit & 7) of the phase; the wave whose add
-// completes its counter (all units u with u & 7 == i) adds to the phase's ninth counter, and the
-// wave completing that one raises the phase flag.  Waiters poll the flag word only.
-// expect: the units counter (u & 7) receives in this phase; nz: the counters that receive any.
-__device__ __forceinline__ void fused_done(const RenderParams& P, int slot0, uint32_t u, uint32_t expect, uint32_t nz,
-                                           uint32_t lane) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    if (lane == 0) {
-        const uint32_t i = u & 7u;
-        const uint32_t c = __hip_atomic_fetch_add(P.live_count + (slot0 + (int)i) * COUNTER_STRIDE, 1u, __ATOMIC_ACQ_REL,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        if (c + 1u == expect) {
-            const uint32_t d = __hip_atomic_fetch_add(P.live_count + (slot0 + 8) * COUNTER_STRIDE, 1u, __ATOMIC_ACQ_REL,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-            if (d + 1u == nz)
-                __hip_atomic_store(P.live_count + (slot0 + 9) * COUNTER_STRIDE, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-// Wait for the phase flag at slot0 + 9; a phase of n == 0 units is done at once.  After a long
-// wait (a grid not all resident: its unclaimed units), take any unit [0, nunits) nobody has
-// claimed (claim words at base).  Bounded: a frame whose wait ran out would be wrong, never a
-// hung GPU.
-template <typename F>
-__device__ __forceinline__ void fused_wait(const RenderParams& P, int slot0, uint32_t n, uint32_t nunits,
-                                           uint32_t base, uint32_t lane, F work) {
-    for (uint32_t it = 0; n > 0 && it < (1u << 20); ++it) {
-        uint32_t f = 0;
-        if (lane == 0)
-            f = __hip_atomic_load(P.live_count + (slot0 + 9) * COUNTER_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (uni(f) != 0) break;
-        if (it >= 512 && (it & 511) == 0) {  // rescue (not reached when the grid is all resident)
-            for (uint32_t u0 = 0; u0 < nunits; u0 += 64) {
-                const uint32_t u = u0 + lane;
-                const bool open = u < nunits && __hip_atomic_load(P.fclaim + base + u, __ATOMIC_RELAXED,
-                                                                  __HIP_MEMORY_SCOPE_AGENT) < P.fepoch;
-                for (uint64_t m = ballot(open); m != 0; m &= m - 1) {
-                    const uint32_t v = u0 + (uint32_t)__builtin_ctzll(m);
-                    if (fused_claim(P, base + v, lane)) work(v);
-                }
-            }
-        }
-        __builtin_amdgcn_s_sleep(8);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-__device__ __forceinline__ void fused_prepass(const RenderParams& P) {
-    const uint32_t lane = lane_id();
-    const uint32_t W = gridDim.x * (BLOCK / 64);
-    const uint32_t w = blockIdx.x * (BLOCK / 64) + (uni((uint32_t)threadIdx.x) >> 6);
-    // the next frame's counters (its previous user, frame k-2, has finished: same stream)
-    if (blockIdx.x == 0 && threadIdx.x < COUNTER_SLOTS) P.next_count[threadIdx.x * COUNTER_STRIDE] = 0u;
-    const uint32_t nC = (uint32_t)(P.tiles_total + 63) / 64u;
-    auto cull_u = [&](uint32_t u) {
-        cull_tiles(P, (int)(u * 64u + lane));
-        fused_done(P, FDONE_SLOT0, u, nC / 8u + ((u & 7u) < nC % 8u ? 1u : 0u), nC < 8u ? nC : 8u, lane);
-    };
-    for (uint32_t u = w; u < nC; u += W)
-        if (fused_claim(P, u, lane)) cull_u(u);
-    fused_wait(P, FDONE_SLOT0, nC, nC, 0u, lane, cull_u);
-    if (P.sc.ncut > 0) {
-        float box[6] = {0.f, 0.f, 0.f, -1.f, -1.f, -1.f};
-        int max_len;
-        const bool test = cut_setup(P, lane, box, max_len);
-        const uint32_t nq = (uint32_t)P.nqueues;
-        const uint32_t nU = nq * (uint32_t)((max_len + CUT_GROUP - 1) / CUT_GROUP);
-        uint32_t nK = 0;  // the groups that exist (a list shorter than max_len has holes)
-        for (int q = 0; q < P.nqueues; ++q)
-            nK += ((uint32_t)ldc_u32(&P.live_count[q * COUNTER_STRIDE]) + CUT_GROUP - 1) / CUT_GROUP;
-        // completion counter p & 7: with 8 lists that is list p % 8 (its groups), with one list
-        // the groups g = p spread evenly
-        uint32_t nzK = 0;
-        if (nq == 8) {
-            for (int q = 0; q < 8; ++q) nzK += ldc_u32(&P.live_count[q * COUNTER_STRIDE]) > 0 ? 1u : 0u;
-        } else {
-            nzK = nK < 8u ? nK : 8u;
-        }
-        auto cut_u = [&](uint32_t p) {
-            if (cut_unit(P, lane, (int)(p % nq), (int)(p / nq), test, box)) {
-                const uint32_t i = p & 7u;
-                const uint32_t expect = nq == 8 ? ((uint32_t)ldc_u32(&P.live_count[(int)i * COUNTER_STRIDE]) + CUT_GROUP - 1) / CUT_GROUP
-                                                : nK / 8u + (i < nK % 8u ? 1u : 0u);
-                fused_done(P, FDONE_SLOT0 + 10, p, expect, nzK, lane);
-            }
-        };
-        for (uint32_t p = w; p < nU; p += W)
-            if (fused_claim(P, nC + p, lane)) cut_u(p);
-        fused_wait(P, FDONE_SLOT0 + 10, nK, nU, nC, lane, cut_u);
-    }
-}
-
 // A persistent grid (the blocks one dispatch keeps resident) over per-XCD work queues: block b
 // serves queue g = b % 8 (dispatch deals blocks round-robin over the XCDs, so queue g is served
 // on XCD g and list g's tiles share an L2).  With 8 lists queue g is list g; with one list
@@ -2604,9 +2206,6 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
     // the wave's index in the block as a uniform value (threadIdx.x itself, kept live to the
     // tile-cost write at the end, was spilled to scratch)
     const uint32_t wv = uni((uint32_t)threadIdx.x) >> 6;
-#ifdef RT_EXP_FUSED
-    if (P.fused) fused_prepass(P);
-#endif
     // The first item of each wave (block) is its place in the grid, the rest come from the
     // queue after those: 900 dequeues per head at once when the grid starts took ~10 us to serve.
     for (bool first = true;; first = false) {
@@ -2665,10 +2264,6 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
             t_start[wv] = (uint32_t)wall_clock64();
             t_item[wv] = (uint32_t)tile * WPT + qw;
         }
-#ifdef RT_RESUME
-        if constexpr (SAMPLES && LS == 4) regen_tile<MODE>(R, tile, qw, tid, col, kpix, park, &lds_zero);
-        else
-#endif
         if constexpr (SAMPLES) samples_tile<MODE, D1, LS>(R, tile, qw, tid, col, kpix, park, &lds_zero);
         else pixels_tile<MODE, D1>(R, tile, qw, tid, park);
         if (R.tile_cost && fresh_lane_id() == 0) {  // this wave's duration, for the next frame's heavy lists
@@ -3186,10 +2781,6 @@ struct rt_scene {
     // so frame k's pre-passes overlap frame k-1's render kernel (its tail leaves CUs idle).
     static constexpr int kRing = 256;
     hipEvent_t ev0[kRing] = {}, evm[kRing] = {}, ev1[kRing] = {}, pdone[kRing] = {};
-    // fused frames (RT_FUSED): one launch, timed ev0 -> ev1 (no evm / pdone); claim words
-    bool fused[kRing] = {};
-    DevBuf fclaim;
-    uint32_t fepoch = 0;
     // evq: recorded on the caller's stream at the start of a frame; the prep stream waits for it
     // so the pre-passes (which write the culled tiles' pixels into the caller's buffers) come
     // after everything the caller queued on that stream before the call.  A caller that orders
@@ -3649,14 +3240,6 @@ void launch_mode(const RenderParams& P, const Launch& L) {
         }
         launch_render<D1_MODE, SAMPLES, true>(P, L);
     } else {
-#ifdef RT_RESUME
-        if constexpr (SAMPLES && (MODE & MODE_WIDE) != 0 && (MODE & (MODE_DEEP | RT_KERNEL_LANE)) == 0) {
-            if (P.regen) {
-                launch_render<MODE, SAMPLES, false, RT_PAIRED_WAVES, 4>(P, L);
-                return;
-            }
-        }
-#endif
         if constexpr (SAMPLES && (MODE & (MODE_DEEP | RT_KERNEL_LANE)) == 0) {
             if (P.half_waves && P.paired_only) {
                 launch_render<MODE, SAMPLES, false, RT_PAIRED_WAVES, 3>(P, L);
@@ -3823,12 +3406,6 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
                         ? 1
                         : 0;
     if (const char* e = std::getenv("RT_PAIRED_ONLY")) P.paired_only = P.paired_only && std::atoi(e) != 0;
-    // Path regeneration (paired_bounces_regen): the paired-only case over 4-ary records with
-    // full-wave items (64 samples per wave, 2 x 2 pixels x 16 spp).  RT_REGEN=1 selects it (A/B).
-    P.regen = 0;
-    if (const char* e = std::getenv("RT_REGEN"))
-        P.regen = P.paired_only && P.sc.wide && s->lane_wide && o->spp <= 64 && std::atoi(e) != 0 ? 1 : 0;
-    if (P.regen) half = P.half_waves = 0;
     int ppb = samples ? (BLOCK >> half) / o->spp : BLOCK;  // pixels per block
     int tw = 1;
     while (tw * tw < ppb) tw <<= 1;                // square-ish power-of-two tile
@@ -3890,7 +3467,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             // the render kernel's time, or the frame period when shorter (overlapping frames:
             // RT_FLAG_OVERLAP starts a kernel while the previous one still runs)
             float ms = 0.f, period = 0.f;
-            if (hipEventElapsedTime(&ms, s->fused[fl] ? s->ev0[fl] : s->evm[fl], s->ev1[fl]) == hipSuccess) {
+            if (hipEventElapsedTime(&ms, s->evm[fl], s->ev1[fl]) == hipSuccess) {
                 const int f0 = int(uint64_t(last - 1) % rt_scene::kRing);
                 if (last >= 1 && hipEventElapsedTime(&period, s->ev1[f0], s->ev1[fl]) == hipSuccess && period > 0.f)
                     ms = std::min(ms, period);
@@ -3961,57 +3538,12 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.heavy_tiles = reinterpret_cast<int32_t*>(lists + list_bytes + cut_bytes);
     const int slot = int(k % rt_scene::kRing);
     // From the cull launch on, a failure leaves the counter sets unknown (counters_dirty).
-    static const bool same_stream = [] {
-        const char* e = std::getenv("RT_PREP_SAME_STREAM");
-        return e && std::atoi(e) != 0;
-    }();
-    static const int cut_per_cu = [] {
-        const char* e = std::getenv("RT_CUT_BLOCKS_PER_CU");
-        return e ? std::max(1, std::atoi(e)) : 4;
-    }();
-    // Fused frames (A/B, RT_FUSED=1): the render kernel runs the cull and cut passes itself
-    // (fused_prepass): one launch per frame on the caller's stream, no prep stream, no
-    // cross-stream wait.
-    bool fused = false;
-#ifdef RT_EXP_FUSED
-    if (const char* e = std::getenv("RT_FUSED")) fused = std::atoi(e) != 0 && !s->deep;
-#endif
-    if (fused) {
-        const size_t nC = (size_t(P.tiles_total) + 63) / 64;
-        const size_t need = (nC + size_t(P.nqueues) * ((size_t(P.queue_cap) + CUT_GROUP - 1) / CUT_GROUP)) * sizeof(uint32_t);
-        if (s->fclaim.n < need) {
-            if (k > 0) HIP_TRY(hipEventSynchronize(ev1_of(k - 1)));
-            if ((rc = s->fclaim.alloc(need)) != RT_OK) return rc;
-            HIP_TRY(hipMemset(s->fclaim.p, 0, need));
-        }
-        P.fused = 1;
-        P.fepoch = ++s->fepoch;
-        P.fclaim = static_cast<uint32_t*>(s->fclaim.p);
-    }
-    s->fused[slot] = fused;
     auto frame = [&]() -> int {
-        if (fused) {
-            if (s->counters_dirty) {
-                HIP_TRY(hipMemsetAsync(base, 0, rt_scene::kSets * kCounterBytes, st));
-                s->counters_dirty = false;
-            }
-            if (cost_reset) HIP_TRY(hipMemsetAsync(s->cost.p, 0, s->cost.n, st));
-            static const size_t big_bytes_f = [] {
-                const char* e = std::getenv("RT_BIG_SCENE_BYTES");
-                return e ? (size_t)std::strtoull(e, nullptr, 10) : kBigSceneBytes;
-            }();
-            const Launch L{st, s->ev0[slot], s->ev1[slot], s->cus, s->bytes > big_bytes_f, &s->last_kernel};
-            if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, L);
-            else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, L);
-            else launch<RT_KERNEL_WAVE>(P, samples, L);
-            HIP_TRY(hipGetLastError());
-            return RT_OK;
-        }
-        hipStream_t pp = same_stream ? st : s->prep;
+        hipStream_t pp = s->prep;
         // set k was last read by frame k-3, set k+1 (zeroed by this cull pass) by frame k-2
-        if (k >= 2 && !same_stream) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 2), 0));
-        if (k >= 1 && overlap && !same_stream) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 1), 0));
-        if (!s->caller_ordered && !same_stream) {  // stream order for the caller's buffers (see rt_scene::evq)
+        if (k >= 2) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 2), 0));
+        if (k >= 1 && overlap) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 1), 0));
+        if (!s->caller_ordered) {  // stream order for the caller's buffers (see rt_scene::evq)
             HIP_TRY(hipEventRecord(s->evq[slot], st));
             HIP_TRY(hipStreamWaitEvent(pp, s->evq[slot], 0));
         }
@@ -4027,11 +3559,11 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         HIP_TRY(hipGetLastError());
         if (cut) {
             // 16 waves per CU; each takes (list, group) pairs grid-stride (c3: about one each)
-            const int cut_blocks = cut_per_cu * s->cus;
+            const int cut_blocks = 4 * s->cus;
             hipExtLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, pp, nullptr, s->pdone[slot], 0, P);
             HIP_TRY(hipGetLastError());
         }
-        if (!same_stream) HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
+        HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
         static const size_t big_bytes = [] {
             const char* e = std::getenv("RT_BIG_SCENE_BYTES");
             return e ? (size_t)std::strtoull(e, nullptr, 10) : kBigSceneBytes;
@@ -4080,12 +3612,8 @@ int event_times(const rt_scene* s, int what, float* ms_out, int max, int* n_out)
         const int slot = int((s->launches - uint64_t(n) + uint64_t(k)) % rt_scene::kRing);
         HIP_TRY(hipEventSynchronize(s->ev1[slot]));
         float kern = 0.f, prep = 0.f;
-        if (s->fused[slot]) {  // one launch: its span is the kernel and the frame, no separate pre-pass
-            if (what != 1) HIP_TRY(hipEventElapsedTime(&kern, s->ev0[slot], s->ev1[slot]));
-        } else {
-            if (what != 1) HIP_TRY(hipEventElapsedTime(&kern, s->evm[slot], s->ev1[slot]));
-            if (what != 0) HIP_TRY(hipEventElapsedTime(&prep, s->ev0[slot], s->pdone[slot]));
-        }
+        if (what != 1) HIP_TRY(hipEventElapsedTime(&kern, s->evm[slot], s->ev1[slot]));
+        if (what != 0) HIP_TRY(hipEventElapsedTime(&prep, s->ev0[slot], s->pdone[slot]));
         ms_out[k] = kern + prep;
     }
     if (n_out) *n_out = n;

@@ -174,18 +174,13 @@ def test_bounce_paths_per_lane_traversal(name, flags):
 
 @pytest.mark.parametrize("name", ["c3b_small", "frog_bounce", "sphere_single"])
 @pytest.mark.parametrize("flags", [0, rt._lib.RT_FLAG_BINARY])
-@pytest.mark.parametrize("half", ["0", "1", "regen"])
+@pytest.mark.parametrize("half", ["0", "1"])
 def test_one_light_bounce_loops_parity(name, flags, half, monkeypatch):
     """One-light multi-bounce frames through both bounce loops: half waves (the default) pair a
     path's lane with a shadow lane (paired_bounces: a depth's Lo add waits for its shadow ray's
     answer, traced beside the next bounce ray); RT_HALF_WAVES=0 forces full waves and the
-    unpaired loop; "regen" selects the paired loop with path regeneration (RT_REGEN=1: full-wave
-    items whose path lanes take the wave's next sample).  The reference's outputs bit for bit,
-    AOVs included."""
-    if half == "regen":
-        monkeypatch.setenv("RT_REGEN", "1")
-    else:
-        monkeypatch.setenv("RT_HALF_WAVES", half)
+    unpaired loop.  The reference's outputs bit for bit, AOVs included."""
+    monkeypatch.setenv("RT_HALF_WAVES", half)
     meta = golden_meta(name)
     assert meta["max_depth"] > 1 and meta["num_lights"] == 1
     scene = G_SCENES[name]
@@ -205,12 +200,6 @@ def test_c3b_full_frame_matches_reference():
     reference's own full-size outputs (hit AOVs by sha256, float frame, P6 file)."""
     meta = golden_meta("c3b_full")
     _c3b_full_check(meta)
-
-
-def test_c3b_full_frame_regen_matches_reference(monkeypatch):
-    """c3b through the path-regeneration kernel (RT_REGEN=1): the same reference outputs."""
-    monkeypatch.setenv("RT_REGEN", "1")
-    _c3b_full_check(golden_meta("c3b_full"))
 
 
 def _c3b_full_check(meta):

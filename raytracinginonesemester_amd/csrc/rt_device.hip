@@ -170,6 +170,26 @@ extern "C" __device__ int rt_llvm_writelane(int, int, int) __asm("llvm.amdgcn.wr
 __device__ __forceinline__ uint32_t wrlane(uint32_t v, uint32_t l, uint32_t old) {
     return (uint32_t)rt_llvm_writelane((int)v, (int)l, (int)old);
 }
+// Wave-wide max / min of a float over all 64 lanes (callers pass the identity on lanes that do
+// not take part), wave-uniform result: DPP steps within quads, half rows, rows, then the row
+// broadcasts; lane 63 ends with the whole wave's.
+template <bool MAX, int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_step(float x) {
+    const float id = MAX ? -INFINITY : INFINITY;
+    const float y =
+        __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(x), CTRL, ROW_MASK, 0xF, false));
+    return MAX ? fmaxf(x, y) : fminf(x, y);
+}
+template <bool MAX>
+__device__ __forceinline__ float wave_reduce_f(float v) {
+    v = dpp_step<MAX, 0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+    v = dpp_step<MAX, 0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+    v = dpp_step<MAX, 0x141, 0xF>(v);  // row_half_mirror
+    v = dpp_step<MAX, 0x140, 0xF>(v);  // row_mirror
+    v = dpp_step<MAX, 0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+    v = dpp_step<MAX, 0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 
 // ---- traversal statistics (instrumented variant builds only: -DRT_STATS) -----------------
 #ifdef RT_STATS
@@ -534,6 +554,143 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
     }
 }
 
+// ---- FRUSTUM traversal (camera rays over the 4-ary records) ------------------------------
+// The camera rays of a wave share their origin, and their directions lie in a narrow cone.
+// traverse_wave_split tests every pushed entry for every lane (per-lane slab tests of four boxes
+// per record, 64-bit lane masks on the stack, pop-time re-tests after hits); here an internal
+// entry is tested once for the whole wave against the family of directions instead, and only
+// leaves take the per-lane test:
+// - the family: per axis the interval [dl, dh] of the live lanes' direction components.  For a
+//   box and a direction d in the family, the slab parameters (b - o)/d of an axis lie between
+//   the values at d = dl and d = dh (linear in 1/d, and 1/d is monotone on an interval of one
+//   sign), so min / max over the four products (min - o, max - o) x (1/dl, 1/dh) bound every
+//   lane's near / far end of that axis; an axis whose interval reaches |d| < 1e-8 (where the
+//   reference's test is an inside test) or crosses 0 gives no bound (1/dl, 1/dh = -inf, +inf:
+//   the products are +-inf or NaN, which the min / max drop).  The wave passes a box when
+//   max(tmin, max near) <= min(tmax_w, min far), widened by 2^-19 relative (the float rounding
+//   of (b - o), 1/d and the product is < 2^-22 relative; the reference's double ends are within
+//   2^-52), with tmax_w the largest bestT over the live lanes.  So the wave test passes whenever
+//   some live lane's exact test (intersectAABB, bvh.h:81-129) passes with that lane's bestT;
+// - the DFS is the reference's order (SearchBVH, query.h:224-311): entries pushed in record
+//   order, the last passing one held (popped next).  At a leaf, each lane makes the reference's
+//   pop-time test of the leaf's own box with its own bestT (box_hit_mask, exact), then
+//   Moller-Trumbore.  Exactness: leaves are reached in the reference's order, so a lane holds
+//   the reference's bestT at each of them; the reference reaches a leaf for a lane iff the leaf's
+//   own pop-time test and every ancestor's test (made earlier, with bestT no smaller) pass, and
+//   since every internal box contains its children's boxes (checked at scene build, wide_ok) and
+//   slab tests are monotone in the box and in tmax, the ancestors' tests are implied by the
+//   leaf's own.  The wave reaches every leaf a lane's reference DFS reaches (the wave test is
+//   conservative), and at leaves it does not, the lane's own test fails.  The root's pop-time
+//   test is made per lane first (the root box need not contain its children's);
+// - each internal record: lanes 0-3 load entry k's box (lane k & 3, vector loads), the refs and
+//   the present-entry mask come through scalar loads; the stack holds refs only (entry k in lane k).
+// Scenes whose coordinates come within 1e30 of the float range give no bound on those axes
+// (products stay finite: |b - o| < 1e30, |1/d| <= 1e8).
+template <bool PK = false, bool XL = false>
+__device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayPre& r, bool active, HitState& hs) {
+    hs.bestT = FLT_MAX;
+    hs.slot = -1;
+#ifdef RT_STATS
+    hs.pops = 0;
+#endif
+    uint64_t alive = ballot(active);
+    if (alive == 0) return;
+    RT_STAT(0, 1);
+    RT_STAT(13, __popcll(alive));
+    alive = box_hit_mask<PK, XL>(r, own_box(sc, sc.root_ref, true), FLT_MAX, alive);  // the root's pop-time test
+    if (alive == 0) {
+        RT_STAT(17, 1);
+        return;
+    }
+    const bool live = lane_in(alive);
+    // the family: the shared origin and per axis (1/dl, 1/dh), wave-uniform
+    const float o[3] = {__int_as_float(uni(__float_as_int(r.o.x))), __int_as_float(uni(__float_as_int(r.o.y))),
+                        __int_as_float(uni(__float_as_int(r.o.z)))};
+    const float dd[3] = {r.d.x, r.d.y, r.d.z};
+    v2f U[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float dl = wave_reduce_f<false>(live ? dd[a] : INFINITY);
+        const float dh = wave_reduce_f<true>(live ? dd[a] : -INFINITY);
+        const bool ok = (dl >= 1e-8f || dh <= -1e-8f) && sc.bmax[a] + fabsf(o[a]) < 1e30f;
+        // (made SGPRs: wave-uniform values the VALU computed stay in VGPRs otherwise)
+        U[a] = (v2f){__int_as_float(uni(__float_as_int(ok ? 1.0f / dl : -INFINITY))),
+                     __int_as_float(uni(__float_as_int(ok ? 1.0f / dh : INFINITY)))};
+    }
+    const float kW = 1.0f / 524288.0f;  // 2^-19
+    float tmax_w = FLT_MAX;
+    uint32_t ref = sc.root_ref;
+    uint32_t st_ref = 0;  // lane k holds entry k
+    int sp = 0;
+    const char* leaf_b = reinterpret_cast<const char*>(sc.leaf);
+    const char* wnode_b = reinterpret_cast<const char*>(sc.wnode);
+    const uint32_t k6 = 6u * (lane_id() & 3u);  // this lane's entry in a record, in floats
+    while (true) {
+        RT_STAT(2, 1);
+#ifdef RT_STATS
+        ++hs.pops;
+#endif
+        uint32_t next = NO_REF;
+        if (ref & LEAF_BIT) {
+            RT_STAT(10, 1);
+            const uint32_t slot = ref & ~LEAF_BIT;
+            const float4* L = reinterpret_cast<const float4*>(leaf_b + (slot << 6));
+            const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2), d = ldc(L + 3);
+            const uint64_t m = box_hit_mask<PK, XL>(r, BoxP{hi2(c), lo2(d), hi2(d)}, hs.bestT, alive);
+            if (m != 0) {
+                RT_STAT(4, 1);
+                const bool act = lane_in(m);
+                float t, u, v;
+                const bool h = act && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin,
+                                           hs.bestT, t, u, v);
+                if (h) {
+                    hs.bestT = t;
+                    hs.slot = (int32_t)slot;
+                }
+                if (ballot(h) != 0) tmax_w = wave_reduce_f<true>(live ? hs.bestT : 0.0f);
+            }
+        } else {
+            RT_STAT(8, 1);
+            const float* W = reinterpret_cast<const float*>(wnode_b + (ref << 7));
+            const uint4 rq = ldc_u(reinterpret_cast<const float4*>(W) + 6);
+            const uint32_t present = ldc_u32(reinterpret_cast<const uint32_t*>(W) + 28);
+            // issued with the box loads (sunk into the push branch, the refs' scalar load added
+            // its latency after the test)
+            asm volatile("" ::"s"(rq.x), "s"(rq.y), "s"(rq.z), "s"(rq.w), "s"(present));
+            const v2f* B = reinterpret_cast<const v2f*>(W + k6);
+            const v2f bb[3] = {B[0], B[1], B[2]};
+            float nr[3], fr[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const v2f db = bb[a] - (v2f){o[a], o[a]};
+                const v2f p = (v2f){db.x, db.x} * U[a], q = (v2f){db.y, db.y} * U[a];
+                nr[a] = fminf(fminf(p.x, p.y), fminf(q.x, q.y));
+                fr[a] = fmaxf(fmaxf(p.x, p.y), fmaxf(q.x, q.y));
+            }
+            float Lc = fmaxf(fmaxf(nr[0], nr[1]), nr[2]);
+            float Hc = fminf(fminf(fr[0], fr[1]), fr[2]);
+            Lc = __builtin_fmaf(fabsf(Lc), -kW, Lc);
+            Hc = __builtin_fmaf(fabsf(Hc), kW, Hc);
+            const uint32_t m4 = (uint32_t)ballot(fmaxf(Lc, kRayTMin) <= fminf(Hc, tmax_w)) & present & 0xFu;
+            if (m4 != 0) {
+                RT_STAT(4, 1);
+                // push the passing entries in record order, hold the last (the reference pops it next)
+                const uint32_t hold = 31u - __builtin_clz(m4);
+                if (m4 & 1u & ~(1u << hold)) st_ref = wrlane(rq.x, sp++, st_ref);
+                if (m4 & 2u & ~(1u << hold)) st_ref = wrlane(rq.y, sp++, st_ref);
+                if (m4 & 4u & ~(1u << hold)) st_ref = wrlane(rq.z, sp++, st_ref);
+                next = hold == 3 ? rq.w : hold == 2 ? rq.z : hold == 1 ? rq.y : rq.x;
+            }
+        }
+        if (next != NO_REF) {
+            ref = next;
+            continue;
+        }
+        if (sp == 0) break;
+        ref = rdlane(st_ref, --sp);
+    }
+}
+
 // ---- LANE traversal (private stack per lane; the reference's shape) ---------------------
 __device__ __forceinline__ void traverse_lane(const SceneView& sc, const RayPre& r, bool active,
                                               bool any_hit, float any_hit_dist, HitState& hs) {
@@ -820,6 +977,19 @@ __device__ __forceinline__ void traverse(const SceneView& sc, const RayPre& r, b
     else if constexpr (MODE == RT_KERNEL_LANE) traverse_lane(sc, r, active, any_hit, any_hit_dist, hs);
     else traverse_wave_split<(MODE & MODE_WIDE) != 0, (MODE & MODE_PK) != 0, (MODE & MODE_PK) != 0 && (MODE & MODE_1L) == 0>(
         sc, r, active, any_hit, any_hit_dist, hs);
+}
+
+// A camera ray's closest-hit query (all lanes share the origin): the frustum traversal in the
+// 4-ary WAVE kernels, the kernel's own traversal otherwise.
+template <int MODE>
+__device__ __forceinline__ void traverse_camera(const SceneView& sc, const RayPre& r, bool active, HitState& hs) {
+#ifndef RT_NO_FRUSTUM
+    if constexpr (MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0 && (MODE & MODE_WIDE) != 0) {
+        traverse_frustum<(MODE & MODE_PK) != 0, (MODE & MODE_PK) != 0 && (MODE & MODE_1L) == 0>(sc, r, active, hs);
+        return;
+    }
+#endif
+    traverse<MODE>(sc, r, active, false, 0.0f, hs);
 }
 
 // The traversal of a ray at bounce depth `depth` (wave-uniform): camera rays (depth 0) and their
@@ -1416,7 +1586,7 @@ __device__ __forceinline__ f3 trace_sample(const RenderParams& P, bool valid, in
         pk.put(13, __int_as_float((int32_t)(aov >> 32)));
         Park::fence();
         HitState hs;
-        traverse<MODE>(sc, ray, valid, false, 0.0f, hs);
+        traverse_camera<MODE>(sc, ray, valid, hs);
         Park::fence();
         aov = (int64_t)(uint32_t)__float_as_int(pk.get(12)) | ((int64_t)__float_as_int(pk.get(13)) << 32);
         RT_PHASE(P, x, y, 0);
@@ -1450,7 +1620,7 @@ __device__ __forceinline__ f3 trace_sample(const RenderParams& P, bool valid, in
             // depth 0's camera ray takes the wave traversal; its shadow ray and every later ray
             // go to paired_bounces' per-lane traversals
             HitState hs;
-            traverse<MODE>(sc, ray, alive, false, 0.0f, hs);
+            traverse_camera<MODE>(sc, ray, alive, hs);
             if (valid && aov >= 0) {
                 const bool hit = alive && hs.slot >= 0;
                 P.hit_idx[aov] = hit ? leaf_tri<false>(sc, hs.slot) : -1;
@@ -1469,7 +1639,8 @@ __device__ __forceinline__ f3 trace_sample(const RenderParams& P, bool valid, in
         if (ballot(alive) == 0) break;
         HitState hs;
         if (depth > 0) count_rays<MODE>(P.ray_count, 2, alive);
-        traverse_at<MODE>(sc, depth, ray, alive, false, 0.0f, hs, park);
+        if (depth == 0) traverse_camera<MODE>(sc, ray, alive, hs);
+        else traverse_at<MODE>(sc, depth, ray, alive, false, 0.0f, hs, park);
         const bool hit = alive && hs.slot >= 0;
         SurfHit sh;
         sh.tri = -1;
@@ -2964,7 +3135,7 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
             const rt_aabb& ob = aabbs[n];
             hib[2 * c] = make_float4(ob.min_corner.x, ob.max_corner.x, ob.min_corner.y, ob.max_corner.y);
             hib[2 * c + 1] = make_float4(ob.min_corner.z, ob.max_corner.z, 0.f, 0.f);
-            if (wide_ok) {  // 4 x (x pair, y pair, z pair) | 4 refs | unused
+            if (wide_ok) {  // 4 x (x pair, y pair, z pair) | 4 refs | mask of the entries present
                 float w[32] = {};
                 uint32_t e[4], wr[4] = {NO_REF, NO_REF, NO_REF, NO_REF};
                 const int k = wide_entries(nd, e);
@@ -2976,6 +3147,8 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
                     wr[i] = ref_of(e[i]);
                 }
                 std::memcpy(&w[24], wr, sizeof(wr));
+                const uint32_t present = (1u << k) - 1u;  // entries fill slots 0..k-1
+                std::memcpy(&w[28], &present, 4);
                 std::memcpy(&hwn[8 * c], w, sizeof(w));
             }
         } else {

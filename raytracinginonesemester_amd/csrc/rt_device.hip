@@ -38,6 +38,7 @@
 #include <memory>
 #include <new>
 #include <string>
+#include <array>
 #include <vector>
 
 #include "rt_common.hpp"
@@ -82,6 +83,8 @@ struct DevLight {
 struct SceneView {
     const float4* __restrict__ inode;
     const float4* __restrict__ wnode;  // 4-ary records (8 x float4) by internal index, if wide
+    const float* __restrict__ fnode;   // 2^f_log2-ary records (8 x 2^f_log2 floats) of traverse_frustum, or null
+    int32_t f_log2;                    // 3 or 4 with fnode; 2: traverse_frustum takes wnode
     const float4* __restrict__ ibox;
     const float4* __restrict__ rootb;  // the root's box, pairs (x | y, z), after ibox's entries
     const float4* __restrict__ leaf;
@@ -554,7 +557,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
     }
 }
 
-// ---- FRUSTUM traversal (camera rays over the 4-ary records) ------------------------------
+// ---- FRUSTUM traversal (camera rays over 16-ary records) ---------------------------------
 // The camera rays of a wave share their origin, and their directions lie in a narrow cone.
 // traverse_wave_split tests every pushed entry for every lane (per-lane slab tests of four boxes
 // per record, 64-bit lane masks on the stack, pop-time re-tests after hits); here an internal
@@ -582,8 +585,12 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
 //   leaf's own.  The wave reaches every leaf a lane's reference DFS reaches (the wave test is
 //   conservative), and at leaves it does not, the lane's own test fails.  The root's pop-time
 //   test is made per lane first (the root box need not contain its children's);
-// - each internal record: lanes 0-3 load entry k's box (lane k & 3, vector loads), the refs and
-//   the present-entry mask come through scalar loads; the stack holds refs only (entry k in lane k).
+// - records: one wave-level test costs the same for 4 entries as for 16 (lane k tests entry k),
+//   so the records hold an internal node's descendants four levels down (fnode, rt_scene_create):
+//   a DFS over them makes about half the internal pops of the 4-ary one, each a dependent
+//   round trip to memory.  Lane k loads entry k's box and ref (vector loads); the stack holds
+//   refs only (entry k in lane k).  Scenes whose 16-ary DFS would need more than STACK_CAP
+//   entries take the 4-ary records the same way.
 // Scenes whose coordinates come within 1e30 of the float range give no bound on those axes
 // (products stay finite: |b - o| < 1e30, |1/d| <= 1e8).
 template <bool PK = false, bool XL = false>
@@ -623,8 +630,14 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
     uint32_t st_ref = 0;  // lane k holds entry k
     int sp = 0;
     const char* leaf_b = reinterpret_cast<const char*>(sc.leaf);
-    const char* wnode_b = reinterpret_cast<const char*>(sc.wnode);
-    const uint32_t k6 = 6u * (lane_id() & 3u);  // this lane's entry in a record, in floats
+    // the wide records (fnode) when the scene has them, else the 4-ary ones (wnode): lane k
+    // (mod the arity A = 2^f_log2) tests entry k; a record is 8A floats, refs at float 6A
+    const uint32_t lg = (uint32_t)sc.f_log2;
+    const char* rec_b = sc.fnode != nullptr ? reinterpret_cast<const char*>(sc.fnode) : reinterpret_cast<const char*>(sc.wnode);
+    const uint32_t rec_shift = 5u + lg;
+    const uint32_t ent_mask = (1u << (1u << lg)) - 1u;
+    const uint32_t kl = lane_id() & ((1u << lg) - 1u);
+    const uint32_t k6 = 6u * kl, kref = (6u << lg) + kl;  // this lane's entry, in floats
     while (true) {
         RT_STAT(2, 1);
 #ifdef RT_STATS
@@ -651,14 +664,10 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
             }
         } else {
             RT_STAT(8, 1);
-            const float* W = reinterpret_cast<const float*>(wnode_b + (ref << 7));
-            const uint4 rq = ldc_u(reinterpret_cast<const float4*>(W) + 6);
-            const uint32_t present = ldc_u32(reinterpret_cast<const uint32_t*>(W) + 28);
-            // issued with the box loads (sunk into the push branch, the refs' scalar load added
-            // its latency after the test)
-            asm volatile("" ::"s"(rq.x), "s"(rq.y), "s"(rq.z), "s"(rq.w), "s"(present));
+            const float* W = reinterpret_cast<const float*>(rec_b + ((size_t)ref << rec_shift));
             const v2f* B = reinterpret_cast<const v2f*>(W + k6);
             const v2f bb[3] = {B[0], B[1], B[2]};
+            const uint32_t rk = reinterpret_cast<const uint32_t*>(W)[kref];
             float nr[3], fr[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
@@ -671,15 +680,15 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
             float Hc = fminf(fminf(fr[0], fr[1]), fr[2]);
             Lc = __builtin_fmaf(fabsf(Lc), -kW, Lc);
             Hc = __builtin_fmaf(fabsf(Hc), kW, Hc);
-            const uint32_t m4 = (uint32_t)ballot(fmaxf(Lc, kRayTMin) <= fminf(Hc, tmax_w)) & present & 0xFu;
-            if (m4 != 0) {
+            const uint32_t m =
+                (uint32_t)ballot(rk != NO_REF && fmaxf(Lc, kRayTMin) <= fminf(Hc, tmax_w)) & ent_mask;
+            if (m != 0) {
                 RT_STAT(4, 1);
                 // push the passing entries in record order, hold the last (the reference pops it next)
-                const uint32_t hold = 31u - __builtin_clz(m4);
-                if (m4 & 1u & ~(1u << hold)) st_ref = wrlane(rq.x, sp++, st_ref);
-                if (m4 & 2u & ~(1u << hold)) st_ref = wrlane(rq.y, sp++, st_ref);
-                if (m4 & 4u & ~(1u << hold)) st_ref = wrlane(rq.z, sp++, st_ref);
-                next = hold == 3 ? rq.w : hold == 2 ? rq.z : hold == 1 ? rq.y : rq.x;
+                const uint32_t hold = 31u - __builtin_clz(m);
+                next = rdlane(rk, hold);
+                for (uint32_t rest = m & ~(1u << hold); rest != 0; rest &= rest - 1u)
+                    st_ref = wrlane(rdlane(rk, __builtin_ctz(rest)), sp++, st_ref);
             }
         }
         if (next != NO_REF) {
@@ -2927,6 +2936,8 @@ struct rt_scene {
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     float bmax[3] = {0, 0, 0};
     DevBuf inode, wnode, ibox, leaf, tnorm, objids, mats, lights, jitter;
+    DevBuf fnode;    // 2^f_log2-ary records of the frustum traversal (empty: it takes wnode's 4-ary ones)
+    int f_log2 = 2;
     DevBuf cut;  // tile culling: boxes of a cut of the tree (6 floats each)
     int ncut = 0;
     bool deep = false;  // the DFS may need more than STACK_CAP entries: MODE_DEEP kernels
@@ -3135,7 +3146,7 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
             const rt_aabb& ob = aabbs[n];
             hib[2 * c] = make_float4(ob.min_corner.x, ob.max_corner.x, ob.min_corner.y, ob.max_corner.y);
             hib[2 * c + 1] = make_float4(ob.min_corner.z, ob.max_corner.z, 0.f, 0.f);
-            if (wide_ok) {  // 4 x (x pair, y pair, z pair) | 4 refs | mask of the entries present
+            if (wide_ok) {  // 4 x (x pair, y pair, z pair) | 4 refs | unused
                 float w[32] = {};
                 uint32_t e[4], wr[4] = {NO_REF, NO_REF, NO_REF, NO_REF};
                 const int k = wide_entries(nd, e);
@@ -3147,8 +3158,6 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
                     wr[i] = ref_of(e[i]);
                 }
                 std::memcpy(&w[24], wr, sizeof(wr));
-                const uint32_t present = (1u << k) - 1u;  // entries fill slots 0..k-1
-                std::memcpy(&w[28], &present, 4);
                 std::memcpy(&hwn[8 * c], w, sizeof(w));
             }
         } else {
@@ -3248,6 +3257,77 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     }
     if ((rc = s->inode.upload(hin.data(), hin.size() * sizeof(float4))) != RT_OK) return rc;
     if (wide_ok && (rc = s->wnode.upload(hwn.data(), hwn.size() * sizeof(float4))) != RT_OK) return rc;
+    // Wide records for the camera rays' frustum traversal (traverse_frustum): an internal node's
+    // descendants D levels down in SearchBVH's push order (a leaf, or a child naming no valid
+    // triangle, stands for itself / is skipped, as in the 4-ary records), for the root and, in
+    // turn, every internal entry of a record; A = 2^D entries.  Records by their own index (an
+    // internal entry's ref is its record's), 8A floats: A x (x pair, y pair, z pair) | A refs
+    // (NO_REF pads) | unused.  Exact for the reason the 4-ary records are (every internal box
+    // contains its children's, wide_ok).  The largest A in {16, 8} whose DFS needs at most
+    // STACK_CAP stack entries (frog: 16, bound 59; the c5 heightfield: 8, bound 50 -- 16 would
+    // need 82); otherwise the frustum traversal takes the 4-ary records (wnode).
+#ifndef RT_NO_F16  // (variant builds for A/B runs: the frustum traversal over the 4-ary records)
+    int dmax = 4;  // RT_FRUSTUM_ARITY: the largest arity's log2 to try (tests; 2 = the 4-ary records)
+    if (const char* e = std::getenv("RT_FRUSTUM_ARITY")) dmax = std::clamp(std::atoi(e), 2, 4);
+    for (int D = dmax; D >= 3 && wide_ok && !(s->root_ref & LEAF_BIT); --D) {
+        const int A = 1 << D;
+        auto expand = [&](auto&& self, uint32_t n, int d, uint32_t* e, int& k) -> void {
+            if (ref_of0(n) == NO_REF) return;
+            if (d == 0 || (ref_of0(n) & LEAF_BIT)) {
+                e[k++] = n;
+                return;
+            }
+            self(self, nodes[n].left_idx, d - 1, e, k);
+            self(self, nodes[n].right_idx, d - 1, e, k);
+        };
+        std::vector<uint32_t> recs{0u};  // binary node of each record, breadth first
+        std::vector<uint32_t> fid(NN, NO_REF);
+        fid[0] = 0;
+        std::vector<std::array<uint32_t, 16>> ents;
+        std::vector<int> nent;
+        for (size_t r = 0; r < recs.size(); ++r) {
+            std::array<uint32_t, 16> e;
+            int k = 0;
+            expand(expand, nodes[recs[r]].left_idx, D - 1, e.data(), k);
+            expand(expand, nodes[recs[r]].right_idx, D - 1, e.data(), k);
+            for (int i = 0; i < k; ++i)
+                if (!(ref_of0(e[i]) & LEAF_BIT) && fid[e[i]] == NO_REF) {
+                    fid[e[i]] = uint32_t(recs.size());
+                    recs.push_back(e[i]);
+                }
+            ents.push_back(e);
+            nent.push_back(k);
+        }
+        // DFS stack bound: entry i of a record is processed with entries 0..i-1 on the stack
+        std::vector<int> SF(recs.size(), 0);
+        for (size_t r = recs.size(); r-- > 0;) {
+            int sf = nent[r];
+            for (int i = 0; i < nent[r]; ++i)
+                if (!(ref_of0(ents[r][i]) & LEAF_BIT)) sf = std::max(sf, i + SF[fid[ents[r][i]]]);
+            SF[r] = sf;
+        }
+        if (SF[0] > STACK_CAP) continue;
+        std::vector<float> hf(size_t(8 * A) * recs.size(), 0.f);
+        for (size_t r = 0; r < recs.size(); ++r) {
+            float* w = &hf[size_t(8 * A) * r];
+            for (int i = 0; i < A; ++i) {
+                uint32_t wr = NO_REF;
+                if (i < nent[r]) {
+                    const uint32_t n = ents[r][i];
+                    const rt_aabb& bb = aabbs[n];
+                    const float v6[6] = {bb.min_corner.x, bb.max_corner.x, bb.min_corner.y,
+                                         bb.max_corner.y, bb.min_corner.z, bb.max_corner.z};
+                    std::memcpy(&w[6 * i], v6, sizeof(v6));
+                    wr = (ref_of0(n) & LEAF_BIT) ? ref_of0(n) : fid[n];
+                }
+                std::memcpy(&w[6 * A + i], &wr, 4);
+            }
+        }
+        if ((rc = s->fnode.upload(hf.data(), hf.size() * sizeof(float))) != RT_OK) return rc;
+        s->f_log2 = D;
+        break;
+    }
+#endif
     s->wide = wide_ok && !(s->root_ref & LEAF_BIT);
     s->lane_stack = !deep && binary_stack <= LANE_LDS_CAP;
     s->lane_wide = s->wide && s->lane_stack && wide_stack <= LANE_LDS_CAP;
@@ -3273,7 +3353,8 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     if (nmat > 0 && (rc = s->mats.upload(mats, size_t(nmat) * sizeof(rt_material))) != RT_OK) return rc;
     if (nlights > 0 && (rc = s->lights.upload(lights, size_t(nlights) * sizeof(rt_light))) != RT_OK) return rc;
     if ((rc = s->create_sync()) != RT_OK) return rc;
-    s->bytes = s->inode.n + s->wnode.n + s->ibox.n + s->leaf.n + s->tnorm.n + s->objids.n + s->mats.n + s->lights.n;
+    s->bytes = s->inode.n + s->wnode.n + s->fnode.n + s->ibox.n + s->leaf.n + s->tnorm.n + s->objids.n +
+               s->mats.n + s->lights.n;
     *out = s.release();
     return RT_OK;
 }
@@ -3297,11 +3378,13 @@ extern "C" int rt_scene_clone(const rt_scene* src, int device, rt_scene** out) {
     s->wide = src->wide;
     s->lane_stack = src->lane_stack;
     s->lane_wide = src->lane_wide;
+    s->f_log2 = src->f_log2;
     s->deep = src->deep;
     s->cus = src->cus;
     s->bytes = src->bytes;
     // device-to-device copies of the packed arrays (over xGMI when the devices differ)
     const std::pair<DevBuf*, const DevBuf*> bufs[] = {{&s->inode, &src->inode}, {&s->wnode, &src->wnode},
+                                                      {&s->fnode, &src->fnode},
                                                       {&s->ibox, &src->ibox},   {&s->leaf, &src->leaf},
                                                       {&s->tnorm, &src->tnorm}, {&s->objids, &src->objids},
                                                       {&s->mats, &src->mats},   {&s->lights, &src->lights},
@@ -3509,6 +3592,8 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     std::memset(&P, 0, sizeof(P));
     P.sc.inode = static_cast<const float4*>(s->inode.p);
     P.sc.wnode = static_cast<const float4*>(s->wnode.p);
+    P.sc.fnode = static_cast<const float*>(s->fnode.p);
+    P.sc.f_log2 = s->fnode.p ? s->f_log2 : 2;
     P.sc.wide = s->wide && !(o->flags & RT_FLAG_BINARY) ? 1 : 0;
     P.sc.lane_stack = s->lane_stack ? 1 : 0;
     P.sc.lane_wide = s->lane_wide ? 1 : 0;

@@ -606,3 +606,60 @@ def test_hw1_timing_entry_point():
     rgb_b, ms_b = rt.render_hw1(*args, timing=True, brute=True)
     assert ms > 0 and ms_b > 0
     assert np.array_equal(rgb.view(np.uint32), rgb_b.view(np.uint32))
+
+
+@pytest.mark.parametrize("arity", ["2", "3", "4"])
+@pytest.mark.parametrize("name", ["c3_small", "frog_bounce", "sphere_single", "cornell", "c5_small", "c3b_small"])
+def test_frustum_record_arity_parity(name, arity, monkeypatch):
+    """The camera rays' frustum traversal over 4-, 8- and 16-ary records (RT_FRUSTUM_ARITY caps
+    the arity rt_scene_create picks): the reference's hits, t and frame bit for bit."""
+    monkeypatch.setenv("RT_FRUSTUM_ARITY", arity)
+    meta = golden_meta(name)
+    hs = host_scene(G_SCENES[name])
+    cam = hs.camera(meta["width"], meta["height"])
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    rgb, hi, ht = ds.render(cam, spp=meta["spp"], max_depth=meta["max_depth"],
+                            diffuse_bounce=bool(meta["diffuse_bounce"]), miss_color=hexv(meta["miss_color"]),
+                            aov=True)
+    assert np.array_equal(hi.reshape(-1), golden_array(name, "hits.i32.gz", np.int32))
+    assert np.array_equal(ht.reshape(-1).view(np.uint32),
+                          golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
+    _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
+
+
+@pytest.mark.parametrize("arity", ["3", "4"])
+@pytest.mark.parametrize("scene", ["frog.json", "cornell.json", "sphere_single.json"])
+def test_frustum_fuzz_cameras(scene, arity, monkeypatch):
+    """The frustum traversal's wave-level box test must pass whenever some lane's exact test
+    does: cameras aimed at box faces, edges and corners, along the axes (direction components
+    crossing zero inside a wave), from inside the scene's boxes, with tiny and wide fields of
+    view.  Frames (hits, t, colour) bit-identical to the binary-record traversal, which tests
+    every box for every lane."""
+    monkeypatch.setenv("RT_FRUSTUM_ARITY", arity)
+    hs = host_scene(scene)
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    lo, hi = hs.aabbs[0, :3].astype(np.float64), hs.aabbs[0, 3:].astype(np.float64)
+    ext = float(np.linalg.norm(hi - lo))
+    rng = np.random.default_rng(7)
+    axes = [np.array(v, np.float64) for v in ((1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1))]
+    for k in range(36):
+        if k % 3 == 0:  # along an axis: the centre column / row has a zero direction component
+            dirn = axes[k // 3 % 6]
+        else:
+            dirn = rng.normal(size=3)
+            dirn /= np.linalg.norm(dirn)
+        if k % 4 == 1:  # from inside the tree: a random internal box's centre
+            n = int(rng.integers(0, len(hs.aabbs)))
+            pos = (hs.aabbs[n, :3] + hs.aabbs[n, 3:]).astype(np.float64) / 2
+            target = pos - dirn * ext
+        else:
+            t = rng.choice([0.0, 1.0, 0.5, rng.uniform()], size=3)
+            target = lo + t * (hi - lo)
+            pos = target + dirn * ext * rng.choice([0.05, 0.6, 3.0])
+        fwd = target - pos
+        up = (0.0, 0.0, 1.0) if abs(fwd[2]) < 0.9 * np.linalg.norm(fwd) else (0.0, 1.0, 0.0)
+        cam = rt.Camera(tuple(pos), tuple(target), up, float(rng.choice([8.0, 35.0, 600.0])), 24.0, 96, 64)
+        a = ds.render(cam, spp=4, max_depth=1, aov=True)
+        b = ds.render(cam, spp=4, max_depth=1, aov=True, flags=rt._lib.RT_FLAG_BINARY)
+        for x, y in zip(a, b):
+            assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), k

@@ -20,4 +20,5 @@ fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$ROOT/build/obj/rt_host.o" "$OUT/rt_device.o" \
     "$ROOT/build/obj/rt_frame.o" "$ROOT/build/obj/rt_lbvh.o" "$ROOT/build/obj/rt_renderer.o" "$ROOT/build/obj/rt_build_id.o" \
     -o "$OUT/librt_mi355x.so"
+rm -f "$OUT/rt_device.o"  # only the library travels to the GPU box
 echo "$OUT/librt_mi355x.so"

@@ -154,6 +154,14 @@ struct RenderParams {
 __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
+// A lane id the compiler cannot merge with any other (mbcnt of an opaque zero): one kept for a
+// whole loop of items is live across all of them (and spills).
+__device__ __forceinline__ uint32_t fresh_lane_id() {
+    uint32_t z = 0;
+    asm volatile("" : "+s"(z));
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, z));
+}
+
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 // This lane's bit of a wave-uniform mask, the inverse of ballot: one v_cndmask on the SGPR pair
 // (`(m >> lane_id()) & 1` keeps a 64-bit lane bit live across the traversal loop, which the
@@ -640,7 +648,8 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
     const char* rec_b = sc.fnode != nullptr ? reinterpret_cast<const char*>(sc.fnode) : reinterpret_cast<const char*>(sc.wnode);
     const uint32_t rec_shift = 5u + lg;
     const uint32_t ent_mask = (1u << (1u << lg)) - 1u;
-    const uint32_t kl = lane_id() & ((1u << lg) - 1u);
+    // (a fresh lane id: lane_id() merged with the kernel's own was kept live across the item loop)
+    const uint32_t kl = fresh_lane_id() & ((1u << lg) - 1u);
     const uint32_t k6 = 6u * kl, kref = (6u << lg) + kl;  // this lane's entry, in floats
     while (true) {
         RT_STAT(2, 1);
@@ -2203,14 +2212,6 @@ __device__ __forceinline__ int work_tile(const RenderParams& P, int q, int e, in
         list = reinterpret_cast<const uint32_t*>(P.sc.ncut > 0 ? P.cut_tiles : P.live_tiles) + (size_t)q * P.queue_cap;
     }
     return (int)ldc_u32(list + e);
-}
-
-// A lane id the compiler cannot merge with any other (mbcnt of an opaque zero): one kept for a
-// whole loop of items is live across all of them (and spills).
-__device__ __forceinline__ uint32_t fresh_lane_id() {
-    uint32_t z = 0;
-    asm volatile("" : "+s"(z));
-    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, z));
 }
 
 // The next work item of a queue: one returning device-scope atomic from lane 0 (a vector

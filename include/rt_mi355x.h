@@ -408,6 +408,16 @@ int rt_powf_batch(int device, const float* x, const float* y, int n, float* out)
 int rt_box_test_host(const float* rays, const float* boxes, const float* tminmax, int n,
                      int32_t* out_fast, int32_t* out_exact, int32_t* out_class);
 
+/* Host build of the camera rays' frustum records rt_scene_create makes (no device): for a BVH
+ * of P triangles (the same arrays as rt_scene_create), the records of arity 2^info[0]
+ * (8 x 2^info[0] floats each: per entry the (min, max) pairs of x, y, z, then the entries'
+ * refs), info = {log2 arity (2: none fits), DFS stack bound, records}: the largest arity up to
+ * 2^max_log2 whose DFS needs at most stack_cap entries (64; 128 for the big-scene kernels).
+ * rec is written when rec_cap (floats) suffices; call with a null rec to size it.
+ * DESIGN.md §4.12. */
+int rt_debug_frustum_records(size_t P, const rt_bvh_node* nodes, const rt_aabb* aabbs, int max_log2, int stack_cap,
+                             int64_t* info, float* rec, size_t rec_cap);
+
 /* Durations (ms) of the render kernel of the most recent min(max, launches, 256)
  * rt_render_device calls on this scene, oldest first, measured with HIP events recorded
  * on the launch stream around the kernel.  Waits for those launches to finish. */

@@ -162,6 +162,7 @@ SIGNATURES = {
     "rt_render_hw1_ex": (I, [I, P, P, P, SZ, P, Vec3, Vec3, I, P, I, P, P, P, P]),
     "rt_intersect_rays": (I, [I, P, P, P, I, I, C.c_float, C.c_float, P, P]),
     "rt_powf_host": (C.c_float, [C.c_float, C.c_float]),
+    "rt_debug_frustum_records": (C.c_int, [C.c_size_t, P, P, C.c_int, C.c_int, P, P, C.c_size_t]),
     "rt_powf_batch": (I, [I, P, P, I, P]),
     "rt_box_test_host": (I, [P, P, P, I, P, P, P]),
     "rt_kernel_times": (I, [P, P, I, P]),

@@ -3740,7 +3740,9 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // 16 samples, measured slower at N = 8 and were dropped.)
     // The multi-bounce kernels take half waves at any split: a wave's bounce paths end with its
     // longest lane's, and the longest waves bound the kernel (c3b 1.96 vs 2.37 ms per frame).
-    int half = o->band_count >= 8 || o->max_depth > 1 ? 1 : 0;
+    // (With the frustum traversal, profiles/r04/exp/half_waves_ab_c3.log: N = 8 max kernel 0.0758
+    // vs 0.0867 ms, N = 4 0.0831 vs 0.0857, N = 2 0.140 vs 0.097: half waves from 4 shards.)
+    int half = o->band_count >= 4 || o->max_depth > 1 ? 1 : 0;
     if (const char* e = std::getenv("RT_HALF_WAVES")) half = std::clamp(std::atoi(e), 0, 1);
     if (!samples || o->spp > (64 >> half)) half = 0;
     P.half_waves = half;
@@ -3776,7 +3778,9 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // RT_HEAVY_FRAC (speed experiments): a tile is in heavy class c when one of its waves took
     // at least 2^(2-c) times this fraction of the latest finished frame's render kernel
     // (0: off).
-    double heavy_frac = 0.12;  // c3: 0.04 0.197, 0.06 0.188, 0.08 0.179, 0.12 0.177, 0.16 0.177 ms
+    // c3 (frustum traversal, profiles/r04/exp/heavy_frac_ab_c3*.log): 0.05 0.153, 0.06 0.149,
+    // 0.08 0.148, 0.10 0.147, 0.12 0.150, 0.18 0.151, 0.25 0.158 ms, off 0.187
+    double heavy_frac = 0.10;
     if (const char* e = std::getenv("RT_HEAVY_FRAC")) heavy_frac = std::atof(e);
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
     const bool costs = P.cull && P.sc.ncut > 0 && P.nqueues == 8 && heavy_frac > 0.0;

@@ -52,6 +52,8 @@ namespace {
 
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 constexpr uint32_t NO_REF = 0xFFFFFFFFu;
+// traverse_frustum's stack: two VGPRs, entry k in lane k of the first, 64 + k of the second
+constexpr int FRUSTUM_STACK = 128;
 constexpr uint32_t VER_FORCE = 0xFFFFFFFFu;   // pop must re-test (root)
 constexpr int STACK_CAP = 64;                 // one entry per lane of the wave stack
 constexpr int LANE_LDS_CAP = 32;              // traverse_lane_lds: per-lane stack entries in LDS (frog needs 18)
@@ -84,9 +86,7 @@ struct SceneView {
     const float4* __restrict__ inode;
     const float4* __restrict__ wnode;  // 4-ary records (8 x float4) by internal index, if wide
     const float* __restrict__ fnode;   // 2^f_log2-ary records (8 x 2^f_log2 floats) of traverse_frustum, or null
-    int32_t f_log2;                    // 3 or 4 with fnode; 2: traverse_frustum takes wnode
-    const float* __restrict__ fnode_big;  // big scenes: 16-ary records whose DFS needs <= 128 entries
-    int32_t f_log2_big;                   // (the one-light big-scene kernels' 2-VGPR stack), or null
+    int32_t f_log2;                    // 3..5 with fnode; 2: traverse_frustum takes wnode
     const float4* __restrict__ ibox;
     const float4* __restrict__ rootb;  // the root's box, pairs (x | y, z), after ibox's entries
     const float4* __restrict__ leaf;
@@ -603,11 +603,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
 //   entries take the 4-ary records the same way.
 // Scenes whose coordinates come within 1e30 of the float range give no bound on those axes
 // (products stay finite: |b - o| < 1e30, |1/d| <= 1e8).
-// BIG (the one-light big-scene kernels): the stack spans two VGPRs (128 entries), and the
-// traversal takes the scene's fnode_big records (16-ary) when it has them: c5's heightfield
-// needs 82 entries at arity 16 (45.9 vs 51.3 ms at arity 8); the other kernels keep one stack
-// VGPR (the second one's branches cost c3 2.4 %).
-template <bool PK = false, bool XL = false, bool BIG = false>
+template <bool PK = false, bool XL = false>
 __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayPre& r, bool active, HitState& hs) {
     hs.bestT = FLT_MAX;
     hs.slot = -1;
@@ -645,18 +641,15 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
     const float kW = 1.0f / 524288.0f;  // 2^-19
     float tmax_w = FLT_MAX;
     uint32_t ref = sc.root_ref;
-    uint32_t st_ref = 0, st_hi = 0;  // lane k holds entry k (BIG: st_hi entries 64 + k)
+    uint32_t st_ref = 0, st_hi = 0;  // lane k holds entry k, st_hi entries 64 + k (FRUSTUM_STACK)
     int sp = 0;
     const char* leaf_b = reinterpret_cast<const char*>(sc.leaf);
     // the wide records (fnode) when the scene has them, else the 4-ary ones (wnode): lane k
     // (mod the arity A = 2^f_log2) tests entry k; a record is 8A floats, refs at float 6A
-    const bool big = BIG && sc.fnode_big != nullptr;
-    const uint32_t lg = (uint32_t)(big ? sc.f_log2_big : sc.f_log2);
-    const char* rec_b = big ? reinterpret_cast<const char*>(sc.fnode_big)
-                        : sc.fnode != nullptr ? reinterpret_cast<const char*>(sc.fnode)
-                                              : reinterpret_cast<const char*>(sc.wnode);
+    const uint32_t lg = (uint32_t)sc.f_log2;
+    const char* rec_b = sc.fnode != nullptr ? reinterpret_cast<const char*>(sc.fnode) : reinterpret_cast<const char*>(sc.wnode);
     const uint32_t rec_shift = 5u + lg;
-    const uint32_t ent_mask = (1u << (1u << lg)) - 1u;
+    const uint32_t ent_mask = (uint32_t)((1ull << (1u << lg)) - 1ull);
     // (a fresh lane id: lane_id() merged with the kernel's own was kept live across the item loop)
     const uint32_t kl = fresh_lane_id() & ((1u << lg) - 1u);
     const uint32_t k6 = 6u * kl, kref = (6u << lg) + kl;  // this lane's entry, in floats
@@ -716,7 +709,7 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
                 next = rdlane(rk, hold);
                 for (uint32_t rest = m & ~(1u << hold); rest != 0; rest &= rest - 1u) {
                     const uint32_t e = rdlane(rk, __builtin_ctz(rest));
-                    if (!BIG || sp < 64) st_ref = wrlane(e, sp, st_ref);
+                    if (sp < 64) st_ref = wrlane(e, sp, st_ref);
                     else st_hi = wrlane(e, sp - 64, st_hi);
                     ++sp;
                 }
@@ -728,7 +721,7 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
         }
         if (sp == 0) break;
         --sp;
-        ref = (!BIG || sp < 64) ? rdlane(st_ref, sp) : rdlane(st_hi, sp - 64);
+        ref = sp < 64 ? rdlane(st_ref, sp) : rdlane(st_hi, sp - 64);
     }
 }
 
@@ -1026,8 +1019,7 @@ template <int MODE>
 __device__ __forceinline__ void traverse_camera(const SceneView& sc, const RayPre& r, bool active, HitState& hs) {
 #ifndef RT_NO_FRUSTUM
     if constexpr (MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0 && (MODE & MODE_WIDE) != 0) {
-        traverse_frustum<(MODE & MODE_PK) != 0, (MODE & MODE_PK) != 0 && (MODE & MODE_1L) == 0, (MODE & MODE_1L) != 0>(
-            sc, r, active, hs);
+        traverse_frustum<(MODE & MODE_PK) != 0, (MODE & MODE_PK) != 0 && (MODE & MODE_1L) == 0>(sc, r, active, hs);
         return;
     }
 #endif
@@ -2962,8 +2954,6 @@ struct rt_scene {
     float bmax[3] = {0, 0, 0};
     DevBuf inode, wnode, ibox, leaf, tnorm, objids, mats, lights, jitter;
     DevBuf fnode;    // 2^f_log2-ary records of the frustum traversal (empty: it takes wnode's 4-ary ones)
-    DevBuf fnode_big;  // big scenes: records for the 2-VGPR-stack kernels (build_frustum_records)
-    int f_log2_big = 2;
     int f_log2 = 2;
     DevBuf cut;  // tile culling: boxes of a cut of the tree (6 floats each)
     int ncut = 0;
@@ -3051,9 +3041,9 @@ extern "C" int rt_device_count(int* n) {
 // triangle is skipped, as in the 4-ary records.  Records by their own index (an internal entry's
 // ref is its record's), 8A floats: A x (x pair, y pair, z pair) | A refs (NO_REF pads) | unused.
 // Exact for the reason the 4-ary records are (every internal box contains its children's,
-// wide_ok).  The largest A in {16, 8} (at most 2^dmax) whose DFS needs at most `cap` stack
-// entries (frog: 16, bound 59 <= 64; the c5 heightfield: 8 at 64 (bound 50), 16 at 128 (82));
-// log2 = 2 when none fits (the frustum traversal then takes the 4-ary records, wnode).
+// wide_ok).  The largest A in {32, 16, 8} (at most 2^dmax) whose DFS needs at most `cap` stack
+// entries (FRUSTUM_STACK = 128: frog 32, bound 91; the c5 heightfield 32, bound 126); log2 = 2
+// when none fits (the frustum traversal then takes the 4-ary records, wnode).
 // cid: compact ids as rt_scene_create makes them (LEAF_BIT | slot, internal index, or NO_REF).
 // (Leaf-pair entries, an internal node with two leaf children tested in one pop, measured no
 // faster: c3 0.1517 vs 0.1517 ms, c5 48.2 vs 45.9; profiles/r04/exp/pairs_stack128_ab_*.log.)
@@ -3067,7 +3057,7 @@ static FrustumRecords build_frustum_records(const rt_bvh_node* nodes, size_t NN,
                                             const rt_aabb* aabbs, int dmax, int cap) {
     FrustumRecords out;
     auto ref_of0 = [&](uint32_t n) -> uint32_t { return n == NO_REF ? NO_REF : cid[n]; };
-    for (int D = dmax; D >= 3; --D) {
+    for (int D = std::min(dmax, 5); D >= 3; --D) {
         const int A = 1 << D;
         auto expand = [&](auto&& self, uint32_t n, int d, uint32_t* e, int& k) -> void {
             if (ref_of0(n) == NO_REF) return;
@@ -3081,10 +3071,10 @@ static FrustumRecords build_frustum_records(const rt_bvh_node* nodes, size_t NN,
         std::vector<uint32_t> recs{0u};  // binary node of each record, breadth first
         std::vector<uint32_t> fid(NN, NO_REF);
         fid[0] = 0;
-        std::vector<std::array<uint32_t, 16>> ents;
+        std::vector<std::array<uint32_t, 32>> ents;
         std::vector<int> nent;
         for (size_t r = 0; r < recs.size(); ++r) {
-            std::array<uint32_t, 16> e;
+            std::array<uint32_t, 32> e;
             int k = 0;
             expand(expand, nodes[recs[r]].left_idx, D - 1, e.data(), k);
             expand(expand, nodes[recs[r]].right_idx, D - 1, e.data(), k);
@@ -3142,7 +3132,7 @@ extern "C" int rt_debug_frustum_records(size_t P, const rt_bvh_node* nodes, cons
         if (nodes[n].object_idx == 0xFFFFFFFFu) cid[n] = uint32_t(n_int++);
         else if (nodes[n].object_idx < P) cid[n] = LEAF_BIT | uint32_t(n_leaf++);
     }
-    const FrustumRecords fr = build_frustum_records(nodes, NN, cid.data(), aabbs, std::clamp(max_log2, 2, 4), stack_cap);
+    const FrustumRecords fr = build_frustum_records(nodes, NN, cid.data(), aabbs, std::clamp(max_log2, 2, 5), stack_cap);
     info[0] = fr.log2;
     info[1] = fr.bound;
     info[2] = (int64_t)fr.nrec;
@@ -3389,15 +3379,15 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     }
     if ((rc = s->inode.upload(hin.data(), hin.size() * sizeof(float4))) != RT_OK) return rc;
     if (wide_ok && (rc = s->wnode.upload(hwn.data(), hwn.size() * sizeof(float4))) != RT_OK) return rc;
-    // the camera rays' frustum records (build_frustum_records), for the traversal's 64-entry stack
-    int fr_dmax = 4;  // RT_FRUSTUM_ARITY: the largest arity's log2 to try (tests; 2 = the 4-ary records)
-    if (const char* e = std::getenv("RT_FRUSTUM_ARITY")) fr_dmax = std::clamp(std::atoi(e), 2, 4);
+    // the camera rays' frustum records (build_frustum_records), for the traversal's 128-entry stack
+    int fr_dmax = 5;  // RT_FRUSTUM_ARITY: the largest arity's log2 to try (tests; 2 = the 4-ary records)
+    if (const char* e = std::getenv("RT_FRUSTUM_ARITY")) fr_dmax = std::clamp(std::atoi(e), 2, 5);
 #ifdef RT_NO_F16  // (variant builds for A/B runs: the frustum traversal over the 4-ary records)
     fr_dmax = 2;
 #endif
     const bool frustum = wide_ok && !(s->root_ref & LEAF_BIT) && fr_dmax > 2;
     if (frustum) {
-        const FrustumRecords fr = build_frustum_records(nodes, NN, cid.data(), aabbs, fr_dmax, STACK_CAP);
+        const FrustumRecords fr = build_frustum_records(nodes, NN, cid.data(), aabbs, fr_dmax, FRUSTUM_STACK);
         if (fr.log2 > 2) {
             if ((rc = s->fnode.upload(fr.rec.data(), fr.rec.size() * sizeof(float))) != RT_OK) return rc;
             s->f_log2 = fr.log2;
@@ -3430,16 +3420,6 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     if ((rc = s->create_sync()) != RT_OK) return rc;
     s->bytes = s->inode.n + s->wnode.n + s->fnode.n + s->ibox.n + s->leaf.n + s->tnorm.n + s->objids.n +
                s->mats.n + s->lights.n;
-    // Big scenes (the one-light big-scene kernels, whose traversal has a 128-entry stack): the
-    // 16-ary records when the 64-entry stack kept a smaller arity
-    if (frustum && s->f_log2 < fr_dmax && s->bytes > kBigSceneBytes) {
-        const FrustumRecords fb = build_frustum_records(nodes, NN, cid.data(), aabbs, fr_dmax, 2 * STACK_CAP);
-        if (fb.log2 > s->f_log2) {
-            if ((rc = s->fnode_big.upload(fb.rec.data(), fb.rec.size() * sizeof(float))) != RT_OK) return rc;
-            s->f_log2_big = fb.log2;
-            s->bytes += s->fnode_big.n;
-        }
-    }
     *out = s.release();
     return RT_OK;
 }
@@ -3464,13 +3444,12 @@ extern "C" int rt_scene_clone(const rt_scene* src, int device, rt_scene** out) {
     s->lane_stack = src->lane_stack;
     s->lane_wide = src->lane_wide;
     s->f_log2 = src->f_log2;
-    s->f_log2_big = src->f_log2_big;
     s->deep = src->deep;
     s->cus = src->cus;
     s->bytes = src->bytes;
     // device-to-device copies of the packed arrays (over xGMI when the devices differ)
     const std::pair<DevBuf*, const DevBuf*> bufs[] = {{&s->inode, &src->inode}, {&s->wnode, &src->wnode},
-                                                      {&s->fnode, &src->fnode}, {&s->fnode_big, &src->fnode_big},
+                                                      {&s->fnode, &src->fnode},
                                                       {&s->ibox, &src->ibox},   {&s->leaf, &src->leaf},
                                                       {&s->tnorm, &src->tnorm}, {&s->objids, &src->objids},
                                                       {&s->mats, &src->mats},   {&s->lights, &src->lights},
@@ -3680,8 +3659,6 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.sc.wnode = static_cast<const float4*>(s->wnode.p);
     P.sc.fnode = static_cast<const float*>(s->fnode.p);
     P.sc.f_log2 = s->fnode.p ? s->f_log2 : 2;
-    P.sc.fnode_big = static_cast<const float*>(s->fnode_big.p);
-    P.sc.f_log2_big = s->fnode_big.p ? s->f_log2_big : 2;
     P.sc.wide = s->wide && !(o->flags & RT_FLAG_BINARY) ? 1 : 0;
     P.sc.lane_stack = s->lane_stack ? 1 : 0;
     P.sc.lane_wide = s->lane_wide ? 1 : 0;

@@ -8,8 +8,8 @@ checked on the host through rt_debug_frustum_records: no GPU.
   yields the leaves in exactly the order SearchBVH's own DFS does when every box passes
   (G/include/query.h:224-311: push left, push right, pop) -- the order the traversal's
   exactness rests on;
-* the stack bound the builder reports covers that DFS and fits the stack it was asked for (64
-  entries; 128 for the big-scene kernels), and the arity is the largest one that fits.
+* the stack bound the builder reports covers that DFS and fits the stack it was asked for (the
+  traversal's 128 entries; smaller caps too), and the arity is the largest one that fits.
 """
 from __future__ import annotations
 
@@ -156,11 +156,13 @@ def check(P, nodes, aabbs, max_log2=4, cap=64):
     return m, log2, bound
 
 
+@pytest.mark.parametrize("cap,max_log2", [(128, 5), (64, 4)])
 @pytest.mark.parametrize("scene", ["frog.json", "cornell.json", "sphere_single.json", "sphere.json"])
-def test_shipped_scene_records(scene):
+def test_shipped_scene_records(scene, cap, max_log2):
+    """(128, 5): what rt_scene_create builds (32-ary records for frog, bound 91)."""
     hs = host_scene(scene)
-    _, log2, bound = check(hs.num_triangles, hs.nodes, hs.aabbs)
-    assert log2 == 4, (log2, bound)
+    _, log2, bound = check(hs.num_triangles, hs.nodes, hs.aabbs, max_log2, cap)
+    assert log2 == max_log2, (log2, bound)
 
 
 def test_arity_cap():
@@ -217,5 +219,6 @@ def test_random_trees(seed):
     P = int(rng.integers(2, 400))
     nodes, aabbs = random_tree(rng, P, invalid_frac=0.15 if seed % 2 else 0.0)
     for cap in (64, 128, 24):
+        check(P, nodes, aabbs, 5, cap)
         check(P, nodes, aabbs, 4, cap)
         check(P, nodes, aabbs, 3, cap)

@@ -2237,7 +2237,8 @@ template <int MODE, bool D1, int LS = 0>
 __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, uint32_t qw, int t, float* col,
                                              int* kpix, float* park, const int* lds_zero) {
     const uint32_t wv = uni((uint32_t)t) >> 6;  // the wave's index in the block (an SGPR)
-    // LS = 1, half waves (band shards of a multi-GPU frame, spp <= 32): each wave traces 32
+    // LS = 1 or 2, half waves (band shards of a multi-GPU frame, spp <= 32; LS = 2: the bounce
+    // kernels for several lights, no paired path): each wave traces 32
     // samples in its low lanes, so a tile's longest wave, which bounds a short kernel, has half
     // the rays' path union; lt is the sample's index in the (half-size) tile.  A template
     // parameter: a run-time flag here cost the full-wave c3 kernel 0.8 % (register allocation).
@@ -3569,7 +3570,11 @@ void launch_mode(const RenderParams& P, const Launch& L) {
         }
         if constexpr (SAMPLES) {
             if (P.half_waves) {
-                launch_render<MODE, SAMPLES, false, RT_BOUNCE_WAVES, 1>(P, L);
+                // LS = 1 carries paired_bounces beside the unpaired loop (one light, chosen per
+                // scene at run time); scenes with several lights take LS = 2, the unpaired loop
+                // alone (LS = 1 keeps 84 B of scratch per lane for it: cornell wrote 0.63 GB per launch)
+                if (P.sc.num_lights == 1) launch_render<MODE, SAMPLES, false, RT_BOUNCE_WAVES, 1>(P, L);
+                else launch_render<MODE, SAMPLES, false, RT_BOUNCE_WAVES, 2>(P, L);
                 return;
             }
         }

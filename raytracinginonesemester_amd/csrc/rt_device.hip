@@ -2237,8 +2237,8 @@ template <int MODE, bool D1, int LS = 0>
 __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, uint32_t qw, int t, float* col,
                                              int* kpix, float* park, const int* lds_zero) {
     const uint32_t wv = uni((uint32_t)t) >> 6;  // the wave's index in the block (an SGPR)
-    // LS = 1 or 2, half waves (band shards of a multi-GPU frame, spp <= 32; LS = 2: the bounce
-    // kernels for several lights, no paired path): each wave traces 32
+    // LS = 1, half waves (band shards of a multi-GPU frame, spp <= 32; the bounce kernels'
+    // unpaired loop): each wave traces 32
     // samples in its low lanes, so a tile's longest wave, which bounds a short kernel, has half
     // the rays' path union; lt is the sample's index in the (half-size) tile.  A template
     // parameter: a run-time flag here cost the full-wave c3 kernel 0.8 % (register allocation).
@@ -2273,7 +2273,7 @@ __device__ __forceinline__ void samples_tile(const RenderParams& P, int tile, ui
         // it, or addresses made from it, live (and spilled) across the shading.
         if (s == 0) kpix[t >> P.spp_log2] = pix;
         const int64_t aov = valid && P.hit_idx ? (int64_t)pix * P.spp + s : -1;
-        const f3 c = trace_sample<MODE, D1, LS == 3 ? 2 : (LS == 1 ? 1 : 0)>(P, valid, x, y, s, aov, park + t,
+        const f3 c = trace_sample<MODE, D1, LS == 3 ? 2 : 0>(P, valid, x, y, s, aov, park + t,
                                                                              park + (wv << 6));
         RT_PHASE(P, x, r, 1);
         // The thread index again, from the wave's index and a lane id the compiler cannot
@@ -3570,11 +3570,10 @@ void launch_mode(const RenderParams& P, const Launch& L) {
         }
         if constexpr (SAMPLES) {
             if (P.half_waves) {
-                // LS = 1 carries paired_bounces beside the unpaired loop (one light, chosen per
-                // scene at run time); scenes with several lights take LS = 2, the unpaired loop
-                // alone (LS = 1 keeps 84 B of scratch per lane for it: cornell wrote 0.63 GB per launch)
-                if (P.sc.num_lights == 1) launch_render<MODE, SAMPLES, false, RT_BOUNCE_WAVES, 1>(P, L);
-                else launch_render<MODE, SAMPLES, false, RT_BOUNCE_WAVES, 2>(P, L);
+                // the unpaired loop alone (one-light scenes whose lanes can pair take LS = 3 above;
+                // carrying paired_bounces here as well cost 84 B of scratch per lane: cornell 7.94
+                // vs 7.06 ms, profiles/r04/exp/ls2_ab_cornell.log)
+                launch_render<MODE, SAMPLES, false, RT_BOUNCE_WAVES, 1>(P, L);
                 return;
             }
         }
@@ -3730,7 +3729,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.half_waves = half;
     // One light and a tree whose DFS fits the per-lane LDS stacks: the bounce kernels that hold
     // only the paired loop (paired_bounces), fewer live registers than the kernels that also
-    // carry the unpaired one.  RT_PAIRED_ONLY=0 turns them off (A/B).
+    // carry the unpaired one.  RT_PAIRED_ONLY=0 turns them off (A/B: the unpaired loop on half waves).
     P.paired_only = half && o->max_depth > 1 && s->nlights == 1 && !s->deep && o->kernel != RT_KERNEL_LANE &&
                             (P.sc.wide ? s->lane_wide : s->lane_stack)
                         ? 1

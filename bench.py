@@ -90,6 +90,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
+    ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
+                    help="library tuning knob (rt_tuning_set, include/rt_mi355x.h), e.g. peer_timeout_s=60; "
+                         "named in the line's config when set")
     ap.add_argument("--traffic-file", default=str(REPO / "profiles" / "traffic.json"),
                     help="per-launch HBM bytes and issue counters measured by rocprofv3 --pmc (DESIGN.md §5)")
     return ap.parse_args()
@@ -599,6 +602,9 @@ def lbvh_times(hs, device: int, reps: int = 5) -> dict:
 
 def main():
     a = parse()
+    for kv in a.tune:
+        k, _, v = kv.partition("=")
+        rt.set_tuning(k, float(v))
     ctx = Ctx(a)
     world, rank = ctx.world, ctx.rank
     cfg = configs.G_CONFIGS[a.config]
@@ -683,6 +689,8 @@ def main():
         "pipeline_depth": a.depth if comm == "native" else 2, "kernel": a.kernel}
     if a.share_gpu and world > 1:
         line["config"]["rehearsal"] = "--share-gpu: ranks share GPUs (not a multi-GPU measurement)"
+    if a.tune:
+        line["config"]["tuning"] = dict(kv.partition("=")[::2] for kv in a.tune)
     if fallback:
         line["config"]["fallback"] = fallback
     if res.get("gather_note"):

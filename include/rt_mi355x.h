@@ -36,7 +36,8 @@ enum {
     RT_ERR_NOMEM = -5,
     RT_ERR_NODEVICE = -6,     /* no gfx950 device / code object not loadable */
     RT_ERR_UNSUPPORTED = -7,  /* input outside what the kernels handle (see rt_last_error) */
-    RT_ERR_COMM = -8          /* RCCL could not be loaded or a collective failed */
+    RT_ERR_COMM = -8,         /* RCCL could not be loaded or a collective failed */
+    RT_ERR_INTERNAL = -9      /* a device-side guard fired (rt_scene_faults); the frame is not valid */
 };
 
 /* ---- reference POD types ------------------------------------------------------------ */
@@ -441,6 +442,43 @@ int rt_heavy_tiles(const rt_scene* s, int64_t* heavy);
  * names it ("render_tiles_kernel<49, true, true, 7, 0>"; "" before the first frame): bench.py
  * keys its measured per-launch HBM traffic by it. */
 const char* rt_scene_kernel_name(const rt_scene* s);
+
+/* Traversal setup rt_scene_create chose for s: info = {log2 of the camera rays' frustum-record
+ * arity (3..5; 2 = the 4-ary records; 0 = no frustum traversal), their DFS stack bound
+ * (<= 128 unless RT_TUNE_FRUSTUM_STACK_CAP raised it), 1 if the 4-ary records exist, 1 if the
+ * scene takes the deep (512-entry stack) kernels}. */
+int rt_scene_traversal_info(const rt_scene* s, int64_t info[4]);
+/* Device-side fault flags of s, OR-ed by the kernels since the last clear (waits for the
+ * scene's work): bit 0 = a camera-ray frustum traversal needed more than its 128 stack
+ * entries (the host bound makes this impossible for records built with the default cap; the
+ * wave's answers were poisoned: no hit).  clear != 0 resets the flags.  rt_render
+ * returns RT_ERR_INTERNAL when a frame raised one. */
+int rt_scene_faults(rt_scene* s, uint32_t* flags, int clear);
+
+/* ---- Tuning knobs (process-wide; read when a scene is created or a frame is set up) ----
+ * The library reads no environment variables: every setting that selects among exact kernel
+ * variants or schedules is set here, by tests and A/B scripts.  Frames are identical under
+ * every value (order of work only), except RT_TUNE_FRUSTUM_STACK_CAP, a test hook. */
+typedef enum {
+    RT_TUNE_FRUSTUM_ARITY = 0,   /* log2 of the largest frustum-record arity to build, 2..5 (5) */
+    RT_TUNE_HALF_WAVES = 1,      /* -1 auto (default: from 4 band shards, and multi-bounce), 0, 1 */
+    RT_TUNE_PAIRED_ONLY = 2,     /* 1 (default): one-light bounce frames take the paired-only kernels */
+    RT_TUNE_HEAVY_FRAC = 3,      /* heavy-first class threshold, fraction of a frame (0.10; 0 = off) */
+    RT_TUNE_HEAVY_CAP = 4,       /* heavy-list entries per (class, list) (512) */
+    RT_TUNE_CULL_COVERAGE = 5,   /* the cut pass runs when the root box covers <= this (0.3; >= 1: always) */
+    RT_TUNE_CULL_BOXES = 6,      /* boxes of the tile-culling cut (64; at scene creation) */
+    RT_TUNE_BIG_SCENE_BYTES = 7, /* scenes above this take the 8-wave depth-1 kernel (64 MiB) */
+    RT_TUNE_FRUSTUM_STACK_CAP = 8, /* TEST HOOK: stack bound the frustum records may need (128) */
+    RT_TUNE_PEER_TIMEOUT_S = 9,  /* rt_renderer: seconds to wait for a peer rank (120) */
+    RT_TUNE_RENDERER_THREADS = 10, /* rt_renderer: -1 auto (default: a thread per further distinct
+                                      GPU), 0 submit every rank from the caller, 1 threads always */
+    RT_TUNE_COUNT = 11
+} rt_tune_id;
+/* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */
+int rt_tuning_set(int id, double value);
+/* The value set for id, or NaN when it has its default. */
+int rt_tuning_get(int id, double* value);
+void rt_tuning_reset(void);
 
 int rt_device_count(int* n);
 const char* rt_last_error(void);

@@ -10,5 +10,5 @@ from ._lib import (RTError, RT_DELIVER_DEVICE, RT_DELIVER_F32, RT_DELIVER_NONE, 
 from .api import (  # noqa: F401
     LIGHT_DTYPE, Camera, DeviceScene, HostScene, MeshHW1, Renderer, build_bvh, comm_unique_id, build_bvh_device, default_material, device_count,
     encode_p6, encode_p6_device, intersect_rays, jittered_samples, p6_header, quantize_p6_device, read_p6,
-    render, render_hw1, unpermute_strips_device, write_p6,
+    render, render_hw1, unpermute_strips_device, write_p6, set_tuning, get_tuning, reset_tuning, tuning,
 )

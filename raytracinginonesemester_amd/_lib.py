@@ -16,6 +16,7 @@ RT_OK = 0
 RT_ERR = {
     -1: "RT_ERR_ARG", -2: "RT_ERR_IO", -3: "RT_ERR_PARSE", -4: "RT_ERR_HIP",
     -5: "RT_ERR_NOMEM", -6: "RT_ERR_NODEVICE", -7: "RT_ERR_UNSUPPORTED", -8: "RT_ERR_COMM",
+    -9: "RT_ERR_INTERNAL",
 }
 RT_KERNEL_AUTO, RT_KERNEL_WAVE, RT_KERNEL_LANE, RT_KERNEL_WAVE_PIXELS = 0, 1, 2, 3
 RT_TILES_AUTO, RT_TILES_LINEAR, RT_TILES_XCD_CHUNK, RT_TILES_ROWS = 0, 1, 2, 3
@@ -25,6 +26,11 @@ RT_DELIVER_P6, RT_DELIVER_F32, RT_DELIVER_DEVICE, RT_DELIVER_NONE = 0, 1, 2, 3
 RT_GATHER_AUTO, RT_GATHER_RCCL, RT_GATHER_DIRECT, RT_GATHER_HOST_SHARED = 0, 1, 2, 3
 RT_RENDERER_SELF_SEND = 1
 RT_TIME_GATHER, RT_TIME_DELIVER, RT_TIME_FRAME = 0, 1, 2
+RT_FAULT_FRUSTUM_STACK = 1
+# rt_tune_id (include/rt_mi355x.h): knob name -> id
+TUNE = {"frustum_arity": 0, "half_waves": 1, "paired_only": 2, "heavy_frac": 3, "heavy_cap": 4,
+        "cull_coverage": 5, "cull_boxes": 6, "big_scene_bytes": 7, "frustum_stack_cap": 8,
+        "peer_timeout_s": 9, "renderer_threads": 10}
 
 
 class RTError(RuntimeError):
@@ -171,6 +177,11 @@ SIGNATURES = {
     "rt_live_tiles": (I, [P, P, P]),
     "rt_heavy_tiles": (I, [P, P]),
     "rt_scene_kernel_name": (C.c_char_p, [P]),
+    "rt_scene_traversal_info": (I, [P, P]),
+    "rt_scene_faults": (I, [P, P, I]),
+    "rt_tuning_set": (I, [I, C.c_double]),
+    "rt_tuning_get": (I, [I, P]),
+    "rt_tuning_reset": (None, []),
     "rt_device_count": (I, [P]),
     "rt_last_error": (C.c_char_p, []),
     "rt_abi_version": (I, []),

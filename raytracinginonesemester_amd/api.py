@@ -326,6 +326,19 @@ class DeviceScene:
         check(lib().rt_prepass_times(self._handle(), ptr(out), max_launches, C.byref(n)))
         return out[:n.value]
 
+    def traversal_info(self) -> dict:
+        """The traversal rt_scene_create chose (rt_scene_traversal_info)."""
+        info = (C.c_int64 * 4)()
+        check(lib().rt_scene_traversal_info(self._handle(), info))
+        return {"frustum_log2": int(info[0]), "frustum_bound": int(info[1]), "wide": bool(info[2]),
+                "deep": bool(info[3])}
+
+    def faults(self, clear: bool = True) -> int:
+        """RT_FAULT_* bits the device guards raised since the last clear (rt_scene_faults)."""
+        f = C.c_uint32()
+        check(lib().rt_scene_faults(self._handle(), C.byref(f), 1 if clear else 0))
+        return f.value
+
     def close(self) -> None:
         if self._h and self._owned:
             lib().rt_scene_destroy(self._h)
@@ -623,6 +636,42 @@ def encode_p6_device(rgb, maxval=255, clamp=True, gamma2=True, flip_y=False):
     stream = torch.cuda.current_stream(rgb.device).cuda_stream
     quantize_p6_device(rgb.data_ptr(), W, H, body.data_ptr(), maxval, clamp, gamma2, flip_y, stream)
     return p6_header(W, H, maxval) + body.cpu().numpy().tobytes()
+
+
+def set_tuning(name: str, value) -> None:
+    """Process-wide tuning knob (rt_tuning_set; include/rt_mi355x.h rt_tune_id): None restores
+    its default.  Read when a scene is created or a frame is set up."""
+    check(lib().rt_tuning_set(L.TUNE[name], float("nan") if value is None else float(value)))
+
+
+def get_tuning(name: str):
+    """The value set for a knob, or None when it has its default."""
+    v = C.c_double()
+    check(lib().rt_tuning_get(L.TUNE[name], C.byref(v)))
+    return None if v.value != v.value else v.value
+
+
+def reset_tuning() -> None:
+    lib().rt_tuning_reset()
+
+
+class tuning:
+    """Context manager: ``with rt.tuning(half_waves=1): ...`` sets knobs, restores them after."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+        self.saved = {}
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            self.saved[k] = get_tuning(k)
+            set_tuning(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            set_tuning(k, v)
+        return False
 
 
 def device_count() -> int:

@@ -14,6 +14,9 @@ namespace rt {
 int set_error(int code, const std::string& msg);
 void clear_error();
 
+// Knob id's value set through rt_tuning_set, else dflt (include/rt_mi355x.h, rt_tune_id).
+double tuning(int id, double dflt);
+
 // Float vector helpers with the reference's evaluation order (G/include/vec3.h:327-348).
 inline rt_vec3 v3(float x, float y, float z) { return rt_vec3{x, y, z}; }
 inline rt_vec3 operator+(rt_vec3 a, rt_vec3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }

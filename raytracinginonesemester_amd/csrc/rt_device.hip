@@ -54,6 +54,7 @@ constexpr uint32_t LEAF_BIT = 0x80000000u;
 constexpr uint32_t NO_REF = 0xFFFFFFFFu;
 // traverse_frustum's stack: two VGPRs, entry k in lane k of the first, 64 + k of the second
 constexpr int FRUSTUM_STACK = 128;
+constexpr uint32_t RT_FAULT_FRUSTUM_STACK = 1u;  // rt_scene_faults bit 0
 constexpr uint32_t VER_FORCE = 0xFFFFFFFFu;   // pop must re-test (root)
 constexpr int STACK_CAP = 64;                 // one entry per lane of the wave stack
 constexpr int LANE_LDS_CAP = 32;              // traverse_lane_lds: per-lane stack entries in LDS (frog needs 18)
@@ -104,6 +105,7 @@ struct SceneView {
     const float* __restrict__ cut;  // tile culling: boxes of a cut of the tree (6 floats each)
     int32_t ncut;
     const float4* __restrict__ tri;  // deep trees: v0 | e1, e2.x | e2.y, e2.z by triangle index (brute force)
+    uint32_t* fault;  // RT_FAULT_* bits the kernels OR in (rt_scene_faults)
 };
 
 __device__ __forceinline__ f3 scene_bmax(const SceneView& sc) { return mk(sc.bmax[0], sc.bmax[1], sc.bmax[2]); }
@@ -643,6 +645,11 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
     uint32_t ref = sc.root_ref;
     uint32_t st_ref = 0, st_hi = 0;  // lane k holds entry k, st_hi entries 64 + k (FRUSTUM_STACK)
     int sp = 0;
+    // A push past FRUSTUM_STACK (records whose DFS bound exceeds it: rt_scene_create never
+    // builds them; RT_TUNE_FRUSTUM_STACK_CAP can, for the test of this guard) drops the entry
+    // instead of wrapping a lane index over live ones; the wave's answers are then poisoned
+    // (no hit) and RT_FAULT_FRUSTUM_STACK is raised for rt_render to report.
+    bool ovf = false;
     const char* leaf_b = reinterpret_cast<const char*>(sc.leaf);
     // the wide records (fnode) when the scene has them, else the 4-ary ones (wnode): lane k
     // (mod the arity A = 2^f_log2) tests entry k; a record is 8A floats, refs at float 6A
@@ -709,8 +716,14 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
                 next = rdlane(rk, hold);
                 for (uint32_t rest = m & ~(1u << hold); rest != 0; rest &= rest - 1u) {
                     const uint32_t e = rdlane(rk, __builtin_ctz(rest));
-                    if (sp < 64) st_ref = wrlane(e, sp, st_ref);
-                    else st_hi = wrlane(e, sp - 64, st_hi);
+                    if (sp < 64) {
+                        st_ref = wrlane(e, sp, st_ref);
+                    } else if (sp < FRUSTUM_STACK) {
+                        st_hi = wrlane(e, sp - 64, st_hi);
+                    } else {  // never with records built for this stack (the host bound)
+                        ovf = true;
+                        continue;
+                    }
                     ++sp;
                 }
             }
@@ -722,6 +735,11 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
         if (sp == 0) break;
         --sp;
         ref = sp < 64 ? rdlane(st_ref, sp) : rdlane(st_hi, sp - 64);
+    }
+    if (ovf) {
+        if (lane_id() == 0) atomicOr(sc.fault, RT_FAULT_FRUSTUM_STACK);
+        hs.bestT = __int_as_float(0x7fc00000);
+        hs.slot = -1;
     }
 }
 
@@ -2956,6 +2974,8 @@ struct rt_scene {
     DevBuf inode, wnode, ibox, leaf, tnorm, objids, mats, lights, jitter;
     DevBuf fnode;    // 2^f_log2-ary records of the frustum traversal (empty: it takes wnode's 4-ary ones)
     int f_log2 = 2;
+    int f_bound = 0;  // their DFS stack bound (<= FRUSTUM_STACK unless RT_TUNE_FRUSTUM_STACK_CAP raised it)
+    DevBuf fault;     // one word: RT_FAULT_* bits the kernels OR in (rt_scene_faults)
     DevBuf cut;  // tile culling: boxes of a cut of the tree (6 floats each)
     int ncut = 0;
     bool deep = false;  // the DFS may need more than STACK_CAP entries: MODE_DEEP kernels
@@ -3017,6 +3037,8 @@ struct rt_scene {
         int lo = 0, hi = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
         HIP_TRY(hipStreamCreateWithPriority(&prep, hipStreamNonBlocking, hi));
+        if (int rc = fault.alloc(sizeof(uint32_t)); rc != RT_OK) return rc;
+        HIP_TRY(hipMemset(fault.p, 0, sizeof(uint32_t)));
         for (int i = 0; i < kRing; ++i) {
             HIP_TRY(hipEventCreate(&ev0[i]));
             HIP_TRY(hipEventCreate(&evm[i]));
@@ -3342,8 +3364,8 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     // with the largest box (half surface area) by its children, up to kCut nodes.  Every leaf
     // keeps exactly one ancestor-or-self in the set; a missing child (NO_REF) holds no leaf.
     if (cid[0] != NO_REF && !(cid[0] & LEAF_BIT)) {
-        int kcut = 64;  // one box per lane of tile_cut_kernel
-        if (const char* e = std::getenv("RT_CULL_BOXES")) kcut = std::min(64, std::max(0, std::atoi(e)));
+        // one box per lane of tile_cut_kernel (RT_TUNE_CULL_BOXES: fewer, for tests)
+        const int kcut = int(std::clamp(rt::tuning(RT_TUNE_CULL_BOXES, 64.0), 0.0, 64.0));
         auto area = [&](uint32_t n) {
             const rt_aabb& bb = aabbs[n];
             const double dx = double(bb.max_corner.x) - bb.min_corner.x, dy = double(bb.max_corner.y) - bb.min_corner.y,
@@ -3381,17 +3403,21 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     if ((rc = s->inode.upload(hin.data(), hin.size() * sizeof(float4))) != RT_OK) return rc;
     if (wide_ok && (rc = s->wnode.upload(hwn.data(), hwn.size() * sizeof(float4))) != RT_OK) return rc;
     // the camera rays' frustum records (build_frustum_records), for the traversal's 128-entry stack
-    int fr_dmax = 5;  // RT_FRUSTUM_ARITY: the largest arity's log2 to try (tests; 2 = the 4-ary records)
-    if (const char* e = std::getenv("RT_FRUSTUM_ARITY")) fr_dmax = std::clamp(std::atoi(e), 2, 5);
+    // RT_TUNE_FRUSTUM_ARITY: the largest arity's log2 to try (tests; 2 = the 4-ary records)
+    int fr_dmax = int(std::clamp(rt::tuning(RT_TUNE_FRUSTUM_ARITY, 5.0), 2.0, 5.0));
 #ifdef RT_NO_F16  // (variant builds for A/B runs: the frustum traversal over the 4-ary records)
     fr_dmax = 2;
 #endif
     const bool frustum = wide_ok && !(s->root_ref & LEAF_BIT) && fr_dmax > 2;
     if (frustum) {
-        const FrustumRecords fr = build_frustum_records(nodes, NN, cid.data(), aabbs, fr_dmax, FRUSTUM_STACK);
+        // RT_TUNE_FRUSTUM_STACK_CAP (test hook only): records whose DFS may outgrow the stack,
+        // to exercise traverse_frustum's overflow guard
+        const int cap = int(std::clamp(rt::tuning(RT_TUNE_FRUSTUM_STACK_CAP, double(FRUSTUM_STACK)), 1.0, 1e6));
+        const FrustumRecords fr = build_frustum_records(nodes, NN, cid.data(), aabbs, fr_dmax, cap);
         if (fr.log2 > 2) {
             if ((rc = s->fnode.upload(fr.rec.data(), fr.rec.size() * sizeof(float))) != RT_OK) return rc;
             s->f_log2 = fr.log2;
+            s->f_bound = fr.bound;
         }
     }
     s->wide = wide_ok && !(s->root_ref & LEAF_BIT);
@@ -3445,6 +3471,7 @@ extern "C" int rt_scene_clone(const rt_scene* src, int device, rt_scene** out) {
     s->lane_stack = src->lane_stack;
     s->lane_wide = src->lane_wide;
     s->f_log2 = src->f_log2;
+    s->f_bound = src->f_bound;
     s->deep = src->deep;
     s->cus = src->cus;
     s->bytes = src->bytes;
@@ -3470,6 +3497,25 @@ extern "C" void rt_scene_destroy(rt_scene* s) {
     delete s;
 }
 extern "C" int rt_scene_device(const rt_scene* s) { return s ? s->device : -1; }
+
+extern "C" int rt_scene_traversal_info(const rt_scene* s, int64_t info[4]) {
+    if (!s || !info) return set_error(RT_ERR_ARG, "rt_scene_traversal_info: null argument");
+    const bool frustum = s->wide && !s->deep;
+    info[0] = frustum ? s->f_log2 : 0;
+    info[1] = frustum && s->f_log2 > 2 ? s->f_bound : 0;
+    info[2] = s->wide ? 1 : 0;
+    info[3] = s->deep ? 1 : 0;
+    return RT_OK;
+}
+
+extern "C" int rt_scene_faults(rt_scene* s, uint32_t* flags, int clear) {
+    if (!s || !flags) return set_error(RT_ERR_ARG, "rt_scene_faults: null argument");
+    DeviceGuard g(s->device);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(flags, s->fault.p, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (clear) HIP_TRY(hipMemset(s->fault.p, 0, sizeof(uint32_t)));
+    return RT_OK;
+}
 extern "C" size_t rt_scene_device_bytes(const rt_scene* s) { return s ? s->bytes : 0; }
 
 extern "C" void rt_render_opts_default(rt_render_opts* o) {
@@ -3680,8 +3726,9 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     std::memcpy(P.sc.root_box, s->root_box, sizeof(P.sc.root_box));
     P.sc.cut = static_cast<const float*>(s->cut.p);
     P.sc.tri = static_cast<const float4*>(s->tri.p);
-    double max_cov = 0.3;  // RT_CULL_COVERAGE: tests force the cut pass on (>= 1: always, untested candidates none)
-    if (const char* e = std::getenv("RT_CULL_COVERAGE")) max_cov = std::atof(e);
+    P.sc.fault = static_cast<uint32_t*>(s->fault.p);
+    // RT_TUNE_CULL_COVERAGE: tests force the cut pass on (>= 1: always, untested candidates none)
+    const double max_cov = rt::tuning(RT_TUNE_CULL_COVERAGE, 0.3);
     P.sc.ncut = s->ncut > 0 && root_box_coverage(s->root_box, cam) <= max_cov ? s->ncut : 0;
     P.cut_force = max_cov >= 1.0 ? 1 : 0;
     std::memcpy(P.sc.bmax, s->bmax, sizeof(P.sc.bmax));
@@ -3724,7 +3771,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // (With the frustum traversal, profiles/r04/exp/half_waves_ab_c3.log: N = 8 max kernel 0.0758
     // vs 0.0867 ms, N = 4 0.0831 vs 0.0857, N = 2 0.140 vs 0.097: half waves from 4 shards.)
     int half = o->band_count >= 4 || o->max_depth > 1 ? 1 : 0;
-    if (const char* e = std::getenv("RT_HALF_WAVES")) half = std::clamp(std::atoi(e), 0, 1);
+    if (const double h = rt::tuning(RT_TUNE_HALF_WAVES, -1.0); h >= 0.0) half = h >= 1.0 ? 1 : 0;
     if (!samples || o->spp > (64 >> half)) half = 0;
     P.half_waves = half;
     // One light and a tree whose DFS fits the per-lane LDS stacks: the bounce kernels that hold
@@ -3734,7 +3781,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
                             (P.sc.wide ? s->lane_wide : s->lane_stack)
                         ? 1
                         : 0;
-    if (const char* e = std::getenv("RT_PAIRED_ONLY")) P.paired_only = P.paired_only && std::atoi(e) != 0;
+    P.paired_only = P.paired_only && rt::tuning(RT_TUNE_PAIRED_ONLY, 1.0) != 0.0;
     int ppb = samples ? (BLOCK >> half) / o->spp : BLOCK;  // pixels per block
     int tw = 1;
     while (tw * tw < ppb) tw <<= 1;                // square-ish power-of-two tile
@@ -3761,12 +3808,11 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // (0: off).
     // c3 (frustum traversal, profiles/r04/exp/heavy_frac_ab_c3*.log): 0.05 0.153, 0.06 0.149,
     // 0.08 0.148, 0.10 0.147, 0.12 0.150, 0.18 0.151, 0.25 0.158 ms, off 0.187
-    double heavy_frac = 0.10;
-    if (const char* e = std::getenv("RT_HEAVY_FRAC")) heavy_frac = std::atof(e);
+    const double heavy_frac = rt::tuning(RT_TUNE_HEAVY_FRAC, 0.10);
     const int mode = o->kernel == RT_KERNEL_LANE ? RT_KERNEL_LANE : RT_KERNEL_WAVE;
     const bool costs = P.cull && P.sc.ncut > 0 && P.nqueues == 8 && heavy_frac > 0.0;
-    int heavy_cap = 512;  // RT_HEAVY_CAP: entries per (class, list) (speed experiments)
-    if (const char* e = std::getenv("RT_HEAVY_CAP")) heavy_cap = std::max(1, std::atoi(e));
+    // RT_TUNE_HEAVY_CAP: entries per (class, list) (speed experiments)
+    const int heavy_cap = int(std::clamp(rt::tuning(RT_TUNE_HEAVY_CAP, 512.0), 1.0, 1e9));
     P.heavy_cap = costs ? std::min(P.queue_cap, heavy_cap) : 0;
     // kSets counter sets (8 live lists, one spare, 8 heavy lists each) at fixed offsets, then
     // kSets x (live lists | cut survivor lists | heavy lists) sized for this geometry; rotating by frame
@@ -3895,10 +3941,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
-        static const size_t big_bytes = [] {
-            const char* e = std::getenv("RT_BIG_SCENE_BYTES");
-            return e ? (size_t)std::strtoull(e, nullptr, 10) : kBigSceneBytes;
-        }();
+        const size_t big_bytes = size_t(std::max(0.0, rt::tuning(RT_TUNE_BIG_SCENE_BYTES, double(kBigSceneBytes))));
         const Launch L{st, s->evm[slot], s->ev1[slot], s->cus, s->bytes > big_bytes, &s->last_kernel};
         if (s->deep) launch<MODE_DEEP>(P, samples, L);
         else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, L);
@@ -4064,6 +4107,10 @@ extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts
         HIP_TRY(hipMemcpy(hit_idx_host, hi.p, npx * size_t(o->spp) * sizeof(int32_t), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(hit_t_host, ht.p, npx * size_t(o->spp) * sizeof(float), hipMemcpyDeviceToHost));
     }
+    // a device-side guard fired (the frame's answers are poisoned where it did): loud, not silent
+    uint32_t fault = 0;
+    HIP_TRY(hipMemcpy(&fault, s->fault.p, sizeof(fault), hipMemcpyDeviceToHost));
+    if (fault & RT_FAULT_FRUSTUM_STACK) return set_error(RT_ERR_INTERNAL, "frustum traversal stack overflow");
     return RT_OK;
 }
 

@@ -4,6 +4,7 @@
 // them is byte-identical to the reference's arrays.  Citations use
 //   G/   = HW2/HW2/GPUandCPU     HW1/ = HW1     (relative to the reference repo)
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
@@ -33,12 +34,43 @@ int set_error(int code, const std::string& msg) {
 }
 void clear_error() { g_last_error.clear(); }
 
+namespace {
+// rt_tuning_set's table: per knob, the bits of the value set XOR a quiet NaN's, so that the
+// zero-initialised table reads NaN (= the default) everywhere
+std::atomic<uint64_t> g_tuning[RT_TUNE_COUNT];
+constexpr uint64_t kTuneNaN = 0x7ff8000000000000ull;
+}  // namespace
+
+double tuning(int id, double dflt) {
+    if (id < 0 || id >= RT_TUNE_COUNT) return dflt;
+    const uint64_t b = g_tuning[id].load(std::memory_order_relaxed) ^ kTuneNaN;
+    double v;
+    std::memcpy(&v, &b, sizeof v);
+    return v == v ? v : dflt;
+}
+
 }  // namespace rt
 
 using namespace rt;
 
 extern "C" const char* rt_last_error(void) { return rt::g_last_error.c_str(); }
 extern "C" int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+extern "C" int rt_tuning_set(int id, double value) {
+    if (id < 0 || id >= RT_TUNE_COUNT) return set_error(RT_ERR_ARG, "rt_tuning_set: unknown knob");
+    uint64_t b;
+    std::memcpy(&b, &value, sizeof b);
+    rt::g_tuning[id].store(value == value ? b ^ rt::kTuneNaN : 0);
+    return RT_OK;
+}
+extern "C" int rt_tuning_get(int id, double* value) {
+    if (id < 0 || id >= RT_TUNE_COUNT || !value) return set_error(RT_ERR_ARG, "rt_tuning_get: unknown knob");
+    *value = rt::tuning(id, NAN);
+    return RT_OK;
+}
+extern "C" void rt_tuning_reset(void) {
+    for (auto& v : rt::g_tuning) v.store(0);
+}
 
 // ---------------------------------------------------------------------------------------
 // Material defaults, camera, jitter

@@ -187,8 +187,7 @@ struct SharedFrames {
 };
 
 double peer_timeout_s() {
-    if (const char* e = std::getenv("RT_PEER_TIMEOUT_S")) return std::max(0.1, std::atof(e));
-    return 120.0;
+    return std::max(0.1, rt::tuning(RT_TUNE_PEER_TIMEOUT_S, 120.0));
 }
 
 // Spin (then yield, then sleep) until pred() holds; false on timeout.
@@ -652,9 +651,11 @@ extern "C" int rt_renderer_create(size_t P, const rt_bvh_node* nodes, const rt_a
     const bool named = o->host_frame_name && o->host_frame_name[0];
     int gather = o->gather;
     if (gather == RT_GATHER_AUTO) {
-        // one process over distinct GPUs delivering into rank 0's HBM: RCCL over xGMI rather
-        // than cross-device 2-D copies
-        if (world == n) gather = (o->deliver == RT_DELIVER_DEVICE && n > 1 && distinct) ? RT_GATHER_RCCL : RT_GATHER_DIRECT;
+        // every rank in this process: per-device copies (for RT_DELIVER_DEVICE, cross-device
+        // 2-D copies into rank 0's HBM).  The RCCL gather over distinct GPUs is taken only when
+        // asked for (RT_GATHER_RCCL): it has not yet run on a multi-GPU box, and an automatic
+        // choice must not turn a configuration that works into an RT_ERR_COMM at create.
+        if (world == n) gather = RT_GATHER_DIRECT;
         else gather = named ? RT_GATHER_HOST_SHARED : RT_GATHER_RCCL;
     }
     if ((o->flags & RT_RENDERER_SELF_SEND) && o->gather == RT_GATHER_AUTO) gather = RT_GATHER_RCCL;
@@ -715,12 +716,11 @@ extern "C" int rt_renderer_create(size_t P, const rt_bvh_node* nodes, const rt_a
             for (int i = 0; i < kTimeRing; ++i) HIP_TRY(hipEventCreate(&ring[i]));
     }
     if (r->uses_rccl() && (rc = init_comms(r.get(), o)) != RT_OK) return rc;
-    // several GPUs in this process: one submission thread per further rank (RT_RENDERER_SERIAL=1
-    // submits every rank from the calling thread, for A/B; RT_RENDERER_THREADS=1 uses the threads
-    // for repeated device ids too, for tests on one GPU)
-    const char* serial = std::getenv("RT_RENDERER_SERIAL");
-    const char* threads = std::getenv("RT_RENDERER_THREADS");
-    const bool use_pool = (distinct && !(serial && std::atoi(serial) != 0)) || (threads && std::atoi(threads) != 0);
+    // several GPUs in this process: one submission thread per further rank (RT_TUNE_RENDERER_THREADS
+    // 0 submits every rank from the calling thread, for A/B; 1 uses the threads for repeated
+    // device ids too, for tests on one GPU)
+    const double threads = rt::tuning(RT_TUNE_RENDERER_THREADS, -1.0);
+    const bool use_pool = threads < 0.0 ? distinct : threads != 0.0;
     if (n > 1 && use_pool) r->pool.start(n - 1);
     *out = r.release();
     return RT_OK;
@@ -794,7 +794,7 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
             const uint64_t need = t + 1 - uint64_t(r->depth);
             if (!spin_until([&] { return SharedFrames::load(r->shared->word(kOffReleased)) >= need; }))
                 return set_error(RT_ERR_COMM, "rank " + std::to_string(L.rank) + ": rank 0 did not release frame " +
-                                                  std::to_string(t - uint64_t(r->depth)) + " within RT_PEER_TIMEOUT_S");
+                                                  std::to_string(t - uint64_t(r->depth)) + " within the peer timeout (RT_TUNE_PEER_TIMEOUT_S)");
         }
         DeviceGuard g(L.device);
         if (own) {
@@ -931,7 +931,7 @@ extern "C" int rt_renderer_wait(rt_renderer* r, uint64_t ticket, const void** fr
                 const uint64_t* w = r->shared->done(q);
                 if (!spin_until([&] { return SharedFrames::load(w) >= ticket + 1; }))
                     return set_error(RT_ERR_COMM, "rank " + std::to_string(q) + " did not deliver frame " +
-                                                      std::to_string(ticket) + " within RT_PEER_TIMEOUT_S");
+                                                      std::to_string(ticket) + " within the peer timeout (RT_TUNE_PEER_TIMEOUT_S)");
             }
         }
     }

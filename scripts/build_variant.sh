@@ -17,8 +17,14 @@ fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall \
     -mcode-object-version=5 -Wno-unused-function "$@" -I"$ROOT/include" -I"$ROOT/raytracinginonesemester_amd/csrc" \
     -c -x hip "$SRC" -o "$OUT/rt_device.o"
+# the variant's own rt_build_id: "variant:<name>:" + sha256 of the device source and the extra
+# flags, so a variant library can never pass for the product build (whose id is the sources' hash)
+VID=$( (cat "$SRC"; printf '%s\0' "$@") | sha256sum | cut -c1-64)
+printf 'static const char tag[] __attribute__((used)) = "variant:%s:%s";\nconst char* rt_build_id(void) { return tag; }\n' \
+    "$NAME" "$VID" > "$OUT/rt_build_id.c"
+gcc -O2 -fPIC -c "$OUT/rt_build_id.c" -o "$OUT/rt_build_id.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$ROOT/build/obj/rt_host.o" "$OUT/rt_device.o" \
-    "$ROOT/build/obj/rt_frame.o" "$ROOT/build/obj/rt_lbvh.o" "$ROOT/build/obj/rt_renderer.o" "$ROOT/build/obj/rt_build_id.o" \
+    "$ROOT/build/obj/rt_frame.o" "$ROOT/build/obj/rt_lbvh.o" "$ROOT/build/obj/rt_renderer.o" "$OUT/rt_build_id.o" \
     -o "$OUT/librt_mi355x.so"
-rm -f "$OUT/rt_device.o"  # only the library travels to the GPU box
+rm -f "$OUT/rt_device.o" "$OUT/rt_build_id.o"  # only the library travels to the GPU box
 echo "$OUT/librt_mi355x.so"

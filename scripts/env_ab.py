@@ -1,7 +1,7 @@
-"""Interleaved in-process A/B of run-time settings the library reads per call (environment
-variables), one device scene, frames checked bit-identical across settings.
+"""Interleaved in-process A/B of run-time settings the library reads per call (tuning knobs,
+rt_tuning_set), one device scene, frames checked bit-identical across settings.
 
-    python scripts/env_ab.py [--config c3] [--rounds 5] [--reps 20] '{"name": {"VAR": "value"}, ...}' | @file.json
+    python scripts/env_ab.py [--config c3] [--rounds 5] [--reps 20] '{"name": {"knob": value}, ...}' | @file.json
 
 Per setting: median render-kernel ms, device-frame ms (HIP events) and wall ms per frame of a
 back-to-back loop on one stream.
@@ -41,14 +41,11 @@ rgb = torch.zeros((H * W * 3,), dtype=torch.float32, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 res = {k: {"kernel": [], "frame": [], "wall": [], "heavy": []} for k in settings}
 ref = None
-base_env = dict(os.environ)
 for _ in range(a.rounds):
-    for name, env in settings.items():
-        for k in set(v for e in settings.values() for v in e):
-            os.environ.pop(k, None)
-            if k in base_env:
-                os.environ[k] = base_env[k]
-        os.environ.update(env)
+    for name, knobs in settings.items():
+        rt.reset_tuning()
+        for k, v in knobs.items():
+            rt.set_tuning(k, v)
         ds.render_device(cam, opts, rgb.data_ptr(), stream=st)  # warm
         torch.cuda.synchronize()
         t0 = time.perf_counter()

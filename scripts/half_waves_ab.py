@@ -45,7 +45,7 @@ for n in [int(x) for x in a.counts.split(",")]:
     outs = {}
     for _ in range(a.rounds):
         for h in S:
-            os.environ["RT_HALF_WAVES"] = h
+            rt.set_tuning("half_waves", int(h))
             for r in range(n):
                 o, _j = ds.make_opts(spp=cfg["spp"], max_depth=cfg["max_depth"],
                                      miss_color=hs.settings["miss_color"], band_rows=8, band_index=r, band_count=n)
@@ -68,5 +68,5 @@ for n in [int(x) for x in a.counts.split(",")]:
                             "frame_max": round(max(f), 4), "frame_mean": round(sum(f) / n, 4)}
     line["identical"] = True
     print(json.dumps(line), flush=True)
-os.environ.pop("RT_HALF_WAVES", None)
+rt.set_tuning("half_waves", None)
 ds.close()

@@ -41,8 +41,8 @@ lib.rt_debug_wave_meta_set.argtypes = [C.c_void_p]
 ds = rt.DeviceScene.from_host(hs)
 band_kw = dict(band_rows=8, band_index=a.band, band_count=a.bands) if a.bands > 1 else {}
 opts, _j = ds.make_opts(spp=spp, max_depth=cfg["max_depth"], miss_color=hs.settings["miss_color"], **band_kw)
-half = os.environ.get("RT_HALF_WAVES") == "1" or (a.bands >= 8 and "RT_HALF_WAVES" not in os.environ) or \
-    (cfg["max_depth"] > 1 and "RT_HALF_WAVES" not in os.environ)
+hw = rt.get_tuning("half_waves")  # the library's rule (rt_render_device), or the knob when set
+half = hw == 1.0 if hw is not None else (a.bands >= 4 or cfg["max_depth"] > 1)
 if a.bands > 1:
     H = _lib.lib().rt_shard_rows(H, 8, a.band, a.bands)
 tw = (128 if half and spp <= 32 else 256) // spp if spp <= 256 else 1  # pixels per tile

@@ -27,10 +27,7 @@ cam = hs.camera(cfg["width"], cfg["height"])
 H, W = cam.pixel_height, cam.pixel_width
 p6 = torch.zeros((H * W * 3,), dtype=torch.uint8, device="cuda")
 for heavy in ("default", "0"):
-    if heavy == "0":
-        os.environ["RT_HEAVY_FRAC"] = "0"
-    else:
-        os.environ.pop("RT_HEAVY_FRAC", None)
+    rt.set_tuning("heavy_frac", 0 if heavy == "0" else None)
     ds = rt.DeviceScene.from_host(hs, device=0)
     for r in [None] + list(range(a.n)):
         kw = {} if r is None else {"band_rows": 8, "band_index": r, "band_count": a.n}

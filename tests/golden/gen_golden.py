@@ -37,6 +37,9 @@ G_FIXTURES = {
     "sphere_single": ("sphere_single.json", 160, 90, 4, 0, True),
     "cornell": ("cornell.json", 160, 120, 4, 0, True),
     "c5_small": ("heightfield_c5.json", 384, 216, 4, 1, True),
+    # BASELINE config 5 at its full size (3840x2160x64, depth 1): the reference's frame, hit
+    # and t buffers by sha256 (reference CPU render(), single-threaded: tens of CPU-minutes)
+    "c5_full": ("heightfield_c5.json", 3840, 2160, 64, 1, None),
     # c3b: frog.json's own max_bounces 8 (diffuse bounce), 16 spp (bench config c3b)
     "c3b_small": ("frog.json", 192, 108, 16, 0, True),
     "c3b_full": ("frog.json", 1920, 1080, 16, 0, False),

@@ -222,3 +222,36 @@ def test_random_trees(seed):
         check(P, nodes, aabbs, 5, cap)
         check(P, nodes, aabbs, 4, cap)
         check(P, nodes, aabbs, 3, cap)
+
+
+def first_leaf_depth(log2, rec):
+    """Stack depth of the records' DFS when it first reaches a leaf, every entry passing: the
+    depth a camera ray reaches when every box it meets before its first triangle test passes
+    (the spine scenes' centre rays)."""
+    A = 1 << log2
+    refs = rec.reshape(-1, 8 * A)[:, 6 * A:7 * A].view(np.uint32)
+    st, ref = [], 0
+    while not ref & LEAF_BIT:
+        es = [int(x) for x in refs[ref] if x != NO_REF]
+        st += es[:-1]
+        ref = es[-1]
+    return len(st)
+
+
+@pytest.mark.parametrize("L,want_log2", [(15, 5), (30, 4), (35, 3)])
+def test_spine_trees_fall_back_to_narrower_records(L, want_log2):
+    """tests/spine_bvh.py trees: the 32-ary records' DFS bound grows ~31 per five spine levels.
+    L = 15: 32-ary, bound in (64, 128] (the traversal's second stack VGPR); L = 30: the 32-ary
+    bound exceeds 128 and the builder falls back to 16-ary (bound in (64, 128]); L = 35: to
+    8-ary.  The records are the rule's, their leaf order SearchBVH's, and the centre rays of the
+    scene really reach more than 64 stack entries before their first leaf."""
+    import spine_bvh
+
+    a = spine_bvh.as_arrays(spine_bvh.spine_scene(L))
+    P, nodes, aabbs = a["P"], a["nodes"], a["aabbs"]
+    _, log2, bound = check(P, nodes, aabbs, 5, 128)
+    assert log2 == want_log2 and 64 < bound <= 128
+    if want_log2 < 5:  # the wider arities do not fit
+        assert build(P, nodes, aabbs, want_log2 + 1, 10**6)[1] > 128
+    lg, _, _, rec = build(P, nodes, aabbs, 5, 128)
+    assert first_leaf_depth(lg, rec) > 64

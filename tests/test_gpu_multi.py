@@ -48,12 +48,11 @@ def _line(stdout: str) -> dict:
 
 def _bench(args, nproc=None, timeout=420):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    env["RT_PEER_TIMEOUT_S"] = "60"
     if nproc:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(REPO / "bench.py"), *args]
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(REPO / "bench.py"), *args, "--tune", "peer_timeout_s=60"]
     else:
-        cmd = [sys.executable, str(REPO / "bench.py"), *args]
+        cmd = [sys.executable, str(REPO / "bench.py"), *args, "--tune", "peer_timeout_s=60"]
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=str(REPO), env=env)
 
 
@@ -120,7 +119,8 @@ def test_bench_failed_rccl_is_not_silent():
 def _shared_worker(rank, world, port, name, depth, q, others_wait=True):
     import torch.distributed as dist
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RT_PEER_TIMEOUT_S="60")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    rt.set_tuning("peer_timeout_s", 60)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         hs = host_scene("frog.json")
@@ -221,12 +221,11 @@ def test_pipelined_alternating_cameras(devices, depth):
 
 
 @pytest.mark.parametrize("threads", ["0", "1"])
-def test_in_process_submission_threads(threads, monkeypatch):
+def test_in_process_submission_threads(threads, tune):
     """Several ranks in one process, their per-rank host work on submission threads (the default
     over distinct GPUs, forced here for band shards sharing GPU 0) or on the calling thread:
     pipelined frames with alternating cameras are the single-frame images."""
-    monkeypatch.setenv("RT_RENDERER_THREADS", threads)
-    monkeypatch.setenv("RT_RENDERER_SERIAL", "1" if threads == "0" else "0")
+    tune(renderer_threads=int(threads))
     hs = host_scene("frog.json")
     ds = rt.DeviceScene.from_host(hs, device=0)
     cams = [hs.camera(W, H), _moved(hs.camera(W, H), 0.005, 0.001)]

@@ -116,10 +116,10 @@ def test_ray_counts_c3_full_frame():
 
 
 @pytest.mark.parametrize("name", ["c3_small", "frog_bounce", "cornell", "c5_small"])
-def test_half_waves_parity(name, monkeypatch):
+def test_half_waves_parity(name, tune):
     """Half waves (32 samples per wave, the default for 8-way band shards) forced on whole
     frames: the reference's outputs bit for bit, AOVs included."""
-    monkeypatch.setenv("RT_HALF_WAVES", "1")
+    tune(half_waves=1)
     meta = golden_meta(name)
     scene = G_SCENES[name]
     hs = host_scene(scene)
@@ -175,12 +175,12 @@ def test_bounce_paths_per_lane_traversal(name, flags):
 @pytest.mark.parametrize("name", ["c3b_small", "frog_bounce", "sphere_single"])
 @pytest.mark.parametrize("flags", [0, rt._lib.RT_FLAG_BINARY])
 @pytest.mark.parametrize("half", ["0", "1"])
-def test_one_light_bounce_loops_parity(name, flags, half, monkeypatch):
+def test_one_light_bounce_loops_parity(name, flags, half, tune):
     """One-light multi-bounce frames through both bounce loops: half waves (the default) pair a
     path's lane with a shadow lane (paired_bounces: a depth's Lo add waits for its shadow ray's
-    answer, traced beside the next bounce ray); RT_HALF_WAVES=0 forces full waves and the
+    answer, traced beside the next bounce ray); half_waves=0 forces full waves and the
     unpaired loop.  The reference's outputs bit for bit, AOVs included."""
-    monkeypatch.setenv("RT_HALF_WAVES", half)
+    tune(half_waves=int(half))
     meta = golden_meta(name)
     assert meta["max_depth"] > 1 and meta["num_lights"] == 1
     scene = G_SCENES[name]
@@ -249,14 +249,13 @@ def test_shipped_scene_full_frames(name, scene):
     assert hashlib.sha256(ht.tobytes()).hexdigest() == meta["sha256"]["hitt.f32"]
 
 
-@pytest.mark.parametrize("env", [{}, {"RT_HEAVY_CAP": "8"}, {"RT_HEAVY_FRAC": "0.0001"}])
-def test_heavy_first_dispatch_changes_nothing(env, monkeypatch):
+@pytest.mark.parametrize("env", [{}, {"heavy_cap": 8}, {"heavy_frac": 0.0001}])
+def test_heavy_first_dispatch_changes_nothing(env, tune):
     """Heavy-first dispatch (the previous frames' per-tile costs order the render blocks; full
     heavy lists spill into the survivor lists; a tiny threshold makes every tile heavy): frames
     after the first take the heavy path and still equal the reference's c3 frame, also after
     the camera moved (stale costs) and back."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    tune(**env)
     meta = golden_meta("c3_full")
     hs = host_scene("frog.json")
     cam = hs.camera(1920, 1080)
@@ -272,8 +271,8 @@ def test_heavy_first_dispatch_changes_nothing(env, monkeypatch):
             assert hashlib.sha256(ht.tobytes()).hexdigest() == meta["sha256"]["hitt.f32"]
             _check_fb(rgb, golden_array("c3_full", "fb.f32.gz", np.float32))
     assert heavy[0] == 0 and heavy[1] > 0 and heavy[4] > 0, heavy
-    if "RT_HEAVY_CAP" in env:
-        assert heavy[4] <= 8 * 3 * int(env["RT_HEAVY_CAP"])
+    if "heavy_cap" in env:
+        assert heavy[4] <= 8 * 3 * int(env["heavy_cap"])
     ds.close()
 
 
@@ -530,12 +529,12 @@ def test_full_size_properties_c5():
 
 @pytest.mark.parametrize("force_cut", [False, True])
 @pytest.mark.parametrize("scene", ["frog.json", "cornell.json", "sphere_single.json"])
-def test_tile_culling_changes_nothing(scene, force_cut, monkeypatch):
+def test_tile_culling_changes_nothing(scene, force_cut, tune):
     """Tile culling against the root box (and, forced on for every camera, against the 64-box
     cut of the tree) is exact: random cameras (near, far, inside the box, grazing, far from
     the origin) give bit-identical frames and hit AOVs with it on and off."""
     if force_cut:
-        monkeypatch.setenv("RT_CULL_COVERAGE", "1.0")
+        tune(cull_coverage=1.0)
     hs = host_scene(scene)
     ds = _device_scene(scene)
     box = np.concatenate([hs.aabbs[0, :3], hs.aabbs[0, 3:]])
@@ -570,11 +569,11 @@ def test_720p_frame_rows_against_oracle(spp):
 
 
 @pytest.mark.parametrize("scene", ["frog.json", "cornell.json", "sphere_single.json"])
-def test_cut_culling_fuzz_grazing_cameras(scene, monkeypatch):
+def test_cut_culling_fuzz_grazing_cameras(scene, tune):
     """The float tile bounds of both culling passes (root box and 64-box cut) against many
     cameras aimed at box faces, edges and corners from near and far, with tiny and wide fields
     of view: culled frames are bit-identical to unculled ones."""
-    monkeypatch.setenv("RT_CULL_COVERAGE", "1.0")
+    tune(cull_coverage=1.0)
     hs = host_scene(scene)
     ds = _device_scene(scene)
     box = np.concatenate([hs.aabbs[0, :3], hs.aabbs[0, 3:]]).astype(np.float64)
@@ -608,49 +607,50 @@ def test_hw1_timing_entry_point():
     assert np.array_equal(rgb.view(np.uint32), rgb_b.view(np.uint32))
 
 
-@pytest.mark.parametrize("arity", ["2", "3", "4"])
+# RT_TUNE_FRUSTUM_ARITY caps the arity rt_scene_create picks (log2: 2 = the 4-ary records,
+# 5 = 32-ary); None = the shipped default (32-ary where the stack bound fits: frog 91, c5 126)
+ARITIES = [None, 5, 4, 3, 2]
+
+
+@pytest.mark.parametrize("arity", ARITIES)
 @pytest.mark.parametrize("name", ["c3_small", "frog_bounce", "sphere_single", "cornell", "c5_small", "c3b_small"])
-def test_frustum_record_arity_parity(name, arity, monkeypatch):
-    """The camera rays' frustum traversal over 4-, 8- and 16-ary records (RT_FRUSTUM_ARITY caps
-    the arity rt_scene_create picks): the reference's hits, t and frame bit for bit."""
-    monkeypatch.setenv("RT_FRUSTUM_ARITY", arity)
+def test_frustum_record_arity_parity(name, arity, tune):
+    """The camera rays' frustum traversal over 4-, 8-, 16- and 32-ary records and the default:
+    the reference's hits, t and frame bit for bit."""
+    tune(frustum_arity=arity)
     meta = golden_meta(name)
     hs = host_scene(G_SCENES[name])
     cam = hs.camera(meta["width"], meta["height"])
     ds = rt.DeviceScene.from_host(hs, device=0)
+    info = ds.traversal_info()
+    if arity is None and name in ("c3_small", "c3b_small", "frog_bounce", "c5_small"):
+        assert info["frustum_log2"] == 5 and 64 < info["frustum_bound"] <= 128, info
     rgb, hi, ht = ds.render(cam, spp=meta["spp"], max_depth=meta["max_depth"],
                             diffuse_bounce=bool(meta["diffuse_bounce"]), miss_color=hexv(meta["miss_color"]),
                             aov=True)
+    assert ds.faults() == 0
     assert np.array_equal(hi.reshape(-1), golden_array(name, "hits.i32.gz", np.int32))
     assert np.array_equal(ht.reshape(-1).view(np.uint32),
                           golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
     _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
 
 
-@pytest.mark.parametrize("arity", ["3", "4"])
-@pytest.mark.parametrize("scene", ["frog.json", "cornell.json", "sphere_single.json"])
-def test_frustum_fuzz_cameras(scene, arity, monkeypatch):
-    """The frustum traversal's wave-level box test must pass whenever some lane's exact test
-    does: cameras aimed at box faces, edges and corners, along the axes (direction components
+def _fuzz_cameras(hs, rng, n, W=96, H=64):
+    """Cameras aimed at box faces, edges and corners, along the axes (direction components
     crossing zero inside a wave), from inside the scene's boxes, with tiny and wide fields of
-    view.  Frames (hits, t, colour) bit-identical to the binary-record traversal, which tests
-    every box for every lane."""
-    monkeypatch.setenv("RT_FRUSTUM_ARITY", arity)
-    hs = host_scene(scene)
-    ds = rt.DeviceScene.from_host(hs, device=0)
+    view."""
     lo, hi = hs.aabbs[0, :3].astype(np.float64), hs.aabbs[0, 3:].astype(np.float64)
     ext = float(np.linalg.norm(hi - lo))
-    rng = np.random.default_rng(7)
     axes = [np.array(v, np.float64) for v in ((1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1))]
-    for k in range(36):
+    for k in range(n):
         if k % 3 == 0:  # along an axis: the centre column / row has a zero direction component
             dirn = axes[k // 3 % 6]
         else:
             dirn = rng.normal(size=3)
             dirn /= np.linalg.norm(dirn)
         if k % 4 == 1:  # from inside the tree: a random internal box's centre
-            n = int(rng.integers(0, len(hs.aabbs)))
-            pos = (hs.aabbs[n, :3] + hs.aabbs[n, 3:]).astype(np.float64) / 2
+            m = int(rng.integers(0, len(hs.aabbs)))
+            pos = (hs.aabbs[m, :3] + hs.aabbs[m, 3:]).astype(np.float64) / 2
             target = pos - dirn * ext
         else:
             t = rng.choice([0.0, 1.0, 0.5, rng.uniform()], size=3)
@@ -658,8 +658,99 @@ def test_frustum_fuzz_cameras(scene, arity, monkeypatch):
             pos = target + dirn * ext * rng.choice([0.05, 0.6, 3.0])
         fwd = target - pos
         up = (0.0, 0.0, 1.0) if abs(fwd[2]) < 0.9 * np.linalg.norm(fwd) else (0.0, 1.0, 0.0)
-        cam = rt.Camera(tuple(pos), tuple(target), up, float(rng.choice([8.0, 35.0, 600.0])), 24.0, 96, 64)
+        yield k, rt.Camera(tuple(pos), tuple(target), up, float(rng.choice([8.0, 35.0, 600.0])), 24.0, W, H)
+
+
+@pytest.mark.parametrize("arity", [None, 5, 4, 3])
+@pytest.mark.parametrize("scene", ["frog.json", "cornell.json", "sphere_single.json"])
+def test_frustum_fuzz_cameras(scene, arity, tune):
+    """The frustum traversal's wave-level box test must pass whenever some lane's exact test
+    does (adversarial cameras, _fuzz_cameras): frames (hits, t, colour) bit-identical to the
+    binary-record traversal, which tests every box for every lane.  At the shipped arity (None,
+    5: 32-ary records, frog's bound 91) the DFS uses the stack's second VGPR."""
+    tune(frustum_arity=arity)
+    hs = host_scene(scene)
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    for k, cam in _fuzz_cameras(hs, np.random.default_rng(7), 36):
         a = ds.render(cam, spp=4, max_depth=1, aov=True)
         b = ds.render(cam, spp=4, max_depth=1, aov=True, flags=rt._lib.RT_FLAG_BINARY)
         for x, y in zip(a, b):
             assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), k
+    assert ds.faults() == 0
+
+
+def test_frustum_fuzz_cameras_c5():
+    """The c5 heightfield (1M triangles) at its shipped 32-ary records, whose DFS bound (126)
+    sits next to the 128-entry stack: grazing, axis-aligned, inside-the-tree and far cameras at
+    reduced resolution against the binary-record traversal, bit for bit."""
+    hs = host_scene("heightfield_c5.json")
+    ds = _device_scene("heightfield_c5.json")
+    info = ds.traversal_info()
+    assert info["frustum_log2"] == 5 and 120 < info["frustum_bound"] <= 128, info
+    rng = np.random.default_rng(55)
+    cams = list(_fuzz_cameras(hs, rng, 12, 64, 48))
+    # grazing: just above the surface, looking along it
+    for k, (x, y) in enumerate(((-1.9, -0.9), (1.9, 0.9), (0.0, -0.95), (-1.95, 0.0))):
+        cams.append((100 + k, rt.Camera((x, y, 0.12), (-x, -y, 0.05), (0.0, 0.0, 1.0), 20.0, 24.0, 64, 48)))
+    for k, cam in cams:
+        a = ds.render(cam, spp=4, max_depth=1, aov=True, miss_color=(0.5, 0.7, 1.0))
+        b = ds.render(cam, spp=4, max_depth=1, aov=True, miss_color=(0.5, 0.7, 1.0), flags=rt._lib.RT_FLAG_BINARY)
+        for x, y in zip(a, b):
+            assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), k
+    assert ds.faults() == 0
+
+
+def _spine(L):
+    import spine_bvh
+
+    a = spine_bvh.as_arrays(spine_bvh.spine_scene(L))
+    ds = rt.DeviceScene(a["P"], a["nodes"], a["aabbs"], a["tris"], a["objids"], a["mats"], a["lights"])
+    pos, look, up, f, s = spine_bvh.CAMERA
+    return a, ds, rt.Camera(pos, look, up, f, s, 48, 32)
+
+
+@pytest.mark.parametrize("L,log2", [(15, 5), (30, 4), (35, 3)])
+def test_spine_trees_deep_frustum_stack(L, log2):
+    """Trees whose frustum DFS goes past 64 stack entries (tests/spine_bvh.py): 32-ary records
+    with bound 109, and trees whose 32-ary bound exceeds the 128-entry stack, which take 16-ary
+    (bound 124) or 8-ary records instead.  The centre rays reach more than 64 entries before
+    their first leaf (tests/test_frustum_records.py).  Frames bit-identical to the binary-record
+    traversal and to the oracle; no device fault."""
+    a, ds, cam = _spine(L)
+    try:
+        info = ds.traversal_info()
+        assert info["frustum_log2"] == log2 and 64 < info["frustum_bound"] <= 128, info
+        got = ds.render(cam, spp=4, max_depth=1, aov=True)
+        ref_b = ds.render(cam, spp=4, max_depth=1, aov=True, flags=rt._lib.RT_FLAG_BINARY)
+        assert ds.faults() == 0
+    finally:
+        ds.close()
+    for x, y in zip(got, ref_b):
+        assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32))
+    rgb, hi, ht = orc.render_g(a["P"], oracle_camera(cam), a["nodes"], a["aabbs"], a["tris"], a["objids"], a["mats"],
+                               a["lights"], spp=4, max_depth=1, aov=True)
+    assert np.array_equal(got[1], hi) and np.array_equal(got[2].view(np.uint32), ht.view(np.uint32))
+    assert (hi >= 0).mean() > 0.5
+    _check_fb(got[0], rgb)
+
+
+def test_frustum_stack_overflow_guard_is_loud(tune):
+    """The device guard on traverse_frustum's 128-entry stack: records built past it (the test
+    hook RT_TUNE_FRUSTUM_STACK_CAP; rt_scene_create never does so by default) overflow on the
+    spine tree's centre rays; the traversal drops the pushes instead of wrapping a lane index,
+    raises RT_FAULT_FRUSTUM_STACK, and rt_render fails with RT_ERR_INTERNAL instead of
+    returning a wrong frame."""
+    tune(frustum_stack_cap=10**6)
+    a, ds, cam = _spine(30)
+    try:
+        info = ds.traversal_info()
+        assert info["frustum_log2"] == 5 and info["frustum_bound"] > 128, info
+        with pytest.raises(rt.RTError) as e:
+            ds.render(cam, spp=4, max_depth=1)
+        assert e.value.code == -9 and "overflow" in str(e.value)
+        assert ds.faults() & rt._lib.RT_FAULT_FRUSTUM_STACK
+        assert ds.faults() == 0  # cleared by the previous call
+        # the binary-record traversal does not use the frustum stack: a valid frame
+        ds.render(cam, spp=4, max_depth=1, flags=rt._lib.RT_FLAG_BINARY)
+    finally:
+        ds.close()

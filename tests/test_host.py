@@ -215,3 +215,33 @@ def test_loaded_library_is_built_from_these_sources():
 
     lib = _lib.lib()
     assert lib.rt_build_id().decode() == b.source_build_id() == b.library_build_id()
+
+
+def test_tuning_knobs_are_explicit():
+    """The library reads no environment variables: knobs are set through rt_tuning_set (the
+    header's rt_tune_id), read back, reset, and an unknown id is refused."""
+    import raytracinginonesemester_amd as rt
+    from raytracinginonesemester_amd import _lib
+
+    so = (_lib.LIB_PATH).read_bytes()
+    # (rocPRIM's headers, used by the device LBVH's sort, read their own variables)
+    for src in (REPO / "raytracinginonesemester_amd" / "csrc").iterdir():
+        assert "getenv" not in src.read_text(), src
+    for name in (b"RT_FRUSTUM_ARITY", b"RT_HALF_WAVES", b"RT_HEAVY_FRAC", b"RT_CULL_COVERAGE", b"RT_RENDERER_SERIAL"):
+        assert name not in so, name
+    rt.reset_tuning()
+    try:
+        assert all(rt.get_tuning(k) is None for k in _lib.TUNE)
+        rt.set_tuning("heavy_frac", 0.25)
+        rt.set_tuning("half_waves", 1)
+        assert rt.get_tuning("heavy_frac") == 0.25 and rt.get_tuning("half_waves") == 1.0
+        with rt.tuning(heavy_frac=0.5, frustum_arity=3):
+            assert rt.get_tuning("heavy_frac") == 0.5 and rt.get_tuning("frustum_arity") == 3.0
+        assert rt.get_tuning("heavy_frac") == 0.25 and rt.get_tuning("frustum_arity") is None
+        rt.set_tuning("heavy_frac", None)
+        assert rt.get_tuning("heavy_frac") is None
+        assert _lib.lib().rt_tuning_set(len(_lib.TUNE), 1.0) == -1
+        assert _lib.lib().rt_tuning_set(-1, 1.0) == -1
+    finally:
+        rt.reset_tuning()
+    assert all(rt.get_tuning(k) is None for k in _lib.TUNE)

@@ -67,7 +67,8 @@ def parse():
     ap.add_argument("--preroll-ms", type=float, default=100.0,
                     help="untimed frames for about this much GPU time before the W warmup frames (clocks; "
                          "0: none); the frames run are reported as warmup_frames_run")
-    ap.add_argument("--config", default="c3", choices=sorted(configs.G_CONFIGS))
+    ap.add_argument("--config", default="c3", choices=sorted(configs.G_CONFIGS) + sorted(configs.HW1_CONFIGS),
+                    help="c1 / c2: the HW1 path (HW1/src/render.cpp:72-116) on one GPU (hw1_main)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "wave", "lane"])
     ap.add_argument("--deliver", default="p6", choices=["p6", "f32"])
     ap.add_argument("--gather", default="auto", choices=["auto", "rccl", "direct", "shm"],
@@ -600,11 +601,143 @@ def lbvh_times(hs, device: int, reps: int = 5) -> dict:
                     "its stream sync), outside the timed region; the reference prints both (G/src/main.cu:293,317)"}
 
 
+# ---- HW1 configurations (C1 / C2: HW1/src/render.cpp:72-116 on the device) --------------
+HW1_GOLDEN = {"c1": "c1_full", "c2": "c2_full"}
+
+
+def hw1_cpu_baseline(mesh, c, W, H) -> dict:
+    """The HW1 brute-force loop on the host: the oracle restatement (bit-exact to the reference's
+    HW1 build, tests/test_oracle.py) on every usable core over a bounded band of rows, repeated to
+    ~10 s, and the reference's own HW1 loop built from its sources (oracle/_ref/ref_hw1, 1 thread)
+    on a reduced-resolution sample of the same camera."""
+    from oracle import pyoracle as orc
+
+    cores = usable_cores()
+    threads = cores["usable"]
+    hcam = orc.camera(c["position"], c["look_at"], c["up"], c["focal_mm"], c["sensor_mm"], W, H, hw1=True)
+    # the band of rows through the middle of the image, where the mesh is
+    rows = (0, H) if mesh.num_triangles < 5000 else (H // 2 - 24, H // 2 + 24)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        orc.render_hw1(mesh.positions, mesh.normals, mesh.indices, hcam, c["light_pos"], c["light_color"],
+                       spp=c["spp"], threads=threads, rows=rows)
+        reps += 1
+        if time.perf_counter() - t0 >= 10.0:
+            break
+    dt = time.perf_counter() - t0
+    n = (rows[1] - rows[0]) * W * c["spp"] * reps
+    out = {"value": n / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/rt_oracle.c HW1 brute force (bit-exact restatement of HW1/src/render.cpp:72-116) "
+                     f"rows {rows[0]}..{rows[1]} of {W}x{H}x{c['spp']}, {reps} pass(es), {n} rays, {dt:.2f} s, "
+                     f"OpenMP {threads} threads", "host": cores}
+    ref = REPO / "oracle" / "_ref" / "ref_hw1"
+    if ref.exists():
+        w, h = (W // 8, H // 8) if mesh.num_triangles >= 5000 else (W, H)
+        with tempfile.TemporaryDirectory() as td:
+            args = [str(ref), "render", str(configs.MESHES / c["mesh"]), td, str(w), str(h),
+                    *map(str, c["position"]), *map(str, c["look_at"]), *map(str, c["up"]), str(c["focal_mm"]),
+                    str(c["sensor_mm"]), *map(str, c["light_pos"]), *map(str, c["light_color"]), str(c["spp"])]
+            t1 = time.perf_counter()
+            r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+            d1 = time.perf_counter() - t1
+            if r.returncode == 0:
+                out["reference_as_shipped"] = {
+                    "value": w * h * c["spp"] / d1 / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "reference",
+                    "sample": f"HW1 brute-force loop built from /root/reference sources (oracle/_ref/ref_hw1), "
+                              f"{w}x{h}x{c['spp']} of the same camera, {d1:.2f} s wall incl. OBJ load"}
+    return out
+
+
+def hw1_main(a):
+    """C1 / C2 on one GPU: a step = one W x H x spp frame of the HW1 path (binning passes +
+    render kernel, rt_hw1_scene resident in HBM) whose P6 body (write_p6 defaults, fused into the
+    render kernel) has reached pinned host memory; frames in stream order on one stream."""
+    if a.gpus != 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("bench: the HW1 configurations run on one GPU (replicas only)")
+    c = configs.HW1_CONFIGS[a.config]
+    W, H, spp = c["width"], c["height"], c["spp"]
+    mesh = rt.MeshHW1(configs.MESHES / c["mesh"])
+    cam = rt.Camera(c["position"], c["look_at"], c["up"], c["focal_mm"], c["sensor_mm"], W, H, hw1=True)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    sc = rt.HW1Scene(mesh.positions, mesh.normals, mesh.indices, device=0)
+    st = torch.cuda.Stream(dev)
+    p6 = [torch.empty(W * H * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
+    host = [torch.empty(W * H * 3, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+
+    def frames(n, k0=0):
+        with torch.cuda.stream(st):
+            for k in range(k0, k0 + n):
+                sc.render_device(cam, c["light_pos"], c["light_color"], spp, p6_ptr=p6[k % 2].data_ptr(),
+                                 stream=st.cuda_stream)
+                host[k % 2].copy_(p6[k % 2], non_blocking=True)
+
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < a.preroll_ms * 1e-3:  # clocks up (timed_native)
+        frames(16)
+        st.synchronize()
+    frames(a.warmup)
+    st.synchronize()
+    t0 = time.perf_counter()
+    frames(a.steps)
+    st.synchronize()
+    elapsed = time.perf_counter() - t0
+    kms = sc.kernel_times(min(a.steps, 64))
+    kernel_ms = float(np.median(kms))
+    rays = W * H * spp
+    value = rays * a.steps / elapsed / 1e6
+    line = {"metric": f"Mrays/s ({a.config}: HW1 path, primary rays)", "value": round(value, 3), "unit": "Mrays/s",
+            "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": f"synthetic=false: HW1/assets/meshes/{c['mesh']} as the reference ships it",
+            "config": {"workload": f"{a.config}: HW1 {c['mesh']} {W}x{H}x{spp}spp, primary rays, HW1 shade "
+                                   "(HW1/include/raytracer.h:21-48), brute-force winner (first index on ties)",
+                       "triangles": mesh.num_triangles,
+                       "step_delivers": "the frame's P6 samples in host memory (pinned), frames in stream order",
+                       "kernels": "hw1_rect_count_kernel + hw1_scan_kernel + hw1_fill_kernel + "
+                                  "render_hw1_binned_kernel (rt_render_hw1_device)"}}
+    if a.tune:
+        line["config"]["tuning"] = dict(kv.partition("=")[::2] for kv in a.tune)
+    instance = sc.kernel_name()
+    tr = load_traffic(Path(a.traffic_file), a.config, instance)
+    roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": instance,
+            "kernel_ms": round(kernel_ms, 4), "note": "kernel_ms: the frame's four launches, HIP events around them"}
+    if tr and tr.get("bytes_per_launch"):
+        ach = tr["bytes_per_launch"] / (tr.get("kernel_ms", kernel_ms) / 1e3) / 1e9
+        roof.update(traffic=tr["bytes_per_launch"], achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
+                    achieved_from=f"measured HBM bytes per frame (rocprofv3 --pmc, {tr.get('source', '?')}) / "
+                                  "the profiled frame's kernel time")
+        for k in ("issue", "binding", "per_kernel"):
+            if tr.get(k):
+                roof[k] = tr[k]
+    else:
+        roof.update(traffic=None, achieved=None, frac=None,
+                    achieved_from=f"no PMC traffic profiled for {instance} on {a.config} (profiles/traffic.json)")
+    line["roofline"] = roof
+    line["timing"] = {"kernel_ms": round(kernel_ms, 4), "kernel_ms_min": round(float(kms.min()), 4)}
+    if not a.no_parity:
+        gdir = REPO / "tests" / "golden" / "scenes" / HW1_GOLDEN[a.config]
+        want = gzip.open(gdir / "image.ppm.gz").read()
+        body = host[(a.warmup + a.steps - 1) % 2].numpy().tobytes()
+        got = rt.p6_header(W, H) + body
+        wb = np.frombuffer(want[len(rt.p6_header(W, H)):], np.uint8).astype(int)
+        line["parity"] = {"vs": f"reference HW1 output written by ppm_p6 (tests/golden/scenes/{HW1_GOLDEN[a.config]})",
+                          "timed_step_ppm_identical": got == want,
+                          "timed_step_ppm_maxabs": int(np.abs(np.frombuffer(body, np.uint8).astype(int) - wb).max())}
+    if not a.no_cpu_baseline:
+        line["cpu_baseline"] = hw1_cpu_baseline(mesh, c, W, H)
+        line["speedup_vs_cpu_baseline"] = round(value / line["cpu_baseline"]["value"], 2)
+    sc.close()
+    print(json.dumps(line), flush=True)
+
+
 def main():
     a = parse()
     for kv in a.tune:
         k, _, v = kv.partition("=")
         rt.set_tuning(k, float(v))
+    if a.config in configs.HW1_CONFIGS:
+        return hw1_main(a)
     ctx = Ctx(a)
     world, rank = ctx.world, ctx.rank
     cfg = configs.G_CONFIGS[a.config]

@@ -388,6 +388,27 @@ int rt_render_hw1_ex(int device, const rt_vec3* positions, const rt_vec3* normal
                      int flags, float* rgb_host, int32_t* hit_idx_host, float* hit_t_host,
                      float* kernel_ms);
 
+/* Resident HW1 mesh for repeated frames (the C2 configuration on the device): the mesh packed
+ * and uploaded once, the binning buffers kept.  rt_render_hw1_device renders one frame on
+ * hip_stream (NULL = the default stream) without synchronising: rgb_dev (W*H*3 floats) and/or
+ * p6_dev (W*H*3 bytes, write_p6 defaults) and the optional AOVs (W*H*spp each) are device
+ * pointers; jitter NULL = jittered_samples(spp, 42) in [0,1).  rt_hw1_kernel_times: ms of the
+ * frame's kernels (events around them) for the latest min(max, frames, 64) frames, oldest first;
+ * rt_hw1_kernel_name: the render kernel the latest frame launched, as rocprofv3 names it. */
+typedef struct rt_hw1_scene rt_hw1_scene;
+int rt_hw1_scene_create(int device, const rt_vec3* positions, const rt_vec3* normals, const uint32_t* indices,
+                        size_t num_triangles, rt_hw1_scene** out);
+void rt_hw1_scene_destroy(rt_hw1_scene* s);
+int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_vec3 light_position, rt_vec3 light_color,
+                         int spp, const float* jitter, int flags, float* rgb_dev, uint8_t* p6_dev,
+                         int32_t* hit_idx_dev, float* hit_t_dev, void* hip_stream);
+int rt_hw1_kernel_times(const rt_hw1_scene* s, float* ms_out, int max, int* n_out);
+const char* rt_hw1_kernel_name(const rt_hw1_scene* s);
+/* info = {entries the bin list holds now, the latest frame's list total (waits for it)}: a
+ * total above the capacity its frame ran with means that frame's overflowing tiles took the
+ * brute-force loop; the next frame runs with a grown list. */
+int rt_hw1_list_info(const rt_hw1_scene* s, int64_t info[2]);
+
 /* Batched ray-triangle queries on the GPU (one triangle, n rays from `origin`), the device
  * Möller–Trumbore used by the kernels:  hw1 != 0 -> HW1 ray_intersection
  * (HW1/include/ray.h:67-117; the HW1 Ray constructor normalises each direction first, ray.h:25),

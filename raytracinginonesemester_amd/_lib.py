@@ -166,6 +166,12 @@ SIGNATURES = {
     "rt_renderer_times": (I, [P, I, P, I, P]),
     "rt_render_hw1": (I, [I, P, P, P, SZ, P, Vec3, Vec3, I, P, P, P, P]),
     "rt_render_hw1_ex": (I, [I, P, P, P, SZ, P, Vec3, Vec3, I, P, I, P, P, P, P]),
+    "rt_hw1_scene_create": (I, [I, P, P, P, SZ, P]),
+    "rt_hw1_scene_destroy": (None, [P]),
+    "rt_render_hw1_device": (I, [P, P, Vec3, Vec3, I, P, I, P, P, P, P, P]),
+    "rt_hw1_kernel_times": (I, [P, P, I, P]),
+    "rt_hw1_kernel_name": (C.c_char_p, [P]),
+    "rt_hw1_list_info": (I, [P, P]),
     "rt_intersect_rays": (I, [I, P, P, P, I, I, C.c_float, C.c_float, P, P]),
     "rt_powf_host": (C.c_float, [C.c_float, C.c_float]),
     "rt_debug_frustum_records": (C.c_int, [C.c_size_t, P, P, C.c_int, C.c_int, P, P, C.c_size_t]),

@@ -516,6 +516,52 @@ def render_hw1(positions, normals, indices, camera: Camera, light_position, ligh
     return out if len(out) > 1 else out[0]
 
 
+class HW1Scene:
+    """A HW1 mesh resident on one MI355X (rt_hw1_scene): repeated frames of the HW1 path
+    (HW1/src/render.cpp:72-116) without re-uploading it."""
+
+    def __init__(self, positions, normals, indices, device: int = 0):
+        pos, nrm, idx = _c(positions, np.float32), _c(normals, np.float32), _c(indices, np.uint32)
+        h = C.c_void_p()
+        check(lib().rt_hw1_scene_create(int(device), ptr(pos), ptr(nrm), ptr(idx), idx.size // 3, C.byref(h)))
+        self._h = h
+        self.device = device
+
+    def render_device(self, camera: Camera, light_position, light_color, spp: int = 1, rgb_ptr=None, p6_ptr=None,
+                      hit_idx_ptr=None, hit_t_ptr=None, stream=None, jitter=None, brute: bool = False) -> None:
+        """One frame into device buffers (raw pointers) on a HIP stream (handle), asynchronously."""
+        jit = None if jitter is None else _c(jitter, np.float32).reshape(-1)
+        check(lib().rt_render_hw1_device(self._h, C.byref(camera.c), _v3(light_position), _v3(light_color), int(spp),
+                                         ptr(jit), RT_HW1_BRUTE if brute else 0, rgb_ptr, p6_ptr, hit_idx_ptr,
+                                         hit_t_ptr, stream))
+
+    def kernel_times(self, max_frames: int = 64) -> np.ndarray:
+        out = np.zeros(max_frames, np.float32)
+        n = C.c_int()
+        check(lib().rt_hw1_kernel_times(self._h, ptr(out), max_frames, C.byref(n)))
+        return out[:n.value]
+
+    def kernel_name(self) -> str:
+        return lib().rt_hw1_kernel_name(self._h).decode()
+
+    def list_info(self) -> tuple:
+        """(bin-list capacity now, the latest frame's list total)."""
+        info = (C.c_int64 * 2)()
+        check(lib().rt_hw1_list_info(self._h, info))
+        return int(info[0]), int(info[1])
+
+    def close(self) -> None:
+        if self._h:
+            lib().rt_hw1_scene_destroy(self._h)
+        self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def intersect_rays(triangle18, dirs, origin=(0.0, 0.0, 0.0), hw1: bool = True, tmin: float = 0.0,
                    tmax: float = 3.4028234663852886e38, device: int = 0):
     """Device Möller–Trumbore over a batch of rays against one triangle (v0,v1,v2,n0,n1,n2 as 18

@@ -737,7 +737,7 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
         ref = sp < 64 ? rdlane(st_ref, sp) : rdlane(st_hi, sp - 64);
     }
     if (ovf) {
-        if (lane_id() == 0) atomicOr(sc.fault, RT_FAULT_FRUSTUM_STACK);
+        if (fresh_lane_id() == 0) atomicOr(sc.fault, RT_FAULT_FRUSTUM_STACK);
         hs.bestT = __int_as_float(0x7fc00000);
         hs.slot = -1;
     }
@@ -2531,9 +2531,12 @@ struct Hw1Params {
     int32_t W, H, spp;
     f3 lpos, lcol;
     const float* __restrict__ jitter;
-    float* __restrict__ rgb;
+    float* __restrict__ rgb;          // optional (W*H*3 floats)
     int32_t* __restrict__ hit_idx;
     float* __restrict__ hit_t;
+    uint8_t* __restrict__ p6;         // optional: write_p6-default samples (W*H*3 bytes)
+    uint32_t list_cap;                // binned path: entries bin_list holds; a tile whose list would
+                                      // reach past it takes the brute-force loop (exact, slower)
 };
 
 // HW1 shade (HW1/include/raytracer.h:21-48), material hard-coded at ray.h:111-114.
@@ -2556,6 +2559,24 @@ __device__ __forceinline__ f3 shade_hw1(f3 o, f3 d, bool hit, f3 p, f3 n, f3 lpo
     if (c.y > 1.0f) c.y = 1.0f;
     if (c.z > 1.0f) c.z = 1.0f;
     return c;
+}
+
+// The pixel: the sample sum / float(spp) (HW1/src/render.cpp:113-115), as floats and/or as
+// write_p6-default samples (the frame epilogue fused in).
+__device__ __forceinline__ void hw1_write_pixel(const Hw1Params& P, int x, int y, f3 acc) {
+    const float fs = (float)P.spp;
+    const f3 px = mk(acc.x / fs, acc.y / fs, acc.z / fs);
+    const size_t k = ((size_t)y * P.W + x) * 3;
+    if (P.rgb) {
+        P.rgb[k] = px.x;
+        P.rgb[k + 1] = px.y;
+        P.rgb[k + 2] = px.z;
+    }
+    if (P.p6) {
+        P.p6[k] = rtp::p6_default_sample(px.x);
+        P.p6[k + 1] = rtp::p6_default_sample(px.y);
+        P.p6[k + 2] = rtp::p6_default_sample(px.z);
+    }
 }
 
 __global__ __launch_bounds__(BLOCK) void render_hw1_kernel(Hw1Params P) {
@@ -2605,20 +2626,14 @@ __global__ __launch_bounds__(BLOCK) void render_hw1_kernel(Hw1Params P) {
             P.hit_t[kk] = hit ? best : -1.0f;
         }
     }
-    if (valid) {
-        const float fs = (float)P.spp;
-        float* o = P.rgb + ((size_t)y * P.W + x) * 3;
-        o[0] = acc.x / fs;
-        o[1] = acc.y / fs;
-        o[2] = acc.z / fs;
-    }
+    if (valid) hw1_write_pixel(P, x, y, acc);
 }
 
 // ---- HW1 binned (rt_render_hw1 default; same output as render_hw1_kernel) ---------------
 // The brute-force loop's answer is the first index among the triangles ray_intersection
 // (mt_hw1) accepts with the smallest t.  Skipping triangles that provably cannot be accepted
 // for a ray, and visiting the rest in index order with the same strict `<`, gives that answer
-// bit for bit.  hw1_rect_kernel bounds, per triangle, the integer pixel positions (ix, iy)
+// bit for bit.  hw1_rect (hw1_rect_count_kernel) bounds, per triangle, the integer pixel positions (ix, iy)
 // whose camera ray mt_hw1 may accept; the render kernel gives each 16x16-pixel block the
 // triangles whose rectangle meets it, in index order.
 //
@@ -2643,9 +2658,7 @@ __device__ __forceinline__ void hw1_cross_d(const double a[3], const double b[3]
     r[2] = a[0] * b[1] - a[1] * b[0];
 }
 
-__global__ __launch_bounds__(BLOCK) void hw1_rect_kernel(Hw1Params P, int4* __restrict__ rects) {
-    const int k = (int)(blockIdx.x * BLOCK + threadIdx.x);
-    if (k >= P.num_tris) return;
+__device__ int4 hw1_rect(const Hw1Params& P, int k) {
     const int X0 = -2, X1 = P.W + 1, Y0 = -2, Y1 = P.H + 1;  // ix in [x, x+1] (truncation)
     const int4 all = make_int4(X0, Y0, X1, Y1), none = make_int4(1, 1, 0, 0);
     const float4 A = P.tri[3 * (size_t)k], B = P.tri[3 * (size_t)k + 1], Cq = P.tri[3 * (size_t)k + 2];
@@ -2658,8 +2671,7 @@ __global__ __launch_bounds__(BLOCK) void hw1_rect_kernel(Hw1Params P, int4* __re
                           qvec.x, qvec.y, qvec.z};
     for (int i = 0; i < 15; ++i) mag = fmax(mag, fabs((double)mv[i]));
     if (!(mag < 1e15) || !(fabsf(tnum) >= 1e-20f)) {
-        rects[k] = all;
-        return;
+        return all;
     }
     const double sg = tnum > 0.0f ? 1.0 : -1.0;
     const double tv[3] = {tvec.x, tvec.y, tvec.z}, ea[3] = {e1.x, e1.y, e1.z}, eb[3] = {e2.x, e2.y, e2.z},
@@ -2681,8 +2693,7 @@ __global__ __launch_bounds__(BLOCK) void hw1_rect_kernel(Hw1Params P, int4* __re
     Ev *= 4 * uu * dm;
     dmax = dmax * dm + Ed;
     if (!(dmax < 1e10)) {  // keeps |t| = |tnum / det| >= 1e-30: a wrong-sign t stays negative
-        rects[k] = all;
-        return;
+        return all;
     }
     const double tiny = 1e-30;
     double c[4][3], w[4];
@@ -2721,8 +2732,7 @@ __global__ __launch_bounds__(BLOCK) void hw1_rect_kernel(Hw1Params P, int4* __re
     }
     const double nmin = sqrt(nmin2) * (1 - 1e-12), nmax = sqrt(nmax2) * (1 + 1e-12);
     if (!(nmin > 0.0) || !(nmax < 1e300)) {
-        rects[k] = all;
-        return;
+        return all;
     }
     double px[8 + 4], py[8 + 4];
     int n = 4;
@@ -2744,8 +2754,7 @@ __global__ __launch_bounds__(BLOCK) void hw1_rect_kernel(Hw1Params P, int4* __re
         const double g = fmin(w1 * nmin, w1 * nmax);            // c.D >= w1 |D|
         const double ga = g - cpad - 1e-9 * cdm - tiny - cD00;  // al ix + be iy >= ga
         if (!(fabs(al) < 1e300 && fabs(be) < 1e300 && fabs(ga) < 1e300)) {
-            rects[k] = all;
-            return;
+            return all;
         }
         double qx[12], qy[12];
         int m = 0;
@@ -2771,8 +2780,7 @@ __global__ __launch_bounds__(BLOCK) void hw1_rect_kernel(Hw1Params P, int4* __re
         }
     }
     if (n == 0) {
-        rects[k] = none;
-        return;
+        return none;
     }
     double lx = px[0], hx = px[0], ly = py[0], hy = py[0];
     for (int j = 1; j < n; ++j) {
@@ -2781,11 +2789,11 @@ __global__ __launch_bounds__(BLOCK) void hw1_rect_kernel(Hw1Params P, int4* __re
         ly = fmin(ly, py[j]);
         hy = fmax(hy, py[j]);
     }
-    rects[k] = make_int4(max(X0, (int)floor(lx) - 1), max(Y0, (int)floor(ly) - 1), min(X1, (int)ceil(hx) + 1),
-                         min(Y1, (int)ceil(hy) + 1));
+    return make_int4(max(X0, (int)floor(lx) - 1), max(Y0, (int)floor(ly) - 1), min(X1, (int)ceil(hx) + 1),
+                     min(Y1, (int)ceil(hy) + 1));
 }
 
-// Binning (a tiled rasterizer's): hw1_bin_kernel counts, per 16x4-pixel wave tile, the
+// Binning (a tiled rasterizer's): hw1_rect_count_kernel counts, per 16x4-pixel wave tile, the
 // triangles whose rectangle meets the tile's (ix, iy) range (pixel x uses ix in {x, x+1});
 // hw1_scan_kernel turns the counts into offsets; hw1_fill_kernel writes the lists.  A list's
 // order is whatever the atomics give, so the render kernel keeps the lexicographic minimum of
@@ -2804,8 +2812,24 @@ __device__ __forceinline__ bool hw1_tile_range(const Hw1Params& P, int4 r, int& 
     return r.z >= 0 && r.w >= 0 && tx0 <= tx1 && ty0 <= ty1;
 }
 
-__global__ __launch_bounds__(BLOCK) void hw1_bin_kernel(Hw1Params P, uint32_t* __restrict__ counts, int fill,
-                                                        uint32_t* __restrict__ cursor, uint32_t* __restrict__ list) {
+// Pass 1: each triangle's rectangle (kept for pass 2) and its count in every tile it meets.
+__global__ __launch_bounds__(BLOCK) void hw1_rect_count_kernel(Hw1Params P, int4* __restrict__ rects,
+                                                               uint32_t* __restrict__ counts) {
+    const int k = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    if (k >= P.num_tris) return;
+    const int4 r = hw1_rect(P, k);
+    rects[k] = r;
+    const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
+    int tx0, tx1, ty0, ty1;
+    if (!hw1_tile_range(P, r, tx0, tx1, ty0, ty1)) return;
+    for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&counts[ty * tiles_x + tx], 1u);
+}
+
+// Pass 2: the lists.  A tile whose list would reach past list_cap is not written; the render
+// kernel gives that tile the brute-force loop instead.
+__global__ __launch_bounds__(BLOCK) void hw1_fill_kernel(Hw1Params P, uint32_t* __restrict__ cursor,
+                                                         uint32_t* __restrict__ list) {
     const int k = (int)(blockIdx.x * BLOCK + threadIdx.x);
     if (k >= P.num_tris) return;
     const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
@@ -2814,8 +2838,7 @@ __global__ __launch_bounds__(BLOCK) void hw1_bin_kernel(Hw1Params P, uint32_t* _
     for (int ty = ty0; ty <= ty1; ++ty)
         for (int tx = tx0; tx <= tx1; ++tx) {
             const int t = ty * tiles_x + tx;
-            if (!fill) atomicAdd(&counts[t], 1u);
-            else list[P.bin_offset[t] + atomicAdd(&cursor[t], 1u)] = (uint32_t)k;
+            if (P.bin_offset[t + 1] <= P.list_cap) list[P.bin_offset[t] + atomicAdd(&cursor[t], 1u)] = (uint32_t)k;
         }
 }
 
@@ -2858,8 +2881,12 @@ __global__ __launch_bounds__(BLOCK) void render_hw1_binned_kernel(Hw1Params P) {
     const bool valid = x < P.W && y < P.H;
     const bool tile_ok = ty * HW1_TH < P.H;  // wave-uniform
     const int tidx = ty * tiles_x + tx;
-    const uint32_t cnt = tile_ok ? uni(P.bin_count[tidx]) : 0u;
+    uint32_t cnt = tile_ok ? uni(P.bin_count[tidx]) : 0u;
     const uint32_t off = tile_ok ? uni(P.bin_offset[tidx]) : 0u;
+    // a list past the capacity was not written: every triangle, in index order (a list "of any
+    // order" whose entries are the indices themselves)
+    const bool all = tile_ok && off + cnt > P.list_cap;
+    if (all) cnt = (uint32_t)P.num_tris;
     f3 acc = mk(0.f, 0.f, 0.f);
     for (int s = 0; s < P.spp; ++s) {
         const float pxs = (float)x + P.jitter[2 * s];
@@ -2876,7 +2903,8 @@ __global__ __launch_bounds__(BLOCK) void render_hw1_binned_kernel(Hw1Params P) {
             int kk[4];
             float4 tq[12];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) kk[j] = i + j < cnt ? (int)ldc_u32(P.bin_list + off + i + j) : -1;
+            for (int j = 0; j < 4; ++j)
+                kk[j] = i + j < cnt ? (all ? (int)(i + j) : (int)ldc_u32(P.bin_list + off + i + j)) : -1;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const float4* T = P.tri + 3 * (size_t)(kk[j] < 0 ? kk[0] : kk[j]);
@@ -2917,13 +2945,7 @@ __global__ __launch_bounds__(BLOCK) void render_hw1_binned_kernel(Hw1Params P) {
             P.hit_t[kk] = hit ? best : -1.0f;
         }
     }
-    if (valid) {
-        const float fs = (float)P.spp;
-        float* out = P.rgb + ((size_t)y * P.W + x) * 3;
-        out[0] = acc.x / fs;
-        out[1] = acc.y / fs;
-        out[2] = acc.z / fs;
-    }
+    if (valid) hw1_write_pixel(P, x, y, acc);
 }
 
 __global__ __launch_bounds__(BLOCK) void powf_kernel(const float* __restrict__ x, const float* __restrict__ y, int n,
@@ -4187,23 +4209,49 @@ extern "C" int rt_render_hw1(int device, const rt_vec3* pos, const rt_vec3* nrm,
                             hit_t_host, nullptr);
 }
 
-extern "C" int rt_render_hw1_ex(int device, const rt_vec3* pos, const rt_vec3* nrm, const uint32_t* idx, size_t P,
-                                const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp, const float* jitter,
-                                int flags, float* rgb_host, int32_t* hit_idx_host, float* hit_t_host,
-                                float* kernel_ms) {
-    if (!pos || !nrm || !idx || !cam || !rgb_host || spp < 1 || P == 0)
-        return set_error(RT_ERR_ARG, "rt_render_hw1: bad argument (HW1 requires per-vertex normals)");
+// ---- HW1 resident scene (the C2 configuration's device path) ---------------------------
+// The mesh packed once (v0, e1, e2 as ray_intersection computes them, the three normals per
+// triangle), the binning buffers kept across frames.  A frame is four launches on the caller's
+// stream (counts zeroed, rect + count, scan, fill, render) and no host synchronisation: the
+// bin list's capacity is checked on the device (a tile whose list would not fit takes the
+// brute-force loop), and the host grows it from the latest finished frame's total.
+struct rt_hw1_scene {
+    int device = 0;
+    size_t P = 0;
+    DevBuf tri, nrm, rects, bins, list, jitter;
+    int bins_tiles = -1;       // tiles the bins buffer is laid out for
+    uint32_t list_cap = 0;
+    int jitter_spp = -1;
+    std::vector<float> jitter_host;
+    static constexpr int kRing = 64;
+    hipEvent_t e0[kRing] = {}, e1[kRing] = {};
+    uint32_t* total_host = nullptr;  // pinned: the list total of frame f at [f % kRing]
+    uint64_t frames = 0;
+    const char* last_kernel = "";
+    ~rt_hw1_scene() {
+        for (int i = 0; i < kRing; ++i) {
+            if (e0[i]) (void)hipEventSynchronize(e1[i]);
+            if (e0[i]) (void)hipEventDestroy(e0[i]);
+            if (e1[i]) (void)hipEventDestroy(e1[i]);
+        }
+        if (total_host) (void)hipHostFree(total_host);
+    }
+};
+
+extern "C" int rt_hw1_scene_create(int device, const rt_vec3* pos, const rt_vec3* nrm, const uint32_t* idx, size_t P,
+                                   rt_hw1_scene** out) {
+    if (!out) return set_error(RT_ERR_ARG, "rt_hw1_scene_create: null out");
+    *out = nullptr;
+    if (!pos || !nrm || !idx || P == 0)
+        return set_error(RT_ERR_ARG, "rt_hw1_scene_create: bad argument (HW1 requires per-vertex normals)");
     if (P > 0x7FFFFFFFull) return set_error(RT_ERR_UNSUPPORTED, "too many triangles");
-    if ((hit_idx_host == nullptr) != (hit_t_host == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
     int rc = check_device(device);
     if (rc != RT_OK) return rc;
     DeviceGuard g(device);
-    const int W = cam->pixel_width, H = cam->pixel_height;
     std::vector<float4> ht(3 * P), hn(3 * P);
-    size_t nv = 0;
-    for (size_t k = 0; k < 3 * P; ++k) nv = std::max<size_t>(nv, size_t(idx[k]) + 1);
     for (size_t k = 0; k < P; ++k) {
         const rt_vec3 a = pos[idx[3 * k]], b = pos[idx[3 * k + 1]], c = pos[idx[3 * k + 2]];
+        // e1 = v1 - v0, e2 = v2 - v0 exactly as ray_intersection computes them (HW1/include/ray.h:71-72)
         ht[3 * k] = make_float4(a.x, a.y, a.z, 0.f);
         ht[3 * k + 1] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, 0.f);
         ht[3 * k + 2] = make_float4(c.x - a.x, c.y - a.y, c.z - a.z, 0.f);
@@ -4212,23 +4260,77 @@ extern "C" int rt_render_hw1_ex(int device, const rt_vec3* pos, const rt_vec3* n
             hn[3 * k + j] = make_float4(n.x, n.y, n.z, 0.f);
         }
     }
+    std::unique_ptr<rt_hw1_scene> s(new (std::nothrow) rt_hw1_scene());
+    if (!s) return set_error(RT_ERR_NOMEM, "out of memory");
+    s->device = device;
+    s->P = P;
+    if ((rc = s->tri.upload(ht.data(), ht.size() * sizeof(float4))) != RT_OK) return rc;
+    if ((rc = s->nrm.upload(hn.data(), hn.size() * sizeof(float4))) != RT_OK) return rc;
+    if ((rc = s->rects.alloc(P * sizeof(int4))) != RT_OK) return rc;
+    // a first capacity: a few tiles per triangle (grown from the frames' totals)
+    s->list_cap = uint32_t(std::min<size_t>(std::max<size_t>(4 * P, size_t(1) << 16), 0x7FFFFFFFull));
+    if ((rc = s->list.alloc(size_t(s->list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->total_host), rt_hw1_scene::kRing * sizeof(uint32_t),
+                          hipHostMallocDefault));
+    for (int i = 0; i < rt_hw1_scene::kRing; ++i) {
+        s->total_host[i] = 0;
+        HIP_TRY(hipEventCreate(&s->e0[i]));
+        HIP_TRY(hipEventCreate(&s->e1[i]));
+    }
+    *out = s.release();
+    return RT_OK;
+}
+
+extern "C" void rt_hw1_scene_destroy(rt_hw1_scene* s) {
+    if (!s) return;
+    DeviceGuard g(s->device);
+    delete s;
+}
+
+extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp,
+                                    const float* jitter, int flags, float* rgb_dev, uint8_t* p6_dev,
+                                    int32_t* hit_idx_dev, float* hit_t_dev, void* stream) {
+    if (!s || !cam || spp < 1) return set_error(RT_ERR_ARG, "rt_render_hw1_device: bad argument");
+    if ((hit_idx_dev == nullptr) != (hit_t_dev == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
+    const int W = cam->pixel_width, H = cam->pixel_height;
+    if (W < 1 || H < 1) return set_error(RT_ERR_ARG, "camera has no pixels");
+    DeviceGuard g(s->device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int rc;
+    // jitter_samples(spp, 42u) offsets in [0,1) (HW1/include/antialias.h:12-27), or the caller's
     std::vector<float> tab(2 * size_t(spp));
     if (jitter) std::memcpy(tab.data(), jitter, tab.size() * sizeof(float));
     else if ((rc = rt_jittered_samples(spp, 42u, 0, tab.data())) != RT_OK) return rc;
-    DevBuf dt, dn, dj, drgb, dhi, dht;
-    if ((rc = dt.upload(ht.data(), ht.size() * sizeof(float4))) != RT_OK) return rc;
-    if ((rc = dn.upload(hn.data(), hn.size() * sizeof(float4))) != RT_OK) return rc;
-    if ((rc = dj.upload(tab.data(), tab.size() * sizeof(float))) != RT_OK) return rc;
-    const size_t npx = size_t(W) * size_t(H);
-    if ((rc = drgb.alloc(npx * 3 * sizeof(float))) != RT_OK) return rc;
-    if (hit_idx_host) {
-        if ((rc = dhi.alloc(npx * size_t(spp) * sizeof(int32_t))) != RT_OK) return rc;
-        if ((rc = dht.alloc(npx * size_t(spp) * sizeof(float))) != RT_OK) return rc;
+    if (s->jitter_spp != spp || s->jitter_host != tab) {
+        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->e1[(s->frames - 1) % rt_hw1_scene::kRing]));
+        if ((rc = s->jitter.upload(tab.data(), tab.size() * sizeof(float))) != RT_OK) return rc;
+        s->jitter_spp = spp;
+        s->jitter_host = tab;
+    }
+    const bool brute = (flags & RT_HW1_BRUTE) != 0;
+    const int ntiles = ((W + HW1_TW - 1) / HW1_TW) * ((H + HW1_TH - 1) / HW1_TH);
+    // the latest finished frame's list total (frames are scanned back to front, non-blocking)
+    for (uint64_t b = 1; b <= std::min<uint64_t>(s->frames, 4); ++b) {
+        const int sl = int((s->frames - b) % rt_hw1_scene::kRing);
+        if (hipEventQuery(s->e1[sl]) != hipSuccess) continue;
+        const uint32_t tot = s->total_host[sl];
+        if (tot > s->list_cap) {  // grow (the old list may still be read by frames in flight)
+            HIP_TRY(hipEventSynchronize(s->e1[(s->frames - 1) % rt_hw1_scene::kRing]));
+            s->list_cap = uint32_t(std::min<uint64_t>(uint64_t(tot) + tot / 4 + 1024, 0x7FFFFFFFull));
+            if ((rc = s->list.alloc(size_t(s->list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
+        }
+        break;
+    }
+    (void)hipGetLastError();  // a not-ready query is not an error of this call
+    if (!brute && s->bins_tiles != ntiles) {
+        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->e1[(s->frames - 1) % rt_hw1_scene::kRing]));
+        if ((rc = s->bins.alloc(size_t(3 * ntiles + 1) * sizeof(uint32_t))) != RT_OK) return rc;
+        s->bins_tiles = ntiles;
     }
     Hw1Params hp;
-    hp.tri = static_cast<const float4*>(dt.p);
-    hp.nrm = static_cast<const float4*>(dn.p);
-    hp.num_tris = int32_t(P);
+    hp.tri = static_cast<const float4*>(s->tri.p);
+    hp.nrm = static_cast<const float4*>(s->nrm.p);
+    hp.num_tris = int32_t(s->P);
     hp.center = f3{cam->center.x, cam->center.y, cam->center.z};
     hp.p00 = f3{cam->pixel00_loc.x, cam->pixel00_loc.y, cam->pixel00_loc.z};
     hp.du = f3{cam->pixel_delta_u.x, cam->pixel_delta_u.y, cam->pixel_delta_u.z};
@@ -4238,61 +4340,105 @@ extern "C" int rt_render_hw1_ex(int device, const rt_vec3* pos, const rt_vec3* n
     hp.spp = spp;
     hp.lpos = f3{lpos.x, lpos.y, lpos.z};
     hp.lcol = f3{lcol.x, lcol.y, lcol.z};
-    hp.jitter = static_cast<const float*>(dj.p);
-    hp.rgb = static_cast<float*>(drgb.p);
-    hp.hit_idx = static_cast<int32_t*>(dhi.p);
-    hp.hit_t = static_cast<float*>(dht.p);
-    const bool brute = (flags & RT_HW1_BRUTE) != 0;
-    DevBuf drect, dbin, dlist;
-    if (!brute && (rc = drect.alloc(P * sizeof(int4))) != RT_OK) return rc;
-    hp.rects = static_cast<const int4*>(drect.p);
+    hp.jitter = static_cast<const float*>(s->jitter.p);
+    hp.rgb = rgb_dev;
+    hp.hit_idx = hit_idx_dev;
+    hp.hit_t = hit_t_dev;
+    hp.p6 = p6_dev;
+    hp.rects = static_cast<const int4*>(s->rects.p);
     hp.bin_count = hp.bin_offset = hp.bin_list = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (kernel_ms) {
-        HIP_TRY(hipEventCreate(&e0));
-        HIP_TRY(hipEventCreate(&e1));
-        HIP_TRY(hipEventRecord(e0, nullptr));
-    }
+    hp.list_cap = s->list_cap;
+    const int sl = int(s->frames % rt_hw1_scene::kRing);
+    HIP_TRY(hipEventRecord(s->e0[sl], st));
     const int blocks = ((W + 15) / 16) * ((H + 15) / 16);
     if (brute) {
-        hipLaunchKernelGGL(render_hw1_kernel, dim3(blocks), dim3(BLOCK), 0, nullptr, hp);
+        hipLaunchKernelGGL(render_hw1_kernel, dim3(blocks), dim3(BLOCK), 0, st, hp);
+        s->last_kernel = "render_hw1_kernel";
     } else {
-        const dim3 tgrid(unsigned((P + BLOCK - 1) / BLOCK));
-        const int ntiles = ((W + HW1_TW - 1) / HW1_TW) * ((H + HW1_TH - 1) / HW1_TH);
-        if ((rc = dbin.alloc(size_t(3 * ntiles + 1) * sizeof(uint32_t))) != RT_OK) return rc;
-        uint32_t* counts = static_cast<uint32_t*>(dbin.p);
+        const dim3 tgrid(unsigned((s->P + BLOCK - 1) / BLOCK));
+        uint32_t* counts = static_cast<uint32_t*>(s->bins.p);
         uint32_t* cursor = counts + ntiles;
         uint32_t* offsets = cursor + ntiles;  // ntiles + 1 entries
-        HIP_TRY(hipMemsetAsync(counts, 0, size_t(2 * ntiles) * sizeof(uint32_t), nullptr));
-        hipLaunchKernelGGL(hw1_rect_kernel, tgrid, dim3(BLOCK), 0, nullptr, hp, static_cast<int4*>(drect.p));
-        hipLaunchKernelGGL(hw1_bin_kernel, tgrid, dim3(BLOCK), 0, nullptr, hp, counts, 0, cursor,
-                           static_cast<uint32_t*>(nullptr));
-        hipLaunchKernelGGL(hw1_scan_kernel, dim3(1), dim3(1024), 0, nullptr, counts, offsets, ntiles);
-        HIP_TRY(hipGetLastError());
-        uint32_t total = 0;
-        HIP_TRY(hipMemcpy(&total, offsets + ntiles, sizeof(total), hipMemcpyDeviceToHost));
-        if ((rc = dlist.alloc(std::max<size_t>(total, 1) * sizeof(uint32_t))) != RT_OK) return rc;
+        HIP_TRY(hipMemsetAsync(counts, 0, size_t(2 * ntiles) * sizeof(uint32_t), st));
+        hipLaunchKernelGGL(hw1_rect_count_kernel, tgrid, dim3(BLOCK), 0, st, hp, static_cast<int4*>(s->rects.p), counts);
+        hipLaunchKernelGGL(hw1_scan_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, ntiles);
         hp.bin_count = counts;
         hp.bin_offset = offsets;
-        hp.bin_list = static_cast<const uint32_t*>(dlist.p);
-        hipLaunchKernelGGL(hw1_bin_kernel, tgrid, dim3(BLOCK), 0, nullptr, hp, counts, 1, cursor,
-                           static_cast<uint32_t*>(dlist.p));
-        hipLaunchKernelGGL(render_hw1_binned_kernel, dim3(blocks), dim3(BLOCK), 0, nullptr, hp);
+        hp.bin_list = static_cast<const uint32_t*>(s->list.p);
+        hipLaunchKernelGGL(hw1_fill_kernel, tgrid, dim3(BLOCK), 0, st, hp, cursor, static_cast<uint32_t*>(s->list.p));
+        hipLaunchKernelGGL(render_hw1_binned_kernel, dim3(blocks), dim3(BLOCK), 0, st, hp);
+        s->last_kernel = "render_hw1_binned_kernel";
+        HIP_TRY(hipGetLastError());
+        // this frame's total, for the capacity of the next ones
+        HIP_TRY(hipMemcpyAsync(s->total_host + sl, offsets + ntiles, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     }
     HIP_TRY(hipGetLastError());
-    if (kernel_ms) HIP_TRY(hipEventRecord(e1, nullptr));
+    HIP_TRY(hipEventRecord(s->e1[sl], st));
+    s->frames++;
+    return RT_OK;
+}
+
+extern "C" int rt_hw1_kernel_times(const rt_hw1_scene* s, float* ms_out, int max, int* n_out) {
+    if (!s || !ms_out || !n_out || max < 0) return set_error(RT_ERR_ARG, "rt_hw1_kernel_times: bad argument");
+    DeviceGuard g(s->device);
+    const int n = int(std::min<uint64_t>({uint64_t(max), s->frames, uint64_t(rt_hw1_scene::kRing)}));
+    for (int i = 0; i < n; ++i) {
+        const int sl = int((s->frames - uint64_t(n - i)) % rt_hw1_scene::kRing);
+        HIP_TRY(hipEventSynchronize(s->e1[sl]));
+        HIP_TRY(hipEventElapsedTime(&ms_out[i], s->e0[sl], s->e1[sl]));
+    }
+    *n_out = n;
+    return RT_OK;
+}
+
+extern "C" const char* rt_hw1_kernel_name(const rt_hw1_scene* s) { return s ? s->last_kernel : ""; }
+
+extern "C" int rt_hw1_list_info(const rt_hw1_scene* s, int64_t info[2]) {
+    if (!s || !info) return set_error(RT_ERR_ARG, "rt_hw1_list_info: null argument");
+    DeviceGuard g(s->device);
+    info[0] = s->list_cap;
+    info[1] = 0;
+    if (s->frames > 0) {
+        const int sl = int((s->frames - 1) % rt_hw1_scene::kRing);
+        HIP_TRY(hipEventSynchronize(s->e1[sl]));
+        info[1] = s->total_host[sl];
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_render_hw1_ex(int device, const rt_vec3* pos, const rt_vec3* nrm, const uint32_t* idx, size_t P,
+                                const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp, const float* jitter,
+                                int flags, float* rgb_host, int32_t* hit_idx_host, float* hit_t_host,
+                                float* kernel_ms) {
+    if (!pos || !nrm || !idx || !cam || !rgb_host || spp < 1 || P == 0)
+        return set_error(RT_ERR_ARG, "rt_render_hw1: bad argument (HW1 requires per-vertex normals)");
+    if ((hit_idx_host == nullptr) != (hit_t_host == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
+    rt_hw1_scene* sp = nullptr;
+    int rc = rt_hw1_scene_create(device, pos, nrm, idx, P, &sp);
+    if (rc != RT_OK) return rc;
+    std::unique_ptr<rt_hw1_scene, void (*)(rt_hw1_scene*)> s(sp, rt_hw1_scene_destroy);
+    DeviceGuard g(device);
+    const int W = cam->pixel_width, H = cam->pixel_height;
+    const size_t npx = size_t(std::max(W, 0)) * size_t(std::max(H, 0));
+    DevBuf drgb, dhi, dht;
+    if ((rc = drgb.alloc(npx * 3 * sizeof(float))) != RT_OK) return rc;
+    if (hit_idx_host) {
+        if ((rc = dhi.alloc(npx * size_t(spp) * sizeof(int32_t))) != RT_OK) return rc;
+        if ((rc = dht.alloc(npx * size_t(spp) * sizeof(float))) != RT_OK) return rc;
+    }
+    rc = rt_render_hw1_device(sp, cam, lpos, lcol, spp, jitter, flags, static_cast<float*>(drgb.p), nullptr,
+                              static_cast<int32_t*>(dhi.p), static_cast<float*>(dht.p), nullptr);
+    if (rc != RT_OK) return rc;
     HIP_TRY(hipDeviceSynchronize());
     if (kernel_ms) {
-        HIP_TRY(hipEventElapsedTime(kernel_ms, e0, e1));
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
+        int n = 0;
+        if ((rc = rt_hw1_kernel_times(sp, kernel_ms, 1, &n)) != RT_OK) return rc;
     }
     HIP_TRY(hipMemcpy(rgb_host, drgb.p, npx * 3 * sizeof(float), hipMemcpyDeviceToHost));
     if (hit_idx_host) {
         HIP_TRY(hipMemcpy(hit_idx_host, dhi.p, npx * size_t(spp) * sizeof(int32_t), hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(hit_t_host, dht.p, npx * size_t(spp) * sizeof(float), hipMemcpyDeviceToHost));
     }
-    (void)nv;
     return RT_OK;
 }
 

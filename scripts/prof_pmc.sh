@@ -10,10 +10,12 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
+DRIVER=profile_frames.py
+case "$CFG" in c1|c2) DRIVER=profile_hw1.py ;; esac  # the HW1 path (rt_hw1_scene)
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- \
-      python3 "$ROOT/scripts/profile_frames.py" --config "$CFG" --frames "$FRAMES" --mode serial > "$OUT/$name.log" 2>&1
+      python3 "$ROOT/scripts/$DRIVER" --config "$CFG" --frames "$FRAMES" --mode serial > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"
   if [ $rc -ge 124 ]; then exit $rc; fi

@@ -28,8 +28,9 @@ a = ap.parse_args()
 
 
 def short(name):
-    for k in ("render_tiles_kernel", "render_samples_kernel", "tile_cull_kernel",
-              "render_hw1_kernel", "copyBuffer", "fillBuffer", "elementwise"):
+    for k in ("render_tiles_kernel", "render_samples_kernel", "tile_cull_kernel", "tile_cut_kernel",
+              "render_hw1_kernel", "render_hw1_binned_kernel", "hw1_rect_count_kernel", "hw1_scan_kernel",
+              "hw1_fill_kernel", "copyBuffer", "fillBuffer", "elementwise"):
         if k in name:
             return k
     return name[:40]
@@ -128,7 +129,7 @@ def binding(i):
 names = {n for n, _ in instances}
 if len(names) > 1:
     raise SystemExit(f"{a.prof}: several {a.kernel} instantiations {sorted(names)}: profile one per run")
-instance = names.pop() if names else None
+instance = names.pop() if names else (a.kernel if a.kernel in summary else None)  # (untemplated kernels)
 if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
     fetch = 2 * k["FETCH_SIZE"] * 1024
     write = k["WRITE_SIZE"] * 1024
@@ -138,6 +139,10 @@ if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
                       "fetch_bytes": round(fetch), "write_bytes": round(write),
                       "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
                                 f"{os.path.basename(a.prof.rstrip('/'))}; FETCH_SIZE x2 (gfx950), KiB->B"}
+    # every kernel of the profiled frames (the HW1 path's frame is four launches)
+    data[a.config]["per_kernel"] = {
+        kn: {"bytes_per_launch": round(2 * cs["FETCH_SIZE"] * 1024 + cs["WRITE_SIZE"] * 1024)}
+        for kn, cs in summary.items() if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs}
     iss = issue(k)
     if iss:
         data[a.config]["issue"] = iss

@@ -1,0 +1,97 @@
+"""The HW1 path resident on the device (rt_hw1_scene, the C2 configuration's bench path):
+frames against the reference's own HW1 outputs (tests/golden/scenes/c1_full, c2_full: the
+HW1/src/render.cpp:72-116 loop built from the reference sources), the P6 samples the render
+kernel writes against the reference's ppm_p6 file, and the bin list's capacity fallback (a tile
+whose list does not fit takes the brute-force loop) against the brute-force kernel."""
+from __future__ import annotations
+
+import gzip
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden_array, golden_meta
+
+import raytracinginonesemester_amd as rt
+from raytracinginonesemester_amd import configs
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _frame(sc, cam, c, spp, brute=False):
+    W, H = cam.pixel_width, cam.pixel_height
+    rgb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
+    p6 = torch.zeros(W * H * 3, dtype=torch.uint8, device="cuda")
+    hi = torch.zeros(W * H * spp, dtype=torch.int32, device="cuda")
+    ht = torch.zeros(W * H * spp, dtype=torch.float32, device="cuda")
+    sc.render_device(cam, c["light_pos"], c["light_color"], spp, rgb_ptr=rgb.data_ptr(), p6_ptr=p6.data_ptr(),
+                     hit_idx_ptr=hi.data_ptr(), hit_t_ptr=ht.data_ptr(),
+                     stream=torch.cuda.current_stream().cuda_stream, brute=brute)
+    torch.cuda.synchronize()
+    return rgb.cpu().numpy(), p6.cpu().numpy(), hi.cpu().numpy(), ht.cpu().numpy()
+
+
+@pytest.mark.parametrize("name,cfg", [("c1_full", "c1"), ("c2_full", "c2")])
+def test_resident_hw1_frames_match_reference(name, cfg):
+    c = configs.HW1_CONFIGS[cfg]
+    meta = golden_meta(name)
+    W, H = meta["width"], meta["height"]
+    mesh = rt.MeshHW1(configs.MESHES / c["mesh"])
+    cam = rt.Camera(c["position"], c["look_at"], c["up"], c["focal_mm"], c["sensor_mm"], W, H, hw1=True)
+    sc = rt.HW1Scene(mesh.positions, mesh.normals, mesh.indices)
+    try:
+        for _ in range(3):  # frames in a row on the same buffers: the same frame
+            rgb, p6, hi, ht = _frame(sc, cam, c, c["spp"])
+            assert np.array_equal(rgb.view(np.uint32), golden_array(name, "fb.f32.gz", np.float32).view(np.uint32))
+            assert np.array_equal(hi, golden_array(name, "hits.i32.gz", np.int32))
+            assert np.array_equal(ht.view(np.uint32), golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
+            want = gzip.open(GOLDEN / "scenes" / name / "image.ppm.gz").read()
+            assert rt.p6_header(W, H) + p6.tobytes() == want
+        assert sc.kernel_name() == "render_hw1_binned_kernel"
+        assert (sc.kernel_times(3) > 0).all()
+    finally:
+        sc.close()
+
+
+def _big_triangles(n=12, seed=3):
+    """n large overlapping triangles in front of the camera: each covers most of a 1080p image,
+    so their bin lists (~n x 32k tile entries) outgrow the first capacity (65536 entries)."""
+    rng = np.random.default_rng(seed)
+    pos, nrm, idx = [], [], []
+    for k in range(n):
+        z = -float(k) * 0.05
+        c = rng.uniform(-0.2, 0.2, size=2)
+        s = rng.uniform(2.0, 3.0)
+        v = [(c[0] - s, c[1] - s, z), (c[0] + s, c[1] - s, z), (c[0], c[1] + s, z)]
+        for j in range(3):
+            pos.append(v[j])
+            nrm.append((0.0, 0.0, 1.0) if k % 2 else (0.3, 0.0, 0.95))
+        idx.append((3 * k, 3 * k + 1, 3 * k + 2))
+    return np.array(pos, np.float32), np.array(nrm, np.float32), np.array(idx, np.uint32)
+
+
+def test_bin_list_capacity_fallback_is_exact():
+    """The first frame's lists outgrow the bin list (the tiles past the capacity take the
+    brute-force loop); the next frame runs with the capacity grown from the first frame's total.
+    Both frames equal the brute-force kernel bit for bit (AOVs included)."""
+    pos, nrm, idx = _big_triangles()
+    c = {"light_pos": (-3.0, 0.0, 1.0), "light_color": (1.0, 0.0, 1.0)}
+    cam = rt.Camera((0.0, 0.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, 24.0, 1920, 1080, hw1=True)
+    sc = rt.HW1Scene(pos, nrm, idx)
+    try:
+        ref = _frame(sc, cam, c, 2, brute=True)
+        cap0 = sc.list_info()[0]
+        for k in range(2):
+            got = _frame(sc, cam, c, 2)
+            cap, total = sc.list_info()
+            if k == 0:  # the first frame's lists outgrew the list: its last tiles took the brute-force loop
+                assert total > cap0
+            else:  # the second ran with a list grown from the first frame's total
+                assert cap >= total > cap0
+            for x, y in zip(got, ref):
+                assert np.array_equal(x.view(np.uint8), y.view(np.uint8))
+        assert (ref[2] >= 0).mean() > 0.3
+    finally:
+        sc.close()

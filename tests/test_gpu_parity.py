@@ -730,7 +730,7 @@ def test_spine_trees_deep_frustum_stack(L, log2):
     rgb, hi, ht = orc.render_g(a["P"], oracle_camera(cam), a["nodes"], a["aabbs"], a["tris"], a["objids"], a["mats"],
                                a["lights"], spp=4, max_depth=1, aov=True)
     assert np.array_equal(got[1], hi) and np.array_equal(got[2].view(np.uint32), ht.view(np.uint32))
-    assert (hi >= 0).mean() > 0.5
+    assert (hi >= 0).mean() > 0.3
     _check_fb(got[0], rgb)
 
 

@@ -702,14 +702,19 @@ def hw1_main(a):
     tr = load_traffic(Path(a.traffic_file), a.config, instance)
     roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": instance,
             "kernel_ms": round(kernel_ms, 4), "note": "kernel_ms: the frame's four launches, HIP events around them"}
-    if tr and tr.get("bytes_per_launch"):
-        ach = tr["bytes_per_launch"] / (tr.get("kernel_ms", kernel_ms) / 1e3) / 1e9
-        roof.update(traffic=tr["bytes_per_launch"], achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
-                    achieved_from=f"measured HBM bytes per frame (rocprofv3 --pmc, {tr.get('source', '?')}) / "
-                                  "the profiled frame's kernel time")
-        for k in ("issue", "binding", "per_kernel"):
+    hw1_kernels = ("hw1_rect_count_kernel", "hw1_scan_kernel", "hw1_fill_kernel", "render_hw1_binned_kernel")
+    per = (tr or {}).get("per_kernel") or {}
+    if tr and all(k in per for k in hw1_kernels):
+        # the frame's four launches (the live kernel_ms spans them): their measured bytes summed
+        frame_bytes = sum(per[k]["bytes_per_launch"] for k in hw1_kernels)
+        ach = frame_bytes / (kernel_ms / 1e3) / 1e9
+        roof.update(traffic=frame_bytes, achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
+                    achieved_from=f"measured HBM bytes of the frame's four kernels (rocprofv3 --pmc, "
+                                  f"{tr.get('source', '?')}) / live kernel_ms",
+                    per_kernel={k: per[k] for k in hw1_kernels})
+        for k in ("issue", "binding"):
             if tr.get(k):
-                roof[k] = tr[k]
+                roof[f"render_kernel_{k}"] = tr[k]
     else:
         roof.update(traffic=None, achieved=None, frac=None,
                     achieved_from=f"no PMC traffic profiled for {instance} on {a.config} (profiles/traffic.json)")

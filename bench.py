@@ -360,7 +360,8 @@ def native(a, hs, cam, cfg, ctx):
     res = {"elapsed": elapsed, "kernel_ms": max(kts), "frame_ms": max(fts), "prepass_ms": max(pts),
            "kernel_ms_local": kts, "live_tiles": list(sc.live_tiles()), "heavy_tiles": sc.heavy_tiles(),
            "kernel_instance": sc.kernel_name(),
-           "gather_path": GATHER_NAMES[gather], "warmup_frames_run": warm_run, "gather_note": gather_note}
+           "gather_path": GATHER_NAMES[gather], "warmup_frames_run": warm_run, "gather_note": gather_note,
+           "copy_engine": r.copy_engine}
     if ctx.rank == 0:
         g, d, f = (r.times(k, a.steps) for k in (rt.RT_TIME_GATHER, rt.RT_TIME_DELIVER, rt.RT_TIME_FRAME))
         res.update(gather_ms=float(g.mean()), deliver_ms=float(d.mean()), frame_latency_ms=float(f.mean()))
@@ -750,8 +751,10 @@ def main():
     hs = rt.HostScene.load_json(sp, REPO if sp.parent == configs.SCENES else sp.parent)
     cam = hs.camera(cfg["width"], cfg["height"])
     W, H, spp = cam.pixel_width, cam.pixel_height, cfg["spp"]
-    if a.depth is None:
-        a.depth = 2 if world == 1 else 3
+    if a.depth is None:  # frames in flight (N = 1: depth 3 keeps the host's waits off the critical
+        # path; the driver's 20-step command: 0.171 ms/step vs 0.174-0.262 at depth 2 with SDMA copies,
+        # profiles/r05/exp/driver_cmd_depth_ab.log)
+        a.depth = 3
 
     comm = a.comm
     fallback = None
@@ -824,6 +827,9 @@ def main():
         "step_delivers": (f"the frame's {'P6 samples (PPM body)' if a.deliver == 'p6' else 'float framebuffer'}"
                           " in rank 0's host memory, every timed frame waited for"),
         "comm": (f"native rt_renderer, gather={gpath}: {COMM_TEXT[gpath]}" if comm == "native" else gpath),
+        "copy_engine": (("sdma: P6 copies queued through the HSA runtime on a DMA engine once each frame's "
+                         "render event fires (no CU slots)" if res.get("copy_engine") == "sdma" else
+                         "runtime: hipMemcpyAsync (blit kernels on the CUs)") if comm == "native" else None),
         "pipeline_depth": a.depth if comm == "native" else 2, "kernel": a.kernel}
     if a.share_gpu and world > 1:
         line["config"]["rehearsal"] = "--share-gpu: ranks share GPUs (not a multi-GPU measurement)"

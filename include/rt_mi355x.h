@@ -337,6 +337,11 @@ typedef struct {
 } rt_renderer_opts;
 void rt_renderer_opts_default(rt_renderer_opts* o);
 
+/* 1 when the renderer delivers its frames with SDMA copies queued through the HSA runtime (one
+ * rank, RT_GATHER_DIRECT, a host frame; RT_TUNE_COPY_ENGINE), 0 when with the HIP runtime's
+ * copies (blit kernels on the CUs). */
+int rt_renderer_copy_engine(const rt_renderer* r);
+
 /* 128-byte RCCL unique id for a multi-process renderer (call on rank 0's process). */
 int rt_comm_unique_id(void* id128);
 
@@ -493,7 +498,9 @@ typedef enum {
     RT_TUNE_PEER_TIMEOUT_S = 9,  /* rt_renderer: seconds to wait for a peer rank (120) */
     RT_TUNE_RENDERER_THREADS = 10, /* rt_renderer: -1 auto (default: a thread per further distinct
                                       GPU), 0 submit every rank from the caller, 1 threads always */
-    RT_TUNE_COUNT = 11
+    RT_TUNE_COPY_ENGINE = 11,    /* rt_renderer's host delivery: -1 auto (SDMA where it applies: one rank,
+                                    DIRECT, a host frame), 0 the HIP runtime's copies, 1 SDMA or fail */
+    RT_TUNE_COUNT = 12
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */
 int rt_tuning_set(int id, double value);

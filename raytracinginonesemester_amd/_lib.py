@@ -30,7 +30,7 @@ RT_FAULT_FRUSTUM_STACK = 1
 # rt_tune_id (include/rt_mi355x.h): knob name -> id
 TUNE = {"frustum_arity": 0, "half_waves": 1, "paired_only": 2, "heavy_frac": 3, "heavy_cap": 4,
         "cull_coverage": 5, "cull_boxes": 6, "big_scene_bytes": 7, "frustum_stack_cap": 8,
-        "peer_timeout_s": 9, "renderer_threads": 10}
+        "peer_timeout_s": 9, "renderer_threads": 10, "copy_engine": 11}
 
 
 class RTError(RuntimeError):
@@ -163,6 +163,7 @@ SIGNATURES = {
     "rt_renderer_render": (I, [P, P, P, P, SZ]),
     "rt_renderer_scene": (P, [P, I]),
     "rt_renderer_local_ranks": (I, [P]),
+    "rt_renderer_copy_engine": (I, [P]),
     "rt_renderer_times": (I, [P, I, P, I, P]),
     "rt_render_hw1": (I, [I, P, P, P, SZ, P, Vec3, Vec3, I, P, P, P, P]),
     "rt_render_hw1_ex": (I, [I, P, P, P, SZ, P, Vec3, Vec3, I, P, I, P, P, P, P]),

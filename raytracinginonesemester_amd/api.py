@@ -404,6 +404,11 @@ class Renderer:
                    hs.lights, **kw)
 
     @property
+    def copy_engine(self) -> str:
+        """"sdma" (copies queued through the HSA runtime on a DMA engine) or "runtime" (HIP's)."""
+        return "sdma" if lib().rt_renderer_copy_engine(self._h) else "runtime"
+
+    @property
     def local_ranks(self) -> int:
         return int(lib().rt_renderer_local_ranks(self._h))
 

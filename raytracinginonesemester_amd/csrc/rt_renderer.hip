@@ -19,7 +19,10 @@
 // RCCL is loaded at run time (dlopen "librccl.so.1"): in a process that has imported torch
 // this is torch's own RCCL (same soname, already loaded), otherwise the image's.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <rccl/rccl.h>
+#include <immintrin.h>
 
 #include <dlfcn.h>
 #include <fcntl.h>
@@ -35,6 +38,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -117,6 +121,193 @@ int nccl_error(ncclResult_t e, const char* what) {
 
 
 constexpr int kTimeRing = 256;
+
+// ---- SDMA copies through the HSA runtime ---------------------------------------------------
+// The runtime's device-to-host copy (hipMemcpyAsync) runs as a blit kernel on the CUs beside the
+// next frame's render kernel: a c3 frame's 6.2 MB P6 body takes ~0.125 ms of PCIe time, and the
+// render kernel beside it lost ~10 us per frame (profiles/r05/exp/).  hsa_amd_memory_async_copy
+// from device memory to system memory runs on a DMA (SDMA) engine instead.  It cannot wait for a
+// HIP event on the device, so a copier thread waits for the frame's render event and queues the
+// copy; its completion is an HSA signal the renderer waits for.  HSA is resolved at run time from
+// the runtime HIP itself loaded (same soname: torch's in a torch process, else the image's).
+struct Hsa {
+    bool ok = false;
+    std::string err;
+    decltype(&hsa_init) init = nullptr;
+    decltype(&hsa_iterate_agents) iterate_agents = nullptr;
+    decltype(&hsa_agent_get_info) agent_get_info = nullptr;
+    decltype(&hsa_signal_create) signal_create = nullptr;
+    decltype(&hsa_signal_destroy) signal_destroy = nullptr;
+    decltype(&hsa_signal_store_screlease) signal_store = nullptr;
+    decltype(&hsa_signal_wait_scacquire) signal_wait = nullptr;
+    decltype(&hsa_amd_memory_async_copy) async_copy = nullptr;
+    decltype(&hsa_amd_profiling_async_copy_enable) prof_enable = nullptr;
+    decltype(&hsa_amd_profiling_get_async_copy_time) prof_copy_time = nullptr;
+    decltype(&hsa_system_get_info) system_get_info = nullptr;
+    uint64_t ts_hz = 0;
+};
+
+const Hsa& hsa() {
+    static Hsa H;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("libhsa-runtime64.so.1", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+        if (!h) h = dlopen("libhsa-runtime64.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            const char* e = dlerror();
+            H.err = std::string("dlopen libhsa-runtime64.so.1: ") + (e ? e : "?");
+            return;
+        }
+        bool all = true;
+        auto sym = [&](auto& fp, const char* name) {
+            fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+            if (!fp) {
+                all = false;
+                H.err += std::string(" missing ") + name;
+            }
+        };
+        sym(H.init, "hsa_init");
+        sym(H.iterate_agents, "hsa_iterate_agents");
+        sym(H.agent_get_info, "hsa_agent_get_info");
+        sym(H.signal_create, "hsa_signal_create");
+        sym(H.signal_destroy, "hsa_signal_destroy");
+        sym(H.signal_store, "hsa_signal_store_screlease");
+        sym(H.signal_wait, "hsa_signal_wait_scacquire");
+        sym(H.async_copy, "hsa_amd_memory_async_copy");
+        sym(H.prof_enable, "hsa_amd_profiling_async_copy_enable");
+        sym(H.prof_copy_time, "hsa_amd_profiling_get_async_copy_time");
+        sym(H.system_get_info, "hsa_system_get_info");
+        // (HIP initialised the runtime; hsa_init only counts one more user)
+        if (all && H.init() != HSA_STATUS_SUCCESS) {
+            all = false;
+            H.err = "hsa_init failed";
+        }
+        if (all && (H.prof_enable(true) != HSA_STATUS_SUCCESS ||
+                    H.system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &H.ts_hz) != HSA_STATUS_SUCCESS || !H.ts_hz)) {
+            all = false;
+            H.err = "HSA copy profiling unavailable";
+        }
+        H.ok = all;
+    });
+    return H;
+}
+
+uint64_t hsa_now() {
+    uint64_t t = 0;
+    (void)hsa().system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &t);
+    return t;
+}
+
+// The HSA GPU agent of HIP device `device` (by PCI domain / bus / device / function) and a CPU
+// agent (the destination agent of a copy into system memory).
+bool hsa_agents(int device, hsa_agent_t* gpu, hsa_agent_t* cpu) {
+    const Hsa& H = hsa();
+    if (!H.ok) return false;
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess) return false;
+    struct Q {
+        const Hsa* H;
+        uint32_t bdf, domain;
+        hsa_agent_t gpu{0}, cpu{0};
+        bool g = false, c = false;
+    } q{&H, uint32_t(p.pciBusID) << 8 | uint32_t(p.pciDeviceID) << 3, uint32_t(p.pciDomainID)};
+    auto cb = [](hsa_agent_t a, void* d) -> hsa_status_t {
+        Q& q = *static_cast<Q*>(d);
+        hsa_device_type_t t;
+        if (q.H->agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+        if (t == HSA_DEVICE_TYPE_CPU && !q.c) {
+            q.cpu = a;
+            q.c = true;
+        } else if (t == HSA_DEVICE_TYPE_GPU) {
+            uint32_t bdf = 0, dom = 0;
+            (void)q.H->agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
+            (void)q.H->agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &dom);
+            if ((bdf & ~7u) == q.bdf && dom == q.domain) {
+                q.gpu = a;
+                q.g = true;
+            }
+        }
+        return HSA_STATUS_SUCCESS;
+    };
+    if (H.iterate_agents(cb, &q) != HSA_STATUS_SUCCESS || !q.g || !q.c) return false;
+    *gpu = q.gpu;
+    *cpu = q.cpu;
+    return true;
+}
+
+// One thread per renderer: for each queued frame, wait for its render event (spinning: the
+// frames come every ~0.15 ms), then queue its SDMA copy, whose completion decrements `done`.
+class DmaCopier {
+  public:
+    struct Job {
+        hipEvent_t ready;
+        void* dst;
+        const void* src;
+        size_t bytes;
+        hsa_signal_t done;
+    };
+    DmaCopier(hsa_agent_t gpu, hsa_agent_t cpu) : gpu_(gpu), cpu_(cpu) { th_ = std::thread([this] { loop(); }); }
+    ~DmaCopier() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    void push(const Job& j) {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            q_.push_back(j);
+        }
+        cv_.notify_one();
+    }
+    // the first failure of the copier (its jobs' signals were completed so nobody hangs)
+    int error(std::string* msg) {
+        std::lock_guard<std::mutex> lk(m_);
+        if (msg) *msg = err_;
+        return rc_;
+    }
+
+  private:
+    void loop() {
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [this] { return quit_ || !q_.empty(); });
+                if (q_.empty()) return;  // quit_ with nothing left
+                j = q_.front();
+                q_.pop_front();
+            }
+            hipError_t e;
+            for (uint32_t i = 0; (e = hipEventQuery(j.ready)) == hipErrorNotReady; ++i) {
+                if (i < 4096) _mm_pause();
+                else std::this_thread::yield();
+            }
+            const Hsa& H = hsa();
+            hsa_status_t hs = HSA_STATUS_SUCCESS;
+            if (e == hipSuccess) hs = H.async_copy(j.dst, cpu_, j.src, gpu_, j.bytes, 0, nullptr, j.done);
+            if (e != hipSuccess || hs != HSA_STATUS_SUCCESS) {
+                std::lock_guard<std::mutex> lk(m_);
+                if (rc_ == RT_OK) {
+                    rc_ = RT_ERR_HIP;
+                    err_ = e != hipSuccess ? hip_msg(e, "render event (SDMA delivery)")
+                                           : "hsa_amd_memory_async_copy failed: " + std::to_string(int(hs));
+                }
+                H.signal_store(j.done, 0);
+            }
+        }
+    }
+    hsa_agent_t gpu_, cpu_;
+    std::thread th_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<Job> q_;
+    bool quit_ = false;
+    int rc_ = RT_OK;
+    std::string err_;
+};
 
 // Bands of rank r (b % world == r) in its strip, in band order, go to image rows b*band_rows.
 // The full bands are one strided 2-D copy; a partial last band (H % band_rows) a plain one.
@@ -347,6 +538,14 @@ struct rt_renderer {
     hipEvent_t ta[3][kTimeRing] = {}, tb[3][kTimeRing] = {};
     bool owns_scenes = true;
     RankPool pool;  // in-process renderers over several GPUs: per-rank submission threads
+    // SDMA delivery (one rank, DIRECT, a host frame): per slot the copy's completion signal and
+    // the HSA timestamp of the frame's submission; per ring entry the copy's and the frame's ms
+    std::unique_ptr<DmaCopier> dma;
+    std::vector<hsa_signal_t> dma_done;
+    std::vector<uint64_t> dma_submit_ts;
+    std::vector<bool> dma_pending;
+    float dma_deliver_ms[kTimeRing] = {}, dma_frame_ms[kTimeRing] = {};
+    bool dma_timed[kTimeRing] = {};
 
     ~rt_renderer() { release(); }
     // HOST_SHARED, after this process's copy streams were synchronised: publish every frame its
@@ -375,6 +574,14 @@ struct rt_renderer {
     }
     void release() {
         pool.stop();
+        if (dma) {  // every queued copy completes before its buffers go
+            for (size_t i = 0; i < dma_done.size(); ++i)
+                if (dma_pending[i]) (void)hsa().signal_wait(dma_done[i], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                                            HSA_WAIT_STATE_BLOCKED);
+            dma.reset();
+            for (hsa_signal_t d : dma_done) (void)hsa().signal_destroy(d);
+            dma_done.clear();
+        }
         for (LocalRank& L : ranks) {
             DeviceGuard g(L.device);
             if (L.compute) (void)hipStreamSynchronize(L.compute);
@@ -557,6 +764,11 @@ int ensure_geometry(rt_renderer* r, int W, int H) {
         HIP_TRY(hipStreamSynchronize(L.comm));
         HIP_TRY(hipStreamSynchronize(L.copy));
     }
+    for (size_t i = 0; i < r->dma_pending.size(); ++i)  // SDMA copies still reading the buffers
+        if (r->dma_pending[i]) {
+            (void)hsa().signal_wait(r->dma_done[i], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+            r->dma_pending[i] = false;
+        }
     r->publish_copied();
     r->release_buffers();
     r->first_valid = r->next;
@@ -610,9 +822,29 @@ void publish_done(rt_renderer* r, uint64_t ticket) {
     for (const LocalRank& L : r->ranks) SharedFrames::raise_to(r->shared->done(L.rank), ticket + 1);
 }
 
+// SDMA delivery: wait for slot s's copy (of frame `ticket`) and keep its times.
+int wait_dma(rt_renderer* r, int s, uint64_t ticket) {
+    if (!r->dma || !r->dma_pending[s]) return RT_OK;
+    const Hsa& H = hsa();
+    (void)H.signal_wait(r->dma_done[s], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+    r->dma_pending[s] = false;
+    std::string msg;
+    if (int rc = r->dma->error(&msg); rc != RT_OK) return set_error(rc, msg);
+    hsa_amd_profiling_async_copy_time_t ct{};
+    const int ring = int(ticket % kTimeRing);
+    r->dma_timed[ring] = false;
+    if (H.prof_copy_time(r->dma_done[s], &ct) == HSA_STATUS_SUCCESS && ct.end >= ct.start) {
+        r->dma_deliver_ms[ring] = float(double(ct.end - ct.start) / double(H.ts_hz) * 1e3);
+        r->dma_frame_ms[ring] = float(double(ct.end - std::min(ct.end, r->dma_submit_ts[s])) / double(H.ts_hz) * 1e3);
+        r->dma_timed[ring] = true;
+    }
+    return RT_OK;
+}
+
 // Host wait until slot s may be reused (its previous frame fully delivered / released).
 int wait_slot(rt_renderer* r, int s) {
     if (r->slot_ticket[s] == 0) return RT_OK;
+    if (int rc = wait_dma(r, s, r->slot_ticket[s] - 1); rc != RT_OK) return rc;
     for (LocalRank& L : r->ranks) {
         DeviceGuard g(L.device);
         if (L.released[s]) HIP_TRY(hipEventSynchronize(L.released[s]));
@@ -722,9 +954,32 @@ extern "C" int rt_renderer_create(size_t P, const rt_bvh_node* nodes, const rt_a
     const double threads = rt::tuning(RT_TUNE_RENDERER_THREADS, -1.0);
     const bool use_pool = threads < 0.0 ? distinct : threads != 0.0;
     if (n > 1 && use_pool) r->pool.start(n - 1);
+    // RT_TUNE_COPY_ENGINE: -1 (default) SDMA where it applies, 0 the runtime's copies, 1 SDMA or
+    // fail.  It applies to one rank delivering into a host frame over its own PCIe link.
+    const double engine = rt::tuning(RT_TUNE_COPY_ENGINE, -1.0);
+    const bool dma_fits = world == 1 && n == 1 && gather == RT_GATHER_DIRECT &&
+                          (o->deliver == RT_DELIVER_P6 || o->deliver == RT_DELIVER_F32);
+    if (engine != 0.0 && dma_fits) {
+        hsa_agent_t ga{0}, ca{0};
+        if (hsa_agents(r->ranks[0].device, &ga, &ca)) {
+            r->dma_done.assign(depth, hsa_signal_t{0});
+            for (hsa_signal_t& d : r->dma_done)
+                if (hsa().signal_create(0, 0, nullptr, &d) != HSA_STATUS_SUCCESS)
+                    return set_error(RT_ERR_HIP, "hsa_signal_create failed");
+            r->dma_submit_ts.assign(depth, 0);
+            r->dma_pending.assign(depth, false);
+            r->dma = std::make_unique<DmaCopier>(ga, ca);
+        } else if (engine > 0.0) {
+            return set_error(RT_ERR_UNSUPPORTED, "SDMA delivery unavailable: " + hsa().err);
+        }
+    } else if (engine > 0.0) {
+        return set_error(RT_ERR_UNSUPPORTED, "SDMA delivery applies to one rank delivering into a host frame");
+    }
     *out = r.release();
     return RT_OK;
 }
+
+extern "C" int rt_renderer_copy_engine(const rt_renderer* r) { return r && r->dma ? 1 : 0; }
 
 extern "C" void rt_renderer_destroy(rt_renderer* r) { delete r; }
 
@@ -797,6 +1052,13 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
                                                   std::to_string(t - uint64_t(r->depth)) + " within the peer timeout (RT_TUNE_PEER_TIMEOUT_S)");
         }
         DeviceGuard g(L.device);
+        if (own && r->dma && L.rendered[s]) {  // SDMA: queued by the copier once the frame is rendered
+            hsa().signal_store(r->dma_done[s], 1);
+            r->dma_submit_ts[s] = hsa_now();
+            r->dma_pending[s] = true;
+            r->dma->push({L.rendered[s], dst, L.strip[s].p, r->frame_bytes, r->dma_done[s]});
+            return RT_OK;
+        }
         if (own) {
             if (L.rendered[s]) HIP_TRY(hipStreamWaitEvent(L.copy, L.rendered[s], 0));
             HIP_TRY(hipEventRecord(r->td0[ring], L.copy));
@@ -885,6 +1147,13 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
     }
     // 2'. DIRECT / HOST_SHARED: the copies went out with the ranks' jobs; rank 0's frame is
     // complete when every local copy is.
+    if (r->dma && R0.rendered[s]) {  // SDMA: the strip is free and the frame delivered with the copy
+        r->delivered[s] = nullptr;
+        R0.released[s] = nullptr;
+        r->ta[RT_TIME_DELIVER][ring] = r->tb[RT_TIME_DELIVER][ring] = r->tb[RT_TIME_FRAME][ring] = nullptr;
+        r->dma_timed[ring] = false;
+        return RT_OK;
+    }
     if (r->rank0_local) {
         DeviceGuard g(R0.device);
         for (size_t i = 1; i < r->ranks.size(); ++i)  // the frame is complete when every local copy is
@@ -914,6 +1183,7 @@ extern "C" int rt_renderer_wait(rt_renderer* r, uint64_t ticket, const void** fr
     if (ticket < r->first_valid)
         return set_error(RT_ERR_ARG, "rt_renderer_wait: frame submitted before a change of the frame size");
     const int s = int(ticket % uint64_t(r->depth));
+    if (int rc = wait_dma(r, s, ticket); rc != RT_OK) return rc;
     for (LocalRank& L : r->ranks) {
         DeviceGuard g(L.device);
         if (L.released[s]) HIP_TRY(hipEventSynchronize(L.released[s]));
@@ -978,6 +1248,10 @@ extern "C" int rt_renderer_times(rt_renderer* r, int kind, float* ms_out, int ma
         const int i = int((r->next - uint64_t(n) + uint64_t(k)) % kTimeRing);
         hipEvent_t a = r->ta[kind][i], b = r->tb[kind][i];
         ms_out[k] = 0.0f;  // a step that did not run (no gather in DIRECT mode, no copy at deliver none)
+        if (r->dma_timed[i] && kind != RT_TIME_GATHER) {  // SDMA: the copy's own timestamps (waited frames)
+            ms_out[k] = kind == RT_TIME_DELIVER ? r->dma_deliver_ms[i] : r->dma_frame_ms[i];
+            continue;
+        }
         if (!a || !b) continue;
         HIP_TRY(hipEventSynchronize(b));
         HIP_TRY(hipEventElapsedTime(&ms_out[k], a, b));

@@ -128,6 +128,51 @@ def test_pipelined_frames_all_identical(frog, golden):
         r.close()
 
 
+@pytest.mark.parametrize("engine", [None, 0, 1])
+@pytest.mark.parametrize("depth", [2, 3])
+def test_copy_engines_deliver_the_reference_frame(frog, golden, engine, depth, tune):
+    """One rank delivering into host memory: by default (and with RT_TUNE_COPY_ENGINE=1) the
+    frames go through SDMA copies queued through the HSA runtime, with 0 through the HIP
+    runtime's copies.  Pipelined frames with alternating cameras are each the single-frame image
+    (P6 and float; the c3 frame is the reference's), and so is a frame after a resize; the
+    copy's own times are reported."""
+    tune(copy_engine=engine)
+    base = frog.camera(W, H)
+    cams = [base, rt.Camera(tuple(np.add(base.pos, (0.004, 0.0, 0.003))), base.look_at, base.up,
+                            base.focal_length_mm, base.sensor_height_mm, W, H)]
+    for deliver in (rt.RT_DELIVER_P6, rt.RT_DELIVER_F32):
+        r = rt.Renderer.from_host(frog, devices=(0,), depth=depth, deliver=deliver)
+        try:
+            assert r.copy_engine == ("runtime" if engine == 0 else "sdma")
+            o, _j = _opts(frog)
+            want = []
+            for c in cams:  # the single-frame images
+                addr, n = r.wait(r.submit(c, o))
+                want.append(bytes((C.c_uint8 * n).from_address(addr)))
+            assert want[0] == (golden[1].tobytes() if deliver == rt.RT_DELIVER_P6 else golden[0].tobytes())
+            assert want[1] != want[0]
+            pend = []
+            for k in [0, 1, 1, 0, 1, 0, 0, 1, 0, 1]:
+                pend.append((k, r.submit(cams[k], o)))
+                if len(pend) >= depth:
+                    kk, t = pend.pop(0)
+                    addr, n = r.wait(t)
+                    assert bytes((C.c_uint8 * n).from_address(addr)) == want[kk]
+            for kk, t in pend:
+                addr, n = r.wait(t)
+                assert bytes((C.c_uint8 * n).from_address(addr)) == want[kk]
+            d = r.times(rt.RT_TIME_DELIVER, 4)
+            f = r.times(rt.RT_TIME_FRAME, 4)
+            assert np.all(d > 0) and np.all(f >= d)
+            small = frog.camera(640, 360)  # a resize, then back
+            a1 = bytes((C.c_uint8 * (640 * 360 * 3 * (4 if deliver == rt.RT_DELIVER_F32 else 1))).from_address(
+                r.wait(r.submit(small, o))[0]))
+            addr, n = r.wait(r.submit(base, o))
+            assert bytes((C.c_uint8 * n).from_address(addr)) == want[0] and len(a1) == n // 9
+        finally:
+            r.close()
+
+
 def test_wait_rejects_stale_ticket(frog):
     r = rt.Renderer.from_host(frog, devices=(0,), depth=2)
     try:

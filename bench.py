@@ -695,22 +695,22 @@ def hw1_main(a):
                                    "(HW1/include/raytracer.h:21-48), brute-force winner (first index on ties)",
                        "triangles": mesh.num_triangles,
                        "step_delivers": "the frame's P6 samples in host memory (pinned), frames in stream order",
-                       "kernels": "hw1_rect_count_kernel + hw1_scan_kernel + hw1_fill_kernel + "
-                                  "render_hw1_binned_kernel (rt_render_hw1_device)"}}
+                       "kernels": "hw1_rect_count_kernel + hw1_scan_chunks_kernel + hw1_fill_kernel + "
+                                  "render_hw1_chunks_kernel + hw1_resolve_kernel (rt_render_hw1_device)"}}
     if a.tune:
         line["config"]["tuning"] = dict(kv.partition("=")[::2] for kv in a.tune)
     instance = sc.kernel_name()
     tr = load_traffic(Path(a.traffic_file), a.config, instance)
     roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": instance,
-            "kernel_ms": round(kernel_ms, 4), "note": "kernel_ms: the frame's four launches, HIP events around them"}
-    hw1_kernels = ("hw1_rect_count_kernel", "hw1_scan_kernel", "hw1_fill_kernel", "render_hw1_binned_kernel")
+            "kernel_ms": round(kernel_ms, 4), "note": "kernel_ms: the frame's five launches, HIP events around them"}
+    hw1_kernels = ("hw1_rect_count_kernel", "hw1_scan_chunks_kernel", "hw1_fill_kernel", "render_hw1_chunks_kernel", "hw1_resolve_kernel")
     per = (tr or {}).get("per_kernel") or {}
     if tr and all(k in per for k in hw1_kernels):
-        # the frame's four launches (the live kernel_ms spans them): their measured bytes summed
+        # the frame's five launches (the live kernel_ms spans them): their measured bytes summed
         frame_bytes = sum(per[k]["bytes_per_launch"] for k in hw1_kernels)
         ach = frame_bytes / (kernel_ms / 1e3) / 1e9
         roof.update(traffic=frame_bytes, achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
-                    achieved_from=f"measured HBM bytes of the frame's four kernels (rocprofv3 --pmc, "
+                    achieved_from=f"measured HBM bytes of the frame's five kernels (rocprofv3 --pmc, "
                                   f"{tr.get('source', '?')}) / live kernel_ms",
                     per_kernel={k: per[k] for k in hw1_kernels})
         for k in ("issue", "binding"):

@@ -2537,6 +2537,13 @@ struct Hw1Params {
     uint8_t* __restrict__ p6;         // optional: write_p6-default samples (W*H*3 bytes)
     uint32_t list_cap;                // binned path: entries bin_list holds; a tile whose list would
                                       // reach past it takes the brute-force loop (exact, slower)
+    // chunked path (rt_render_hw1_device): work items of at most HW1_CHUNK list entries
+    const uint32_t* __restrict__ chunk_tile;   // per chunk: its tile
+    const uint32_t* __restrict__ chunk_first;  // per tile: its first chunk (exclusive prefix; [ntiles] = total)
+    uint32_t chunk_cap;                         // chunk_tile's entries
+    unsigned long long* __restrict__ keys;      // per (pixel, sample): min over chunks of (t bits << 32 | index)
+    uint32_t* __restrict__ zero_counts;         // resolve: counts + cursor (2 * ntiles) zeroed for the next frame
+    int32_t ntiles;
 };
 
 // HW1 shade (HW1/include/raytracer.h:21-48), material hard-coded at ray.h:111-114.
@@ -2651,7 +2658,6 @@ __global__ __launch_bounds__(BLOCK) void render_hw1_kernel(Hw1Params P) {
 // a half-plane in (ix, iy); the rectangle is the bounding box (+1 pixel) of the padded image
 // rectangle clipped by the four half-planes.  Degenerate cases (tiny tnum, huge magnitudes,
 // an image whose directions reach 0) get the whole image.
-constexpr int HW1_TILE = 16;
 __device__ __forceinline__ void hw1_cross_d(const double a[3], const double b[3], double r[3]) {
     r[0] = a[1] * b[2] - a[2] * b[1];
     r[1] = a[2] * b[0] - a[0] * b[2];
@@ -2795,7 +2801,7 @@ __device__ int4 hw1_rect(const Hw1Params& P, int k) {
 
 // Binning (a tiled rasterizer's): hw1_rect_count_kernel counts, per 16x4-pixel wave tile, the
 // triangles whose rectangle meets the tile's (ix, iy) range (pixel x uses ix in {x, x+1});
-// hw1_scan_kernel turns the counts into offsets; hw1_fill_kernel writes the lists.  A list's
+// hw1_scan_chunks_kernel turns the counts into offsets; hw1_fill_kernel writes the lists.  A list's
 // order is whatever the atomics give, so the render kernel keeps the lexicographic minimum of
 // (t, index): the smallest t, the smallest index among equal t — exactly the brute-force
 // loop's winner (it keeps the first index whose t is strictly below every earlier one), and
@@ -2842,11 +2848,20 @@ __global__ __launch_bounds__(BLOCK) void hw1_fill_kernel(Hw1Params P, uint32_t* 
         }
 }
 
+// The chunked pass: a tile's list is cut into work items of at most HW1_CHUNK entries (a tile
+// whose list does not fit the capacity is one item over every triangle), so a long list no
+// longer makes one wave the kernel's tail.
+constexpr uint32_t HW1_CHUNK = 64;
+
 // Exclusive prefix sum of n counts in one workgroup (n is the number of wave tiles, small);
-// offsets[n] = total.
-__global__ __launch_bounds__(1024) void hw1_scan_kernel(const uint32_t* __restrict__ counts, uint32_t* __restrict__ offsets,
-                                                        int n) {
-    __shared__ uint32_t part[1024];
+// offsets[n] = total.  With chunk_first: the same over the tiles' chunk counts, and every
+// chunk's tile in chunk_tile (at most chunk_cap; chunks past it are not written, the total in
+// chunk_first[n] says how many there were).
+__global__ __launch_bounds__(1024) void hw1_scan_chunks_kernel(const uint32_t* __restrict__ counts,
+                                                               uint32_t* __restrict__ offsets, int n, uint32_t list_cap,
+                                                               uint32_t* __restrict__ chunk_first,
+                                                               uint32_t* __restrict__ chunk_tile, uint32_t chunk_cap) {
+    __shared__ uint32_t part[1024], cpart[1024];
     const int t = (int)threadIdx.x;
     const int per = (n + 1023) / 1024;
     const int lo = min(n, t * per), hi = min(n, lo + per);
@@ -2860,78 +2875,128 @@ __global__ __launch_bounds__(1024) void hw1_scan_kernel(const uint32_t* __restri
         part[t] += v;
         __syncthreads();
     }
-    uint32_t run = part[t] - sum;
+    // the tiles' chunk counts need the tiles' offsets (a list past the capacity: one chunk)
+    uint32_t run = part[t] - sum, csum = 0;
     for (int i = lo; i < hi; ++i) {
         offsets[i] = run;
-        run += counts[i];
+        const uint32_t c = counts[i];
+        csum += run + c > list_cap ? 1u : (c + HW1_CHUNK - 1) / HW1_CHUNK;
+        run += c;
     }
     if (t == 1023) offsets[n] = part[1023];
+    cpart[t] = csum;
+    __syncthreads();
+    for (int st = 1; st < 1024; st <<= 1) {
+        const uint32_t v = t >= st ? cpart[t - st] : 0u;
+        __syncthreads();
+        cpart[t] += v;
+        __syncthreads();
+    }
+    uint32_t crun = cpart[t] - csum;
+    run = part[t] - sum;
+    for (int i = lo; i < hi; ++i) {
+        chunk_first[i] = crun;
+        const uint32_t c = counts[i];
+        const uint32_t nc = run + c > list_cap ? 1u : (c + HW1_CHUNK - 1) / HW1_CHUNK;
+        for (uint32_t k = 0; k < nc; ++k)
+            if (crun + k < chunk_cap) chunk_tile[crun + k] = (uint32_t)i;
+        crun += nc;
+        run += c;
+    }
+    if (t == 1023) chunk_first[n] = cpart[1023];
 }
 
-// One 16x16-pixel block per workgroup, one 16x4-pixel tile (and list) per wave; every pixel
-// lane runs mt_hw1 over the tile's list (wave-uniform triangle: scalar loads).
-__global__ __launch_bounds__(BLOCK) void render_hw1_binned_kernel(Hw1Params P) {
-    const int blocks_x = (P.W + HW1_TILE - 1) / HW1_TILE;
+// One wave per chunk, grid-stride over the frame's chunks: the tile's 64 pixel lanes run mt_hw1
+// over the chunk's entries and fold each sample's winner into keys with a 64-bit atomicMin of
+// (t bits << 32 | index).  t >= 0 and never -0 (t + 0.0f), so its bits order like its value; the
+// minimum over the chunks is the lexicographic (t, index) minimum of the whole list -- the
+// brute-force loop's winner (rec.t < prev.t keeps the first index).
+__global__ __launch_bounds__(BLOCK) void render_hw1_chunks_kernel(Hw1Params P) {
+    const uint32_t total = uni(P.chunk_first[P.ntiles]);
+    const uint32_t nchunks = total < P.chunk_cap ? total : P.chunk_cap;
     const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
-    const int wave = (int)threadIdx.x / 64;
     const uint32_t lane = lane_id();
-    const int tx = (int)blockIdx.x % blocks_x, ty = ((int)blockIdx.x / blocks_x) * (HW1_TILE / HW1_TH) + wave;
-    const int x = tx * HW1_TW + (int)(lane % HW1_TW);
-    const int y = ty * HW1_TH + (int)(lane / HW1_TW);
-    const bool valid = x < P.W && y < P.H;
-    const bool tile_ok = ty * HW1_TH < P.H;  // wave-uniform
-    const int tidx = ty * tiles_x + tx;
-    uint32_t cnt = tile_ok ? uni(P.bin_count[tidx]) : 0u;
-    const uint32_t off = tile_ok ? uni(P.bin_offset[tidx]) : 0u;
-    // a list past the capacity was not written: every triangle, in index order (a list "of any
-    // order" whose entries are the indices themselves)
-    const bool all = tile_ok && off + cnt > P.list_cap;
-    if (all) cnt = (uint32_t)P.num_tris;
+    const uint32_t waves = gridDim.x * (BLOCK / 64);
+    for (uint32_t j = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64; j < nchunks; j += waves) {
+        const uint32_t tidx = uni(P.chunk_tile[uni(j)]);
+        const uint32_t c = j - uni(P.chunk_first[tidx]);
+        const uint32_t cnt = uni(P.bin_count[tidx]);
+        const uint32_t off = uni(P.bin_offset[tidx]);
+        const bool all = off + cnt > P.list_cap;  // the list was not written: every triangle, in order
+        const uint32_t b = all ? 0u : c * HW1_CHUNK;
+        const uint32_t e = all ? (uint32_t)P.num_tris : min(cnt, b + HW1_CHUNK);
+        const int x = (int)(tidx % tiles_x) * HW1_TW + (int)(lane % HW1_TW);
+        const int y = (int)(tidx / tiles_x) * HW1_TH + (int)(lane / HW1_TW);
+        const bool valid = x < P.W && y < P.H;
+        for (int s = 0; s < P.spp; ++s) {
+            const float pxs = (float)x + P.jitter[2 * s];
+            const float pys = (float)y + P.jitter[2 * s + 1];
+            const int ix = (int)pxs, iy = (int)pys;  // get_pixel_position(int, int) truncates
+            const f3 pix = add(add(P.p00, scale(P.du, (float)ix)), scale(P.dv, (float)iy));
+            const f3 d = unit(sub(pix, P.center));  // HW1 Ray normalises (ray.h:25)
+            const f3 o = P.center;
+            unsigned long long best = ~0ull;
+            for (uint32_t i = b; i < e; i += 4) {
+                int kk[4];
+                float4 tq[12];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    kk[q] = i + q < e ? (all ? (int)(i + q) : (int)ldc_u32(P.bin_list + off + i + q)) : -1;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4* T = P.tri + 3 * (size_t)(kk[q] < 0 ? kk[0] : kk[q]);
+                    tq[3 * q] = ldc(T);
+                    tq[3 * q + 1] = ldc(T + 1);
+                    tq[3 * q + 2] = ldc(T + 2);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 a = tq[3 * q], bq = tq[3 * q + 1], cq = tq[3 * q + 2];
+                    float t, u, v;
+                    // (t < FLT_MAX: the loop's `t < best` from best = FLT_MAX never takes FLT_MAX,
+                    // +inf or NaN)
+                    if (valid && kk[q] >= 0 &&
+                        mt_hw1(o, d, mk(a.x, a.y, a.z), mk(bq.x, bq.y, bq.z), mk(cq.x, cq.y, cq.z), t, u, v) &&
+                        t < FLT_MAX) {
+                        const unsigned long long key =
+                            (unsigned long long)__float_as_uint(t + 0.0f) << 32 | (uint32_t)kk[q];
+                        best = key < best ? key : best;
+                    }
+                }
+            }
+            if (valid && best != ~0ull) atomicMin(&P.keys[((size_t)y * P.W + x) * (size_t)P.spp + (size_t)s], best);
+        }
+    }
+}
+
+// Per pixel: each sample's winner from keys (then reset for the next frame), HW1 shade, the
+// average, AOVs; the first threads also zero the bin counters for the next frame.
+__global__ __launch_bounds__(BLOCK) void hw1_resolve_kernel(Hw1Params P) {
+    const int gid = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    if (gid < 2 * P.ntiles) P.zero_counts[gid] = 0u;
+    if (gid >= P.W * P.H) return;
+    const int x = gid % P.W, y = gid / P.W;
     f3 acc = mk(0.f, 0.f, 0.f);
     for (int s = 0; s < P.spp; ++s) {
         const float pxs = (float)x + P.jitter[2 * s];
         const float pys = (float)y + P.jitter[2 * s + 1];
-        const int ix = (int)pxs, iy = (int)pys;  // get_pixel_position(int, int) truncates
+        const int ix = (int)pxs, iy = (int)pys;
         const f3 pix = add(add(P.p00, scale(P.du, (float)ix)), scale(P.dv, (float)iy));
-        const f3 d = unit(sub(pix, P.center));  // HW1 Ray normalises (ray.h:25)
+        const f3 d = unit(sub(pix, P.center));
         const f3 o = P.center;
-        float best = FLT_MAX;
-        int32_t besti = -1;
-        // Four list entries per round trip: their indices, then their twelve 16-byte records are
-        // all in flight before the first test (the list order does not matter, see above).
-        for (uint32_t i = 0; i < cnt; i += 4) {
-            int kk[4];
-            float4 tq[12];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                kk[j] = i + j < cnt ? (all ? (int)(i + j) : (int)ldc_u32(P.bin_list + off + i + j)) : -1;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float4* T = P.tri + 3 * (size_t)(kk[j] < 0 ? kk[0] : kk[j]);
-                tq[3 * j] = ldc(T);
-                tq[3 * j + 1] = ldc(T + 1);
-                tq[3 * j + 2] = ldc(T + 2);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float4 a = tq[3 * j], b = tq[3 * j + 1], cq = tq[3 * j + 2];
-                float t, u, v;
-                if (valid && kk[j] >= 0 &&
-                    mt_hw1(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(cq.x, cq.y, cq.z), t, u, v)) {
-                    if (t < best || (t == best && kk[j] < besti)) {  // lexicographic (t, index)
-                        best = t;
-                        besti = kk[j];
-                    }
-                }
-            }
-        }
+        const size_t kk = (size_t)gid * (size_t)P.spp + (size_t)s;
+        const unsigned long long key = P.keys[kk];
+        P.keys[kk] = ~0ull;
+        const bool hit = key != ~0ull;
+        const int32_t besti = hit ? (int32_t)(uint32_t)key : -1;
         f3 p = mk(0.f, 0.f, 0.f), n = p;
-        const bool hit = besti >= 0;
-        if (hit) {
+        float best = FLT_MAX;
+        if (hit) {  // the accepting test's own t, u, v
             const float4* T = P.tri + 3 * (size_t)besti;
             const float4 a = T[0], b = T[1], cq = T[2];
             float t, u, v;
             mt_hw1(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(cq.x, cq.y, cq.z), t, u, v);
+            best = t;
             p = add(o, scale(d, t));
             const float4* N = P.nrm + 3 * (size_t)besti;
             const float wgt = 1.0f - u - v;
@@ -2939,13 +3004,12 @@ __global__ __launch_bounds__(BLOCK) void render_hw1_binned_kernel(Hw1Params P) {
                     scale(mk(N[2].x, N[2].y, N[2].z), v));
         }
         acc = add(acc, shade_hw1(o, d, hit, p, n, P.lpos, P.lcol));
-        if (valid && P.hit_idx) {
-            const size_t kk = ((size_t)y * P.W + x) * (size_t)P.spp + (size_t)s;
+        if (P.hit_idx) {
             P.hit_idx[kk] = besti;
             P.hit_t[kk] = hit ? best : -1.0f;
         }
     }
-    if (valid) hw1_write_pixel(P, x, y, acc);
+    hw1_write_pixel(P, x, y, acc);
 }
 
 __global__ __launch_bounds__(BLOCK) void powf_kernel(const float* __restrict__ x, const float* __restrict__ y, int n,
@@ -4219,14 +4283,18 @@ struct rt_hw1_scene {
     int device = 0;
     size_t P = 0;
     DevBuf tri, nrm, rects, bins, list, jitter;
+    DevBuf chunks;             // chunk_first (ntiles + 1) | chunk_tile (chunk_cap)
+    DevBuf keys;               // per (pixel, sample): the chunked pass's winners, kept at ~0 between frames
     int bins_tiles = -1;       // tiles the bins buffer is laid out for
-    uint32_t list_cap = 0;
+    size_t keys_n = 0;         // samples the keys buffer holds
+    uint32_t list_cap = 0, chunk_cap = 0;
     int jitter_spp = -1;
     std::vector<float> jitter_host;
     static constexpr int kRing = 64;
     hipEvent_t e0[kRing] = {}, e1[kRing] = {};
     uint32_t* total_host = nullptr;  // pinned: the list total of frame f at [f % kRing]
     uint64_t frames = 0;
+    hipStream_t last_stream = nullptr;
     const char* last_kernel = "";
     ~rt_hw1_scene() {
         for (int i = 0; i < kRing; ++i) {
@@ -4318,14 +4386,25 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
             HIP_TRY(hipEventSynchronize(s->e1[(s->frames - 1) % rt_hw1_scene::kRing]));
             s->list_cap = uint32_t(std::min<uint64_t>(uint64_t(tot) + tot / 4 + 1024, 0x7FFFFFFFull));
             if ((rc = s->list.alloc(size_t(s->list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
+            s->bins_tiles = -1;  // the chunk table follows the list's capacity
         }
         break;
     }
     (void)hipGetLastError();  // a not-ready query is not an error of this call
-    if (!brute && s->bins_tiles != ntiles) {
+    const size_t nsamples = size_t(W) * size_t(H) * size_t(spp);
+    if (!brute && (s->bins_tiles != ntiles || s->keys_n != nsamples)) {
         if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->e1[(s->frames - 1) % rt_hw1_scene::kRing]));
+        // counts | cursor | offsets (ntiles + 1): counts and cursor zeroed here, then by every
+        // frame's resolve pass for the next
         if ((rc = s->bins.alloc(size_t(3 * ntiles + 1) * sizeof(uint32_t))) != RT_OK) return rc;
+        HIP_TRY(hipMemset(s->bins.p, 0, size_t(2 * ntiles) * sizeof(uint32_t)));
+        // chunks: at most one per HW1_CHUNK listed entries plus one per tile
+        s->chunk_cap = uint32_t(std::min<uint64_t>(uint64_t(s->list_cap) / HW1_CHUNK + uint64_t(ntiles) + 1, 0x7FFFFFFFull));
+        if ((rc = s->chunks.alloc((size_t(ntiles) + 1 + s->chunk_cap) * sizeof(uint32_t))) != RT_OK) return rc;
+        if ((rc = s->keys.alloc(nsamples * sizeof(unsigned long long))) != RT_OK) return rc;
+        HIP_TRY(hipMemset(s->keys.p, 0xFF, nsamples * sizeof(unsigned long long)));
         s->bins_tiles = ntiles;
+        s->keys_n = nsamples;
     }
     Hw1Params hp;
     hp.tri = static_cast<const float4*>(s->tri.p);
@@ -4348,26 +4427,44 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
     hp.rects = static_cast<const int4*>(s->rects.p);
     hp.bin_count = hp.bin_offset = hp.bin_list = nullptr;
     hp.list_cap = s->list_cap;
+    hp.chunk_first = hp.chunk_tile = nullptr;
+    hp.chunk_cap = s->chunk_cap;
+    hp.keys = static_cast<unsigned long long*>(s->keys.p);
+    hp.zero_counts = static_cast<uint32_t*>(s->bins.p);
+    hp.ntiles = ntiles;
     const int sl = int(s->frames % rt_hw1_scene::kRing);
+    // the scene's buffers are shared by its frames: a frame on another stream waits for the last
+    if (s->frames > 0 && st != s->last_stream)
+        HIP_TRY(hipStreamWaitEvent(st, s->e1[(s->frames - 1) % rt_hw1_scene::kRing], 0));
+    s->last_stream = st;
     HIP_TRY(hipEventRecord(s->e0[sl], st));
     const int blocks = ((W + 15) / 16) * ((H + 15) / 16);
     if (brute) {
         hipLaunchKernelGGL(render_hw1_kernel, dim3(blocks), dim3(BLOCK), 0, st, hp);
         s->last_kernel = "render_hw1_kernel";
     } else {
-        const dim3 tgrid(unsigned((s->P + BLOCK - 1) / BLOCK));
-        uint32_t* counts = static_cast<uint32_t*>(s->bins.p);
+        // one wave per 64 triangles (a block each): the per-triangle passes spread over every CU
+        // (256-thread blocks kept c2's 19,858 triangles on 78 CUs: 30 + 25 us)
+        const dim3 tgrid(unsigned((s->P + 63) / 64));
+        uint32_t* counts = static_cast<uint32_t*>(s->bins.p);  // zeroed by the previous frame's resolve
         uint32_t* cursor = counts + ntiles;
         uint32_t* offsets = cursor + ntiles;  // ntiles + 1 entries
-        HIP_TRY(hipMemsetAsync(counts, 0, size_t(2 * ntiles) * sizeof(uint32_t), st));
-        hipLaunchKernelGGL(hw1_rect_count_kernel, tgrid, dim3(BLOCK), 0, st, hp, static_cast<int4*>(s->rects.p), counts);
-        hipLaunchKernelGGL(hw1_scan_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, ntiles);
+        uint32_t* cfirst = static_cast<uint32_t*>(s->chunks.p);
+        uint32_t* ctile = cfirst + ntiles + 1;
+        hipLaunchKernelGGL(hw1_rect_count_kernel, tgrid, dim3(64), 0, st, hp, static_cast<int4*>(s->rects.p), counts);
+        hipLaunchKernelGGL(hw1_scan_chunks_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, ntiles, s->list_cap,
+                           cfirst, ctile, s->chunk_cap);
         hp.bin_count = counts;
         hp.bin_offset = offsets;
         hp.bin_list = static_cast<const uint32_t*>(s->list.p);
-        hipLaunchKernelGGL(hw1_fill_kernel, tgrid, dim3(BLOCK), 0, st, hp, cursor, static_cast<uint32_t*>(s->list.p));
-        hipLaunchKernelGGL(render_hw1_binned_kernel, dim3(blocks), dim3(BLOCK), 0, st, hp);
-        s->last_kernel = "render_hw1_binned_kernel";
+        hp.chunk_first = cfirst;
+        hp.chunk_tile = ctile;
+        hipLaunchKernelGGL(hw1_fill_kernel, tgrid, dim3(64), 0, st, hp, cursor, static_cast<uint32_t*>(s->list.p));
+        // chunks grid-stride over a grid of every CU's worth of waves (the count is on the device)
+        hipLaunchKernelGGL(render_hw1_chunks_kernel, dim3(1024), dim3(BLOCK), 0, st, hp);
+        const int rgrid = (std::max(W * H, 2 * ntiles) + BLOCK - 1) / BLOCK;
+        hipLaunchKernelGGL(hw1_resolve_kernel, dim3(rgrid), dim3(BLOCK), 0, st, hp);
+        s->last_kernel = "render_hw1_chunks_kernel";
         HIP_TRY(hipGetLastError());
         // this frame's total, for the capacity of the next ones
         HIP_TRY(hipMemcpyAsync(s->total_host + sl, offsets + ntiles, sizeof(uint32_t), hipMemcpyDeviceToHost, st));

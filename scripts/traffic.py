@@ -29,8 +29,8 @@ a = ap.parse_args()
 
 def short(name):
     for k in ("render_tiles_kernel", "render_samples_kernel", "tile_cull_kernel", "tile_cut_kernel",
-              "render_hw1_kernel", "render_hw1_binned_kernel", "hw1_rect_count_kernel", "hw1_scan_kernel",
-              "hw1_fill_kernel", "copyBuffer", "fillBuffer", "elementwise"):
+              "render_hw1_kernel", "render_hw1_chunks_kernel", "hw1_rect_count_kernel", "hw1_scan_chunks_kernel",
+              "hw1_fill_kernel", "hw1_resolve_kernel", "copyBuffer", "fillBuffer", "elementwise"):
         if k in name:
             return k
     return name[:40]
@@ -139,7 +139,7 @@ if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
                       "fetch_bytes": round(fetch), "write_bytes": round(write),
                       "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
                                 f"{os.path.basename(a.prof.rstrip('/'))}; FETCH_SIZE x2 (gfx950), KiB->B"}
-    # every kernel of the profiled frames (the HW1 path's frame is four launches)
+    # every kernel of the profiled frames (the HW1 path's frame is five launches)
     data[a.config]["per_kernel"] = {
         kn: {"bytes_per_launch": round(2 * cs["FETCH_SIZE"] * 1024 + cs["WRITE_SIZE"] * 1024)}
         for kn, cs in summary.items() if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs}

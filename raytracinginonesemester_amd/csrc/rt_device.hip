@@ -671,12 +671,33 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
             const uint32_t slot = ref & ~LEAF_BIT;
             const float4* L = reinterpret_cast<const float4*>(leaf_b + (slot << 6));
             const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2), d = ldc(L + 3);
+            bool skip = false;
+#ifdef RT_LEAF_FAMILY
+            // The leaf's box passed the family test when it was pushed; once some lane has a hit
+            // (tmax_w < FLT_MAX) the same test with today's tmax_w may fail, and then no lane's
+            // exact pop-time test passes either (the family test is conservative): skip the
+            // triangle test.
+            if (tmax_w < FLT_MAX) {
+                const v2f lb[3] = {hi2(c), lo2(d), hi2(d)};
+                float ln = -INFINITY, lf = INFINITY;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const v2f db = lb[q] - (v2f){o[q], o[q]};
+                    const v2f p = (v2f){db.x, db.x} * U[q], pq = (v2f){db.y, db.y} * U[q];
+                    ln = fmaxf(ln, fminf(fminf(p.x, p.y), fminf(pq.x, pq.y)));
+                    lf = fminf(lf, fmaxf(fmaxf(p.x, p.y), fmaxf(pq.x, pq.y)));
+                }
+                ln = __builtin_fmaf(fabsf(ln), -kW, ln);
+                lf = __builtin_fmaf(fabsf(lf), kW, lf);
+                skip = !(fmaxf(ln, kRayTMin) <= fminf(lf, tmax_w));
+            }
+#endif
             // Moller-Trumbore first, for every live lane; the leaf's pop-time box test (which the
             // reference makes before it) only for lanes whose triangle test would change their
             // state: the same outcome, and most leaf pops change no lane's bestT
             float t, u, v;
-            const bool hm = live && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y), kRayTMin,
-                                         hs.bestT, t, u, v);
+            const bool hm = !skip && live && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y),
+                                                  kRayTMin, hs.bestT, t, u, v);
             const uint64_t mh = ballot(hm);
             if (mh != 0) {
                 RT_STAT(4, 1);

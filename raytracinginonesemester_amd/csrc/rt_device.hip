@@ -69,6 +69,9 @@ constexpr int MODE_DEEP = 64;
 // The depth-1 kernels' one-light form: the scene has exactly one light, so shade_d1 has no light
 // loop (whose loop-carried values spilled in the big-scene 8-wave build).
 constexpr int MODE_1L = 128;
+// The big-scene kernels' frustum traversal over the quantised records (qent/qhdr: 16 B per entry
+// instead of 32; build_quant_records)
+constexpr int MODE_QR = 256;
 constexpr int REF_STACK = 512;                // query.h:245
 constexpr uint32_t INV_LEAF = 0xFFFFFFFEu;    // deep stack entry: a leaf naming no triangle (query.h:263)
 constexpr uint32_t BRUTE_BIT = 0x40000000u;   // HitState::slot of a brute-force hit: BRUTE_BIT | triangle
@@ -88,6 +91,8 @@ struct SceneView {
     const float4* __restrict__ wnode;  // 4-ary records (8 x float4) by internal index, if wide
     const float* __restrict__ fnode;   // 2^f_log2-ary records (8 x 2^f_log2 floats) of traverse_frustum, or null
     int32_t f_log2;                    // 3..5 with fnode; 2: traverse_frustum takes wnode
+    const uint4* __restrict__ qent;    // fnode's records quantised (MODE_QR kernels): 2^f_log2 x 16 B each
+    const float4* __restrict__ qhdr;   // their grids: (origin xyz, step x | step yz, -, -) per record
     const float4* __restrict__ ibox;
     const float4* __restrict__ rootb;  // the root's box, pairs (x | y, z), after ibox's entries
     const float4* __restrict__ leaf;
@@ -605,7 +610,7 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
 //   entries take the 4-ary records the same way.
 // Scenes whose coordinates come within 1e30 of the float range give no bound on those axes
 // (products stay finite: |b - o| < 1e30, |1/d| <= 1e8).
-template <bool PK = false, bool XL = false>
+template <bool PK = false, bool XL = false, bool QR = false>
 __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayPre& r, bool active, HitState& hs) {
     hs.bestT = FLT_MAX;
     hs.slot = -1;
@@ -712,10 +717,31 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
             }
         } else {
             RT_STAT(8, 1);
-            const float* W = reinterpret_cast<const float*>(rec_b + ((size_t)ref << rec_shift));
-            const v2f* B = reinterpret_cast<const v2f*>(W + k6);
-            const v2f bb[3] = {B[0], B[1], B[2]};
-            const uint32_t rk = reinterpret_cast<const uint32_t*>(W)[kref];
+            v2f bb[3];
+            uint32_t rk;
+            if constexpr (QR) {
+                // entry k: (x lo | x hi, y lo | y hi, z lo | z hi) 16-bit grid steps and the ref, one
+                // 16 B load; the record's grid (scalar loads) maps step q to fma(q, step, origin),
+                // which the host checked lies at or below the entry's min (lo) and at or above its
+                // max (hi): a box containing the entry's own, so the family test stays conservative
+                const vf4 g0 = ldc_v(sc.qhdr + 2 * ref), g1 = ldc_v(sc.qhdr + 2 * ref + 1);
+                const uint4 e = sc.qent[((size_t)ref << lg) + kl];
+                const float og[3] = {g0.x, g0.y, g0.z}, st[3] = {g0.w, g1.x, g1.y};
+                const uint32_t qw[3] = {e.x, e.y, e.z};
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const v2f q = {(float)(qw[a] & 0xFFFFu), (float)(qw[a] >> 16)};
+                    bb[a] = __builtin_elementwise_fma(q, (v2f){st[a], st[a]}, (v2f){og[a], og[a]});
+                }
+                rk = e.w;
+            } else {
+                const float* W = reinterpret_cast<const float*>(rec_b + ((size_t)ref << rec_shift));
+                const v2f* B = reinterpret_cast<const v2f*>(W + k6);
+                bb[0] = B[0];
+                bb[1] = B[1];
+                bb[2] = B[2];
+                rk = reinterpret_cast<const uint32_t*>(W)[kref];
+            }
             float nr[3], fr[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
@@ -1058,7 +1084,8 @@ template <int MODE>
 __device__ __forceinline__ void traverse_camera(const SceneView& sc, const RayPre& r, bool active, HitState& hs) {
 #ifndef RT_NO_FRUSTUM
     if constexpr (MODE != RT_KERNEL_LANE && (MODE & MODE_DEEP) == 0 && (MODE & MODE_WIDE) != 0) {
-        traverse_frustum<(MODE & MODE_PK) != 0, (MODE & MODE_PK) != 0 && (MODE & MODE_1L) == 0>(sc, r, active, hs);
+        traverse_frustum<(MODE & MODE_PK) != 0, (MODE & MODE_PK) != 0 && (MODE & MODE_1L) == 0, (MODE & MODE_QR) != 0>(
+            sc, r, active, hs);
         return;
     }
 #endif
@@ -3082,6 +3109,7 @@ struct rt_scene {
     DevBuf fnode;    // 2^f_log2-ary records of the frustum traversal (empty: it takes wnode's 4-ary ones)
     int f_log2 = 2;
     int f_bound = 0;  // their DFS stack bound (<= FRUSTUM_STACK unless RT_TUNE_FRUSTUM_STACK_CAP raised it)
+    DevBuf qent, qhdr;  // fnode quantised (build_quant_records): the big-scene kernels' records
     DevBuf fault;     // one word: RT_FAULT_* bits the kernels OR in (rt_scene_faults)
     DevBuf cut;  // tile culling: boxes of a cut of the tree (6 floats each)
     int ncut = 0;
@@ -3247,6 +3275,62 @@ static FrustumRecords build_frustum_records(const rt_bvh_node* nodes, size_t NN,
         return out;
     }
     return out;
+}
+
+// The frustum records quantised (MODE_QR kernels: the big scenes, whose 1 KB records do not stay
+// in the L2s): per record a grid over the union of its entries' boxes, origin o = the union's
+// min and per axis a step h >= extent / 65534; entry bounds become 16-bit steps q_lo = the
+// largest q with fma(q, h, o) <= min and q_hi = the smallest with fma(q, h, o) >= max, evaluated
+// in float as the kernel does (fmaf, one rounding), so the dequantised box contains the entry's.
+// The family test only decides what is pushed (leaves are tested exactly at pop), so looser
+// boxes cost pops, never a different hit.  qent: A x (x lo | x hi << 16, y, z, ref) per record;
+// qhdr: (o.x, o.y, o.z, h.x), (h.y, h.z, 0, 0).  False (no quantised records) when a bound is not
+// finite, an extent exceeds 1e30 or a step would be subnormal.
+static bool build_quant_records(const FrustumRecords& fr, std::vector<uint32_t>& qent, std::vector<float>& qhdr) {
+    const int A = 1 << fr.log2;
+    qent.assign(size_t(4 * A) * fr.nrec, 0u);
+    qhdr.assign(size_t(8) * fr.nrec, 0.f);
+    for (size_t r = 0; r < fr.nrec; ++r) {
+        const float* w = &fr.rec[size_t(8 * A) * r];
+        uint32_t* qe = &qent[size_t(4 * A) * r];
+        float* qh = &qhdr[8 * r];
+        for (int a = 0; a < 3; ++a) {
+            float lo = INFINITY, hi = -INFINITY;
+            for (int i = 0; i < A; ++i) {
+                uint32_t ref;
+                std::memcpy(&ref, &w[6 * A + i], 4);
+                if (ref == NO_REF) continue;
+                lo = std::min(lo, w[6 * i + 2 * a]);
+                hi = std::max(hi, w[6 * i + 2 * a + 1]);
+            }
+            if (lo > hi) lo = hi = 0.f;  // a record without entries (not built, kept total)
+            if (!std::isfinite(lo) || !std::isfinite(hi) || double(hi) - double(lo) > 1e30) return false;
+            float h = float((double(hi) - double(lo)) / 65534.0);
+            if (double(h) * 65534.0 < double(hi) - double(lo)) h = std::nextafter(h, INFINITY);
+            if (h != 0.f && !(h >= 1e-30f)) return false;
+            (a == 0 ? qh[3] : qh[3 + a]) = h;
+            qh[a] = lo;
+            for (int i = 0; i < A; ++i) {
+                uint32_t ref;
+                std::memcpy(&ref, &w[6 * A + i], 4);
+                if (ref == NO_REF) continue;
+                const float mn = w[6 * i + 2 * a], mx = w[6 * i + 2 * a + 1];
+                uint32_t ql = 0, qh16 = 0;
+                if (h > 0.f) {
+                    double fl = std::floor((double(mn) - double(lo)) / double(h));
+                    double fh = std::ceil((double(mx) - double(lo)) / double(h));
+                    ql = uint32_t(std::clamp(fl, 0.0, 65535.0));
+                    qh16 = uint32_t(std::clamp(fh, 0.0, 65535.0));
+                    while (ql > 0 && std::fmaf(float(ql), h, lo) > mn) --ql;
+                    while (qh16 < 65535 && std::fmaf(float(qh16), h, lo) < mx) ++qh16;
+                }
+                if (std::fmaf(float(ql), h, lo) > mn || std::fmaf(float(qh16), h, lo) < mx) return false;
+                qe[4 * i + a] = ql | (qh16 << 16);
+            }
+        }
+        for (int i = 0; i < A; ++i) std::memcpy(&qe[4 * i + 3], &w[6 * A + i], 4);
+    }
+    return true;
 }
 
 // Host-only view of build_frustum_records for the CPU tests (no device), with the ids as
@@ -3525,6 +3609,18 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
             if ((rc = s->fnode.upload(fr.rec.data(), fr.rec.size() * sizeof(float))) != RT_OK) return rc;
             s->f_log2 = fr.log2;
             s->f_bound = fr.bound;
+            // RT_TUNE_QUANT_RECORDS: 1 quantised records for every scene with frustum records,
+            // 0 none, else (default) for scenes whose float records alone exceed the big-scene
+            // threshold's eighth (c5: 34 MB; frog: 0.6 MB)
+            const double qk = rt::tuning(RT_TUNE_QUANT_RECORDS, -1.0);
+            const double big = rt::tuning(RT_TUNE_BIG_SCENE_BYTES, double(kBigSceneBytes));
+            const bool want_q = qk > 0.5 || (qk < -0.5 && double(fr.rec.size() * sizeof(float)) > big / 8.0);
+            std::vector<uint32_t> qe;
+            std::vector<float> qh;
+            if (want_q && build_quant_records(fr, qe, qh)) {
+                if ((rc = s->qent.upload(qe.data(), qe.size() * sizeof(uint32_t))) != RT_OK) return rc;
+                if ((rc = s->qhdr.upload(qh.data(), qh.size() * sizeof(float))) != RT_OK) return rc;
+            }
         }
     }
     s->wide = wide_ok && !(s->root_ref & LEAF_BIT);
@@ -3585,6 +3681,7 @@ extern "C" int rt_scene_clone(const rt_scene* src, int device, rt_scene** out) {
     // device-to-device copies of the packed arrays (over xGMI when the devices differ)
     const std::pair<DevBuf*, const DevBuf*> bufs[] = {{&s->inode, &src->inode}, {&s->wnode, &src->wnode},
                                                       {&s->fnode, &src->fnode},
+                                                      {&s->qent, &src->qent},   {&s->qhdr, &src->qhdr},
                                                       {&s->ibox, &src->ibox},   {&s->leaf, &src->leaf},
                                                       {&s->tnorm, &src->tnorm}, {&s->objids, &src->objids},
                                                       {&s->mats, &src->mats},   {&s->lights, &src->lights},
@@ -3676,6 +3773,7 @@ struct Launch {
     hipEvent_t start, stop;
     int cus;
     bool big;  // scene data beyond kBigSceneBytes: the depth-1 wave kernels at RT_RENDER_WAVES_BIG
+    bool qr;   // ... over the quantised frustum records (MODE_QR), which the scene has
     const char** name;  // out: the launched instantiation, as rocprofv3 names it (rt_scene_kernel_name)
 };
 template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0>
@@ -3708,6 +3806,14 @@ void launch_mode(const RenderParams& P, const Launch& L) {
         }
         if constexpr ((MODE & (MODE_DEEP | RT_KERNEL_LANE)) == 0) {
             if (L.big) {
+                if constexpr ((MODE & MODE_WIDE) != 0) {
+                    if (L.qr) {
+                        if (P.sc.num_lights == 1)
+                            launch_render<D1_MODE | MODE_1L | MODE_QR, SAMPLES, true, RT_RENDER_WAVES_BIG>(P, L);
+                        else launch_render<D1_MODE | MODE_QR, SAMPLES, true, RT_RENDER_WAVES_BIG>(P, L);
+                        return;
+                    }
+                }
                 if (P.sc.num_lights == 1) launch_render<D1_MODE | MODE_1L, SAMPLES, true, RT_RENDER_WAVES_BIG>(P, L);
                 else launch_render<D1_MODE, SAMPLES, true, RT_RENDER_WAVES_BIG>(P, L);
                 return;
@@ -3816,6 +3922,8 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     P.sc.wnode = static_cast<const float4*>(s->wnode.p);
     P.sc.fnode = static_cast<const float*>(s->fnode.p);
     P.sc.f_log2 = s->fnode.p ? s->f_log2 : 2;
+    P.sc.qent = static_cast<const uint4*>(s->qent.p);
+    P.sc.qhdr = static_cast<const float4*>(s->qhdr.p);
     P.sc.wide = s->wide && !(o->flags & RT_FLAG_BINARY) ? 1 : 0;
     P.sc.lane_stack = s->lane_stack ? 1 : 0;
     P.sc.lane_wide = s->lane_wide ? 1 : 0;
@@ -4049,7 +4157,8 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         }
         HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
         const size_t big_bytes = size_t(std::max(0.0, rt::tuning(RT_TUNE_BIG_SCENE_BYTES, double(kBigSceneBytes))));
-        const Launch L{st, s->evm[slot], s->ev1[slot], s->cus, s->bytes > big_bytes, &s->last_kernel};
+        const bool qr = P.sc.qent != nullptr && P.sc.f_log2 > 2;
+        const Launch L{st, s->evm[slot], s->ev1[slot], s->cus, s->bytes > big_bytes, qr, &s->last_kernel};
         if (s->deep) launch<MODE_DEEP>(P, samples, L);
         else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, L);
         else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, L);

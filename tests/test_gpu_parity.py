@@ -760,3 +760,54 @@ def test_frustum_stack_overflow_guard_is_loud(tune):
         ds.render(cam, spp=4, max_depth=1, flags=rt._lib.RT_FLAG_BINARY)
     finally:
         ds.close()
+
+
+@pytest.mark.parametrize("arity", [None, 4, 3])
+@pytest.mark.parametrize("name", ["c3_small", "sphere_single", "cornell", "c5_small"])
+def test_quantised_records_parity(name, arity, tune):
+    """The big-scene kernels' frustum traversal over the quantised records (16-bit grid steps,
+    build_quant_records), forced onto small scenes (RT_TUNE_QUANT_RECORDS = 1 and a zero
+    big-scene threshold): the reference's hits, t and frame bit for bit at every arity."""
+    tune(frustum_arity=arity, quant_records=1, big_scene_bytes=0)
+    meta = golden_meta(name)
+    if meta["max_depth"] != 1:
+        pytest.skip("the big-scene kernels are the depth-1 ones")
+    hs = host_scene(G_SCENES[name])
+    cam = hs.camera(meta["width"], meta["height"])
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    rgb, hi, ht = ds.render(cam, spp=meta["spp"], max_depth=1, miss_color=hexv(meta["miss_color"]), aov=True)
+    kn = ds.kernel_name()
+    assert kn.startswith("render_tiles_kernel<433,") or kn.startswith("render_tiles_kernel<305,"), kn
+    assert ds.faults() == 0
+    assert np.array_equal(hi.reshape(-1), golden_array(name, "hits.i32.gz", np.int32))
+    assert np.array_equal(ht.reshape(-1).view(np.uint32),
+                          golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
+    _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))
+
+
+@pytest.mark.parametrize("scene", ["frog.json", "cornell.json", "sphere_single.json"])
+def test_quantised_records_fuzz_cameras(scene, tune):
+    """Quantised records under the adversarial cameras (_fuzz_cameras): frames bit-identical to
+    the binary-record traversal."""
+    tune(quant_records=1, big_scene_bytes=0)
+    hs = host_scene(scene)
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    for k, cam in _fuzz_cameras(hs, np.random.default_rng(19), 24):
+        a = ds.render(cam, spp=4, max_depth=1, aov=True)
+        assert ",".join(ds.kernel_name().split(",")[:1]) in ("render_tiles_kernel<433", "render_tiles_kernel<305")
+        b = ds.render(cam, spp=4, max_depth=1, aov=True, flags=rt._lib.RT_FLAG_BINARY)
+        for x, y in zip(a, b):
+            assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), k
+    assert ds.faults() == 0
+
+
+def test_c5_takes_the_quantised_records():
+    """The shipped default: the c5 heightfield (34 MB of 32-ary float records) renders through
+    the quantised records' kernel; frog (0.6 MB) does not."""
+    ds = _device_scene("heightfield_c5.json")
+    hs = host_scene("heightfield_c5.json")
+    ds.render(hs.camera(64, 48), spp=1, max_depth=1)
+    assert ds.kernel_name().startswith("render_tiles_kernel<433,"), ds.kernel_name()
+    fr = _device_scene("frog.json")
+    fr.render(host_scene("frog.json").camera(64, 48), spp=1, max_depth=1)
+    assert not fr.kernel_name().startswith("render_tiles_kernel<433,"), fr.kernel_name()

@@ -501,8 +501,8 @@ typedef enum {
     RT_TUNE_COPY_ENGINE = 11,    /* rt_renderer's host delivery: -1 auto (SDMA where it applies: one rank,
                                     DIRECT, a host frame), 0 the HIP runtime's copies, 1 SDMA or fail */
     RT_TUNE_QUANT_RECORDS = 12,  /* quantised frustum records for the big-scene kernels, at scene creation:
-                                    -1 auto (default: scenes whose float records exceed 1/8 of
-                                    RT_TUNE_BIG_SCENE_BYTES), 0 never, 1 always */
+                                    0 never (default; measured slower on c5), -1 scenes whose float
+                                    records exceed 1/8 of RT_TUNE_BIG_SCENE_BYTES, 1 always */
     RT_TUNE_COUNT = 13
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */

@@ -676,32 +676,11 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
             const uint32_t slot = ref & ~LEAF_BIT;
             const float4* L = reinterpret_cast<const float4*>(leaf_b + (slot << 6));
             const float4 a = ldc(L), b = ldc(L + 1), c = ldc(L + 2), d = ldc(L + 3);
-            bool skip = false;
-#ifdef RT_LEAF_FAMILY
-            // The leaf's box passed the family test when it was pushed; once some lane has a hit
-            // (tmax_w < FLT_MAX) the same test with today's tmax_w may fail, and then no lane's
-            // exact pop-time test passes either (the family test is conservative): skip the
-            // triangle test.
-            if (tmax_w < FLT_MAX) {
-                const v2f lb[3] = {hi2(c), lo2(d), hi2(d)};
-                float ln = -INFINITY, lf = INFINITY;
-#pragma unroll
-                for (int q = 0; q < 3; ++q) {
-                    const v2f db = lb[q] - (v2f){o[q], o[q]};
-                    const v2f p = (v2f){db.x, db.x} * U[q], pq = (v2f){db.y, db.y} * U[q];
-                    ln = fmaxf(ln, fminf(fminf(p.x, p.y), fminf(pq.x, pq.y)));
-                    lf = fminf(lf, fmaxf(fmaxf(p.x, p.y), fmaxf(pq.x, pq.y)));
-                }
-                ln = __builtin_fmaf(fabsf(ln), -kW, ln);
-                lf = __builtin_fmaf(fabsf(lf), kW, lf);
-                skip = !(fmaxf(ln, kRayTMin) <= fminf(lf, tmax_w));
-            }
-#endif
             // Moller-Trumbore first, for every live lane; the leaf's pop-time box test (which the
             // reference makes before it) only for lanes whose triangle test would change their
             // state: the same outcome, and most leaf pops change no lane's bestT
             float t, u, v;
-            const bool hm = !skip && live && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y),
+            const bool hm = live && mt_g(r, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(b.w, c.x, c.y),
                                                   kRayTMin, hs.bestT, t, u, v);
             const uint64_t mh = ballot(hm);
             if (mh != 0) {
@@ -2869,7 +2848,7 @@ __device__ __forceinline__ bool hw1_tile_range(const Hw1Params& P, int4 r, int& 
 // Pass 1: each triangle's rectangle (kept for pass 2) and its count in every tile it meets.
 __global__ __launch_bounds__(BLOCK) void hw1_rect_count_kernel(Hw1Params P, int4* __restrict__ rects,
                                                                uint32_t* __restrict__ counts) {
-    const int k = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);  // (launched with 64-thread blocks)
     if (k >= P.num_tris) return;
     const int4 r = hw1_rect(P, k);
     rects[k] = r;
@@ -2884,7 +2863,7 @@ __global__ __launch_bounds__(BLOCK) void hw1_rect_count_kernel(Hw1Params P, int4
 // kernel gives that tile the brute-force loop instead.
 __global__ __launch_bounds__(BLOCK) void hw1_fill_kernel(Hw1Params P, uint32_t* __restrict__ cursor,
                                                          uint32_t* __restrict__ list) {
-    const int k = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (k >= P.num_tris) return;
     const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
     int tx0, tx1, ty0, ty1;
@@ -3610,9 +3589,11 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
             s->f_log2 = fr.log2;
             s->f_bound = fr.bound;
             // RT_TUNE_QUANT_RECORDS: 1 quantised records for every scene with frustum records,
-            // 0 none, else (default) for scenes whose float records alone exceed the big-scene
-            // threshold's eighth (c5: 34 MB; frog: 0.6 MB)
-            const double qk = rt::tuning(RT_TUNE_QUANT_RECORDS, -1.0);
+            // -1 for scenes whose float records alone exceed the big-scene threshold's eighth
+            // (c5: 34 MB; frog: 0.6 MB), 0 (default) none: c5 45.5 vs 42.4 ms with them, the
+            // dequantisation's VALU costing more than the halved record lines save
+            // (profiles/r05/exp/quant_records_ab_c5.log)
+            const double qk = rt::tuning(RT_TUNE_QUANT_RECORDS, 0.0);
             const double big = rt::tuning(RT_TUNE_BIG_SCENE_BYTES, double(kBigSceneBytes));
             const bool want_q = qk > 0.5 || (qk < -0.5 && double(fr.rec.size() * sizeof(float)) > big / 8.0);
             std::vector<uint32_t> qe;

@@ -801,13 +801,23 @@ def test_quantised_records_fuzz_cameras(scene, tune):
     assert ds.faults() == 0
 
 
-def test_c5_takes_the_quantised_records():
-    """The shipped default: the c5 heightfield (34 MB of 32-ary float records) renders through
-    the quantised records' kernel; frog (0.6 MB) does not."""
-    ds = _device_scene("heightfield_c5.json")
+def test_c5_quantised_records_auto(tune):
+    """RT_TUNE_QUANT_RECORDS = -1: the c5 heightfield (34 MB of 32-ary float records) renders
+    through the quantised records' kernel, frog (0.6 MB) does not; c5 rows through it against the
+    binary-record traversal, bit for bit.  The shipped default (0) keeps the float records."""
     hs = host_scene("heightfield_c5.json")
-    ds.render(hs.camera(64, 48), spp=1, max_depth=1)
+    assert _device_scene("heightfield_c5.json").render(hs.camera(64, 48), spp=1, max_depth=1) is not None
+    assert _device_scene("heightfield_c5.json").kernel_name().startswith("render_tiles_kernel<177,")
+    tune(quant_records=-1)
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    cam = hs.camera(480, 270)
+    a = ds.render(cam, spp=4, max_depth=1, aov=True, miss_color=(0.5, 0.7, 1.0))
     assert ds.kernel_name().startswith("render_tiles_kernel<433,"), ds.kernel_name()
-    fr = _device_scene("frog.json")
+    b = ds.render(cam, spp=4, max_depth=1, aov=True, miss_color=(0.5, 0.7, 1.0), flags=rt._lib.RT_FLAG_BINARY)
+    for x, y in zip(a, b):
+        assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32))
+    assert ds.faults() == 0
+    ds.close()
+    fr = rt.DeviceScene.from_host(host_scene("frog.json"), device=0)
     fr.render(host_scene("frog.json").camera(64, 48), spp=1, max_depth=1)
     assert not fr.kernel_name().startswith("render_tiles_kernel<433,"), fr.kernel_name()

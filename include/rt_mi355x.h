@@ -503,7 +503,10 @@ typedef enum {
     RT_TUNE_QUANT_RECORDS = 12,  /* quantised frustum records for the big-scene kernels, at scene creation:
                                     0 never (default; measured slower on c5), -1 scenes whose float
                                     records exceed 1/8 of RT_TUNE_BIG_SCENE_BYTES, 1 always */
-    RT_TUNE_COUNT = 13
+    RT_TUNE_PREPASS_GATE = 13,   /* 1 (default): a frame's render kernel opens the next frame's cull/cut
+                                    pre-passes when its first work queue drains (they then fill its
+                                    tail); 0: they start when the frame before it has finished */
+    RT_TUNE_COUNT = 14
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */
 int rt_tuning_set(int id, double value);

@@ -157,6 +157,12 @@ struct RenderParams {
     // W*H*spp by definition and counted on the host), [3] camera rays of the tiles the culling
     // passes left to the render kernel (the camera rays that are actually traversed)
     unsigned long long* ray_count;
+    // The pre-pass gate (RT_TUNE_PREPASS_GATE): the first waves to find their queue drained
+    // store drain_tag into this host word, and the next frame's pre-passes wait for it on the
+    // prep stream (hipStreamWaitValue32), so they take wave slots in this kernel's tail instead
+    // of racing its grid for them at its start.  Null: no gate.
+    uint32_t* drained;
+    uint32_t drain_tag;
 };
 
 // ---- wave primitives ------------------------------------------------------------------
@@ -2482,7 +2488,13 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
         int heavy;
         const int n = work_length(R, q, heavy);
         const int e = (R.nqueues == 1 ? g : 0) + (R.nqueues == 1 ? 8 : 1) * (int)(blockwise ? j : j / WPT);
-        if (e >= n) break;
+        if (e >= n) {
+            // the queue's first waves past its end (every queue has them: its items are handed
+            // out in order) open the next frame's pre-passes (a vector store to host memory)
+            if (R.drained && lane == 0 && e < n + (R.nqueues == 1 ? 8 : 1))
+                __hip_atomic_store(R.drained, R.drain_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
         const uint32_t qw = blockwise ? wv : j % WPT;
         int cls;
         const int tile = work_tile(R, q, e, heavy, cls);
@@ -2845,34 +2857,72 @@ __device__ __forceinline__ bool hw1_tile_range(const Hw1Params& P, int4 r, int& 
     return r.z >= 0 && r.w >= 0 && tx0 <= tx1 && ty0 <= ty1;
 }
 
+// The (triangle, tile) pairs of a wave's 64 triangles, 64 at a time over the wave's lanes: a
+// triangle covering many tiles no longer keeps one lane looping while the others wait (c2: 30 and
+// 25 us for the two passes with a lane per triangle).  Lane l's triangle covers cnt tiles from
+// (tx0, ty0), w per row; fn(tx, ty, triangle) runs once per pair.  Every lane of the wave calls
+// this (the shuffles read every lane).
+template <typename F>
+__device__ __forceinline__ void hw1_wave_pairs(uint32_t lane, int k, uint32_t cnt, int tx0, int ty0, int w, F&& fn) {
+    uint32_t incl = cnt;  // inclusive prefix sum over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, d);
+        if ((int)lane >= d) incl += v;
+    }
+    const uint32_t excl = incl - cnt;
+    const uint32_t total = uni((uint32_t)__shfl((int)incl, 63));
+    for (uint32_t base = 0; base < total; base += 64) {
+        const uint32_t p = base + lane;
+        // the pair's lane: the last one whose range starts at or before p (lanes without pairs
+        // start where the next lane does, so the last such lane has pairs)
+        int o = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const uint32_t e = (uint32_t)__shfl((int)excl, o + step);
+            if (e <= p) o += step;
+        }
+        const uint32_t local = p - (uint32_t)__shfl((int)excl, o);
+        const int ow = __shfl(w, o);
+        const int tx = __shfl(tx0, o) + (int)(local % (uint32_t)max(ow, 1));
+        const int ty = __shfl(ty0, o) + (int)(local / (uint32_t)max(ow, 1));
+        const int tri = __shfl(k, o);
+        if (p < total) fn(tx, ty, tri);
+    }
+}
+
 // Pass 1: each triangle's rectangle (kept for pass 2) and its count in every tile it meets.
-__global__ __launch_bounds__(BLOCK) void hw1_rect_count_kernel(Hw1Params P, int4* __restrict__ rects,
-                                                               uint32_t* __restrict__ counts) {
-    const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);  // (launched with 64-thread blocks)
-    if (k >= P.num_tris) return;
-    const int4 r = hw1_rect(P, k);
-    rects[k] = r;
+// (Launched with 64-thread blocks: one wave each.)
+__global__ __launch_bounds__(64) void hw1_rect_count_kernel(Hw1Params P, int4* __restrict__ rects,
+                                                            uint32_t* __restrict__ counts) {
+    const uint32_t lane = lane_id();
+    const int k = (int)(blockIdx.x * 64 + lane);
     const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
-    int tx0, tx1, ty0, ty1;
-    if (!hw1_tile_range(P, r, tx0, tx1, ty0, ty1)) return;
-    for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&counts[ty * tiles_x + tx], 1u);
+    int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;
+    if (k < P.num_tris) {
+        const int4 r = hw1_rect(P, k);
+        rects[k] = r;
+        if (!hw1_tile_range(P, r, tx0, tx1, ty0, ty1)) tx1 = tx0 - 1;
+    }
+    const uint32_t cnt = tx1 >= tx0 && ty1 >= ty0 ? (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1)) : 0u;
+    hw1_wave_pairs(lane, k, cnt, tx0, ty0, tx1 - tx0 + 1,
+                   [&](int tx, int ty, int) { atomicAdd(&counts[ty * tiles_x + tx], 1u); });
 }
 
 // Pass 2: the lists.  A tile whose list would reach past list_cap is not written; the render
 // kernel gives that tile the brute-force loop instead.
-__global__ __launch_bounds__(BLOCK) void hw1_fill_kernel(Hw1Params P, uint32_t* __restrict__ cursor,
-                                                         uint32_t* __restrict__ list) {
-    const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (k >= P.num_tris) return;
+__global__ __launch_bounds__(64) void hw1_fill_kernel(Hw1Params P, uint32_t* __restrict__ cursor,
+                                                      uint32_t* __restrict__ list) {
+    const uint32_t lane = lane_id();
+    const int k = (int)(blockIdx.x * 64 + lane);
     const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
-    int tx0, tx1, ty0, ty1;
-    if (!hw1_tile_range(P, P.rects[k], tx0, tx1, ty0, ty1)) return;
-    for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) {
-            const int t = ty * tiles_x + tx;
-            if (P.bin_offset[t + 1] <= P.list_cap) list[P.bin_offset[t] + atomicAdd(&cursor[t], 1u)] = (uint32_t)k;
-        }
+    int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;
+    if (k < P.num_tris && !hw1_tile_range(P, P.rects[k], tx0, tx1, ty0, ty1)) tx1 = tx0 - 1;
+    const uint32_t cnt = tx1 >= tx0 && ty1 >= ty0 ? (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1)) : 0u;
+    hw1_wave_pairs(lane, k, cnt, tx0, ty0, tx1 - tx0 + 1, [&](int tx, int ty, int tri) {
+        const int t = ty * tiles_x + tx;
+        if (P.bin_offset[t + 1] <= P.list_cap) list[P.bin_offset[t] + atomicAdd(&cursor[t], 1u)] = (uint32_t)tri;
+    });
 }
 
 // The chunked pass: a tile's list is cut into work items of at most HW1_CHUNK entries (a tile
@@ -3123,6 +3173,10 @@ struct rt_scene {
     bool caller_ordered = false;
     hipStream_t prep = nullptr;
     uint64_t launches = 0;
+    // the pre-pass gate's host word (RenderParams::drained) and the frame whose render kernel
+    // last stored into it (~0: none)
+    uint32_t* drain = nullptr;
+    uint64_t drain_frame = ~0ull;
     uint64_t est_next = 0;  // the oldest frame not yet seen finished (heavy-threshold estimate)
     size_t bytes = 0;
     // Work buffers rotate over kSets per frame (frame k: set k % 3; its cull pass zeroes the
@@ -3146,6 +3200,7 @@ struct rt_scene {
             if (evq[i]) (void)hipEventDestroy(evq[i]);
         }
         if (prep) (void)hipStreamDestroy(prep);
+        if (drain) (void)hipHostFree(drain);
     }
     int create_sync() {  // streams and events (rt_scene_create / rt_scene_clone)
         int lo = 0, hi = 0;
@@ -3153,6 +3208,8 @@ struct rt_scene {
         HIP_TRY(hipStreamCreateWithPriority(&prep, hipStreamNonBlocking, hi));
         if (int rc = fault.alloc(sizeof(uint32_t)); rc != RT_OK) return rc;
         HIP_TRY(hipMemset(fault.p, 0, sizeof(uint32_t)));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&drain), sizeof(uint32_t), hipHostMallocCoherent));
+        *drain = 0;
         for (int i = 0; i < kRing; ++i) {
             HIP_TRY(hipEventCreate(&ev0[i]));
             HIP_TRY(hipEventCreate(&evm[i]));
@@ -4116,6 +4173,9 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         // set k was last read by frame k-3, set k+1 (zeroed by this cull pass) by frame k-2
         if (k >= 2) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 2), 0));
         if (k >= 1 && overlap) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 1), 0));
+        // the pre-pass gate: frame k-1's render kernel opens it when its first queue drains
+        if (k >= 1 && s->drain_frame == k - 1)
+            HIP_TRY(hipStreamWaitValue32(pp, s->drain, uint32_t(k), hipStreamWaitValueGte, 0xFFFFFFFFu));
         if (!s->caller_ordered) {  // stream order for the caller's buffers (see rt_scene::evq)
             HIP_TRY(hipEventRecord(s->evq[slot], st));
             HIP_TRY(hipStreamWaitEvent(pp, s->evq[slot], 0));
@@ -4140,11 +4200,17 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         const size_t big_bytes = size_t(std::max(0.0, rt::tuning(RT_TUNE_BIG_SCENE_BYTES, double(kBigSceneBytes))));
         const bool qr = P.sc.qent != nullptr && P.sc.f_log2 > 2;
         const Launch L{st, s->evm[slot], s->ev1[slot], s->cus, s->bytes > big_bytes, qr, &s->last_kernel};
+        // RT_TUNE_PREPASS_GATE: 1 (default) this kernel opens the next frame's pre-passes when
+        // its first queue drains; 0 they start once the frame before this one has finished
+        const bool gate = rt::tuning(RT_TUNE_PREPASS_GATE, 1.0) > 0.5;
+        P.drained = gate ? s->drain : nullptr;
+        P.drain_tag = uint32_t(k + 1);
         if (s->deep) launch<MODE_DEEP>(P, samples, L);
         else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, L);
         else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, L);
         else launch<RT_KERNEL_WAVE>(P, samples, L);
         HIP_TRY(hipGetLastError());
+        if (gate) s->drain_frame = k;
         return RT_OK;
     };
     std::copy(std::begin(out_now), std::end(out_now), std::begin(s->prev_out));

@@ -506,7 +506,9 @@ typedef enum {
     RT_TUNE_PREPASS_GATE = 13,   /* 1 (default): a frame's render kernel opens the next frame's cull/cut
                                     pre-passes when its first work queue drains (they then fill its
                                     tail); 0: they start when the frame before it has finished */
-    RT_TUNE_COUNT = 14
+    RT_TUNE_OVERLAP_FRAMES = 14, /* rt_renderer frames: 1 lets a frame's render kernel start while the previous
+                                    one's tail still runs (two render streams per scene); 0 (default) */
+    RT_TUNE_COUNT = 15
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */
 int rt_tuning_set(int id, double value);

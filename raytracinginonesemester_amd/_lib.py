@@ -31,7 +31,8 @@ RT_FAULT_FRUSTUM_STACK = 1
 TUNE = {"frustum_arity": 0, "half_waves": 1, "paired_only": 2, "heavy_frac": 3, "heavy_cap": 4,
         "cull_coverage": 5, "cull_boxes": 6, "big_scene_bytes": 7, "frustum_stack_cap": 8,
         "peer_timeout_s": 9, "renderer_threads": 10, "copy_engine": 11,
-        "quant_records": 12, "prepass_gate": 13}
+        "quant_records": 12, "prepass_gate": 13,
+        "overlap_frames": 14}
 
 
 class RTError(RuntimeError):

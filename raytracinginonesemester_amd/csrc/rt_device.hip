@@ -3172,6 +3172,9 @@ struct rt_scene {
     hipEvent_t evq[kRing] = {};
     bool caller_ordered = false;
     hipStream_t prep = nullptr;
+    // RT_TUNE_OVERLAP_FRAMES (caller-ordered frames only): render kernels alternate over these
+    // two streams, so frame k+1's kernel takes the wave slots frame k's tail leaves
+    hipStream_t rstream[2] = {};
     uint64_t launches = 0;
     // the pre-pass gate's host word (RenderParams::drained) and the frame whose render kernel
     // last stored into it (~0: none)
@@ -3199,6 +3202,11 @@ struct rt_scene {
             if (pdone[i]) (void)hipEventDestroy(pdone[i]);
             if (evq[i]) (void)hipEventDestroy(evq[i]);
         }
+        for (hipStream_t r : rstream)
+            if (r) {
+                (void)hipStreamSynchronize(r);
+                (void)hipStreamDestroy(r);
+            }
         if (prep) (void)hipStreamDestroy(prep);
         if (drain) (void)hipHostFree(drain);
     }
@@ -3206,6 +3214,7 @@ struct rt_scene {
         int lo = 0, hi = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
         HIP_TRY(hipStreamCreateWithPriority(&prep, hipStreamNonBlocking, hi));
+        for (hipStream_t& r : rstream) HIP_TRY(hipStreamCreateWithFlags(&r, hipStreamNonBlocking));
         if (int rc = fault.alloc(sizeof(uint32_t)); rc != RT_OK) return rc;
         HIP_TRY(hipMemset(fault.p, 0, sizeof(uint32_t)));
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&drain), sizeof(uint32_t), hipHostMallocCoherent));
@@ -4155,7 +4164,11 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // the previous frame of this scene ran on another stream: wait for it.  (Letting two frames'
     // render kernels overlap on two streams, the next filling the CUs the last waves of the
     // previous one leave idle, measured slower for rt_renderer: 0.257 vs 0.246 ms per c3 frame.)
-    if (k > 0 && st != s->last_stream) HIP_TRY(hipStreamWaitEvent(st, ev1_of(k - 1), 0));
+    if (k > 0 && st != s->last_stream) {
+        HIP_TRY(hipStreamWaitEvent(st, ev1_of(k - 1), 0));
+        // (overlapping frames, RT_TUNE_OVERLAP_FRAMES: the one before may finish last)
+        if (k > 1) HIP_TRY(hipStreamWaitEvent(st, ev1_of(k - 2), 0));
+    }
     s->last_stream = st;
     const int set = int(k % rt_scene::kSets), nset = int((k + 1) % rt_scene::kSets);
     char* base = static_cast<char*>(s->work.p);
@@ -4196,10 +4209,15 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             hipExtLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, pp, nullptr, s->pdone[slot], 0, P);
             HIP_TRY(hipGetLastError());
         }
-        HIP_TRY(hipStreamWaitEvent(st, s->pdone[slot], 0));
+        // RT_TUNE_OVERLAP_FRAMES: the render kernel on one of the scene's two render streams (the
+        // caller orders its buffers itself; its stream then waits for the kernel), else on the
+        // caller's stream
+        const bool ovl = s->caller_ordered && rt::tuning(RT_TUNE_OVERLAP_FRAMES, 0.0) > 0.5;
+        const hipStream_t rs = ovl ? s->rstream[k & 1] : st;
+        HIP_TRY(hipStreamWaitEvent(rs, s->pdone[slot], 0));
         const size_t big_bytes = size_t(std::max(0.0, rt::tuning(RT_TUNE_BIG_SCENE_BYTES, double(kBigSceneBytes))));
         const bool qr = P.sc.qent != nullptr && P.sc.f_log2 > 2;
-        const Launch L{st, s->evm[slot], s->ev1[slot], s->cus, s->bytes > big_bytes, qr, &s->last_kernel};
+        const Launch L{rs, s->evm[slot], s->ev1[slot], s->cus, s->bytes > big_bytes, qr, &s->last_kernel};
         // RT_TUNE_PREPASS_GATE: 1 (default) this kernel opens the next frame's pre-passes when
         // its first queue drains; 0 they start once the frame before this one has finished
         const bool gate = rt::tuning(RT_TUNE_PREPASS_GATE, 1.0) > 0.5;
@@ -4210,6 +4228,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, L);
         else launch<RT_KERNEL_WAVE>(P, samples, L);
         HIP_TRY(hipGetLastError());
+        if (ovl) HIP_TRY(hipStreamWaitEvent(st, s->ev1[slot], 0));
         if (gate) s->drain_frame = k;
         return RT_OK;
     };

@@ -59,6 +59,7 @@ def trial(tag, k):
                               "kernel_p90": round(float(sorted(kt)[9 * len(kt) // 10]), 4),
                               "ms_per_step": round(el / a.steps * 1e3, 4),
                               "prepass_ms": round(float(sc.prepass_times(a.steps).mean()), 4),
+                              "deliver_ms": round(float(r.times(rt.RT_TIME_DELIVER, a.steps).mean()), 4),
                               "heavy_tiles": sc.heavy_tiles(), "kernel": sc.kernel_name(),
                               **({"series": [round(float(x), 4) for x in kt]} if a.series else {})}), flush=True)
     finally:

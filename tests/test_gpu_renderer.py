@@ -128,15 +128,16 @@ def test_pipelined_frames_all_identical(frog, golden):
         r.close()
 
 
-@pytest.mark.parametrize("engine", [None, 0, 1])
+@pytest.mark.parametrize("engine,overlap", [(None, 0), (0, 0), (1, 0), (None, 1), (0, 1)])
 @pytest.mark.parametrize("depth", [2, 3])
-def test_copy_engines_deliver_the_reference_frame(frog, golden, engine, depth, tune):
+def test_copy_engines_deliver_the_reference_frame(frog, golden, engine, overlap, depth, tune):
     """One rank delivering into host memory: by default (and with RT_TUNE_COPY_ENGINE=1) the
     frames go through SDMA copies queued through the HSA runtime, with 0 through the HIP
-    runtime's copies.  Pipelined frames with alternating cameras are each the single-frame image
-    (P6 and float; the c3 frame is the reference's), and so is a frame after a resize; the
-    copy's own times are reported."""
-    tune(copy_engine=engine)
+    runtime's copies; RT_TUNE_OVERLAP_FRAMES=1 lets consecutive render kernels overlap.
+    Pipelined frames with alternating cameras are each the single-frame image (P6 and float; the
+    c3 frame is the reference's), and so is a frame after a resize; the copy's own times are
+    reported."""
+    tune(copy_engine=engine, overlap_frames=overlap)
     base = frog.camera(W, H)
     cams = [base, rt.Camera(tuple(np.add(base.pos, (0.004, 0.0, 0.003))), base.look_at, base.up,
                             base.focal_length_mm, base.sensor_height_mm, W, H)]

@@ -445,9 +445,11 @@ int rt_box_test_host(const float* rays, const float* boxes, const float* tminmax
 int rt_debug_frustum_records(size_t P, const rt_bvh_node* nodes, const rt_aabb* aabbs, int max_log2, int stack_cap,
                              int64_t* info, float* rec, size_t rec_cap);
 
-/* Durations (ms) of the render kernel of the most recent min(max, launches, 256)
+/* Durations (ms) of the render kernel of the most recent min(max, launches, 256) timed
  * rt_render_device calls on this scene, oldest first, measured with HIP events recorded
- * on the launch stream around the kernel.  Waits for those launches to finish. */
+ * on the launch stream around the kernel (direct calls are all timed; an rt_renderer's frames
+ * one in RT_TUNE_KERNEL_TIMING_EVERY, *n_out then counts the timed ones).  Waits for those
+ * launches to finish. */
 int rt_kernel_times(const rt_scene* s, float* ms_out, int max, int* n_out);
 /* The same for the whole device frame: the root-box cull pass and the tree-cut cull pass (when
  * it runs), timed on the scene's prep stream, plus the render kernel.  (A frame's pre-passes
@@ -503,12 +505,16 @@ typedef enum {
     RT_TUNE_QUANT_RECORDS = 12,  /* quantised frustum records for the big-scene kernels, at scene creation:
                                     0 never (default; measured slower on c5), -1 scenes whose float
                                     records exceed 1/8 of RT_TUNE_BIG_SCENE_BYTES, 1 always */
-    RT_TUNE_PREPASS_GATE = 13,   /* 1 (default): a frame's render kernel opens the next frame's cull/cut
-                                    pre-passes when its first work queue drains (they then fill its
+    RT_TUNE_PREPASS_GATE = 13,   /* f in (0, 1]: a frame's render kernel opens the next frame's cull/cut
+                                    pre-passes when its first work queue has handed out the fraction
+                                    f of its items (0.5 default; 1: drained, they then fill its
                                     tail); 0: they start when the frame before it has finished */
     RT_TUNE_OVERLAP_FRAMES = 14, /* rt_renderer frames: 1 lets a frame's render kernel start while the previous
                                     one's tail still runs (two render streams per scene); 0 (default) */
-    RT_TUNE_COUNT = 15
+    RT_TUNE_KERNEL_TIMING_EVERY = 15, /* rt_renderer frames: the render kernel's start event (kernel times) in one
+                                    frame of this many (4); an event before every kernel held each
+                                    dispatch ~5 us */
+    RT_TUNE_COUNT = 16
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */
 int rt_tuning_set(int id, double value);

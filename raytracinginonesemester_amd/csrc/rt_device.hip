@@ -163,6 +163,7 @@ struct RenderParams {
     // of racing its grid for them at its start.  Null: no gate.
     uint32_t* drained;
     uint32_t drain_tag;
+    int32_t gate_q8;  // the gate opens when a queue has handed out gate_q8/256 of its items (256: drained)
 };
 
 // ---- wave primitives ------------------------------------------------------------------
@@ -229,6 +230,10 @@ __device__ unsigned long long g_rt_stats[24];
 // active at traversal start (primary), 14 (shadow), 15 primary traversals with no lane hitting,
 // 16 their pops, 17 primary traversals whose root test no lane passes
 
+#ifdef RT_FRAME_SPAN  // instrumented variant builds only: per render launch (drain_tag % 256) the first
+// wave's start and the last wave's end (wall clock, 100 MHz), and the pre-passes' first start
+__device__ unsigned long long* g_frame_span;
+#endif
 #ifdef RT_WAVE_TIMES  // instrumented variant builds only: per-wave start / end (wall clock, 100 MHz),
 // per-wave phase ends (primary traversal, whole sample) and per tile the number of cut boxes
 // its rays may meet (tile_cut_kernel)
@@ -2112,6 +2117,9 @@ __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
     // the previous frame's pass; zero the next frame's (its last user, frame k-2, has finished:
     // the scene's prep stream waited for it).
     if (blockIdx.x == 0 && threadIdx.x < COUNTER_SLOTS) P.next_count[threadIdx.x * COUNTER_STRIDE] = 0u;
+#ifdef RT_FRAME_SPAN
+    if (threadIdx.x == 0 && g_frame_span) atomicMin(&g_frame_span[4 * (P.drain_tag & 255u) + 2], wall_clock64());
+#endif
     cull_tiles(P, (int)(blockIdx.x * BLOCK + threadIdx.x));
 }
 
@@ -2237,6 +2245,9 @@ __global__ __launch_bounds__(BLOCK) void tile_cut_kernel(RenderParams P) {
         if (CUT_GROUP * g >= max_len) break;
         (void)cut_unit(P, lane, q, g, test, box);
     }
+#ifdef RT_FRAME_SPAN
+    if (lane == 0 && g_frame_span) atomicMax(&g_frame_span[4 * (P.drain_tag & 255u) + 3], wall_clock64());
+#endif
 }
 
 // The render kernel's work: list q's entries, its heavy lists' first (classes in order,
@@ -2471,6 +2482,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
         uint32_t* head = R.live_count + (HEAD_SLOT0 + g) * COUNTER_STRIDE;
         const bool blockwise = SAMPLES && R.spp > 64;
         const uint32_t lane = fresh_lane_id();
+#ifdef RT_FRAME_SPAN
+        if (first && lane == 0 && g_frame_span) atomicMin(&g_frame_span[4 * (R.drain_tag & 255u)], wall_clock64());
+#endif
         const int tid = (int)((wv << 6) | lane);
         const uint32_t per_queue = (gridDim.x >> 3) * (blockwise ? 1u : (uint32_t)WPT);  // first items
         uint32_t j;
@@ -2488,11 +2502,18 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
         int heavy;
         const int n = work_length(R, q, heavy);
         const int e = (R.nqueues == 1 ? g : 0) + (R.nqueues == 1 ? 8 : 1) * (int)(blockwise ? j : j / WPT);
-        if (e >= n) {
-            // the queue's first waves past its end (every queue has them: its items are handed
-            // out in order) open the next frame's pre-passes (a vector store to host memory)
-            if (R.drained && lane == 0 && e < n + (R.nqueues == 1 ? 8 : 1))
+        // the waves at the queue's gate item (its items are handed out in order, so every queue
+        // has them; gate_q8 = 256: the first waves past its end) open the next frame's
+        // pre-passes (a vector store to host memory)
+        if (R.drained && lane == 0) {
+            const int ge = (int)(((int64_t)n * R.gate_q8) >> 8);
+            if (e >= ge && e < ge + (R.nqueues == 1 ? 8 : 1))
                 __hip_atomic_store(R.drained, R.drain_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (e >= n) {
+#ifdef RT_FRAME_SPAN
+            if (lane == 0 && g_frame_span) atomicMax(&g_frame_span[4 * (R.drain_tag & 255u) + 1], wall_clock64());
+#endif
             break;
         }
         const uint32_t qw = blockwise ? wv : j % WPT;
@@ -3165,6 +3186,11 @@ struct rt_scene {
     // so frame k's pre-passes overlap frame k-1's render kernel (its tail leaves CUs idle).
     static constexpr int kRing = 256;
     hipEvent_t ev0[kRing] = {}, evm[kRing] = {}, ev1[kRing] = {}, pdone[kRing] = {};
+    // evm is recorded (the render kernel's start timestamp) only for timed frames: a start event
+    // holds the kernel's dispatch until the previous kernel has completed and its timestamp is
+    // written, ~5 us between back-to-back kernels (scripts/micro/kernel_gap.hip); the
+    // renderer's frames time one in RT_TUNE_KERNEL_TIMING_EVERY
+    bool timed[kRing] = {};
     // evq: recorded on the caller's stream at the start of a frame; the prep stream waits for it
     // so the pre-passes (which write the culled tiles' pixels into the caller's buffers) come
     // after everything the caller queued on that stream before the call.  A caller that orders
@@ -4106,7 +4132,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             // the render kernel's time, or the frame period when shorter (overlapping frames:
             // RT_FLAG_OVERLAP starts a kernel while the previous one still runs)
             float ms = 0.f, period = 0.f;
-            if (hipEventElapsedTime(&ms, s->evm[fl], s->ev1[fl]) == hipSuccess) {
+            if (s->timed[fl] && hipEventElapsedTime(&ms, s->evm[fl], s->ev1[fl]) == hipSuccess) {
                 const int f0 = int(uint64_t(last - 1) % rt_scene::kRing);
                 if (last >= 1 && hipEventElapsedTime(&period, s->ev1[f0], s->ev1[fl]) == hipSuccess && period > 0.f)
                     ms = std::min(ms, period);
@@ -4183,6 +4209,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // From the cull launch on, a failure leaves the counter sets unknown (counters_dirty).
     auto frame = [&]() -> int {
         hipStream_t pp = s->prep;
+        P.drain_tag = uint32_t(k + 1);
         // set k was last read by frame k-3, set k+1 (zeroed by this cull pass) by frame k-2
         if (k >= 2) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 2), 0));
         if (k >= 1 && overlap) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 1), 0));
@@ -4217,12 +4244,22 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         HIP_TRY(hipStreamWaitEvent(rs, s->pdone[slot], 0));
         const size_t big_bytes = size_t(std::max(0.0, rt::tuning(RT_TUNE_BIG_SCENE_BYTES, double(kBigSceneBytes))));
         const bool qr = P.sc.qent != nullptr && P.sc.f_log2 > 2;
-        const Launch L{rs, s->evm[slot], s->ev1[slot], s->cus, s->bytes > big_bytes, qr, &s->last_kernel};
-        // RT_TUNE_PREPASS_GATE: 1 (default) this kernel opens the next frame's pre-passes when
-        // its first queue drains; 0 they start once the frame before this one has finished
-        const bool gate = rt::tuning(RT_TUNE_PREPASS_GATE, 1.0) > 0.5;
+        // RT_TUNE_KERNEL_TIMING_EVERY: the caller-ordered (rt_renderer) frames record the render
+        // kernel's start event in one frame of this many (direct calls: every frame)
+        const uint64_t every = uint64_t(std::clamp(rt::tuning(RT_TUNE_KERNEL_TIMING_EVERY, 4.0), 1.0, 256.0));
+        s->timed[slot] = !s->caller_ordered || k % every == 0;
+        const Launch L{rs, s->timed[slot] ? s->evm[slot] : nullptr, s->ev1[slot], s->cus, s->bytes > big_bytes, qr,
+                       &s->last_kernel};
+        // RT_TUNE_PREPASS_GATE f in (0, 1]: this kernel opens the next frame's pre-passes when
+        // its first queue has handed out the fraction f of its items (0.5 default; 1: drained);
+        // 0 they start once the frame before this one has finished
+        // (0.5: c3 0.1557-0.157 ms per delivered frame vs 0.1587-0.1593 at 1.0, the pre-passes
+        // then finishing well before this kernel does; profiles/r05/exp/prepass_gate_frac_c3.log)
+        const double gate_f = rt::tuning(RT_TUNE_PREPASS_GATE, 0.5);
+        const bool gate = gate_f > 0.0;
         P.drained = gate ? s->drain : nullptr;
         P.drain_tag = uint32_t(k + 1);
+        P.gate_q8 = int(std::clamp(gate_f, 0.0, 1.0) * 256.0 + 0.5);
         if (s->deep) launch<MODE_DEEP>(P, samples, L);
         else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, L);
         else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, L);
@@ -4263,9 +4300,16 @@ int event_times(const rt_scene* s, int what, float* ms_out, int max, int* n_out)
     if (!s || max < 0 || (max > 0 && !ms_out)) return set_error(RT_ERR_ARG, "kernel times: bad args");
     DeviceGuard g(s->device);
     const uint64_t have = std::min<uint64_t>(s->launches, uint64_t(rt_scene::kRing));
-    const int n = int(std::min<uint64_t>(have, uint64_t(max)));
-    for (int k = 0; k < n; ++k) {  // oldest first among the n most recent
-        const int slot = int((s->launches - uint64_t(n) + uint64_t(k)) % rt_scene::kRing);
+    // the most recent frames with a kernel start event (all of them unless the renderer samples,
+    // RT_TUNE_KERNEL_TIMING_EVERY), at most max, oldest first; pre-pass times need no sampling
+    std::vector<int> slots;
+    for (uint64_t b = 1; b <= have && (int)slots.size() < max; ++b) {
+        const int slot = int((s->launches - b) % rt_scene::kRing);
+        if (what == 1 || s->timed[slot]) slots.push_back(slot);
+    }
+    const int n = (int)slots.size();
+    for (int k = 0; k < n; ++k) {
+        const int slot = slots[size_t(n - 1 - k)];
         HIP_TRY(hipEventSynchronize(s->ev1[slot]));
         float kern = 0.f, prep = 0.f;
         if (what != 1) HIP_TRY(hipEventElapsedTime(&kern, s->evm[slot], s->ev1[slot]));
@@ -4348,6 +4392,12 @@ extern "C" int rt_debug_lane_iters_set(void* iters_ptr, void* acc_ptr) {
 extern "C" int rt_debug_wave_times_set(void* dev_ptr, void* cut_counts_ptr) {
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wave_times), &dev_ptr, sizeof(dev_ptr)));
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_cut_counts), &cut_counts_ptr, sizeof(cut_counts_ptr)));
+    return RT_OK;
+}
+#endif
+#ifdef RT_FRAME_SPAN
+extern "C" int rt_debug_frame_span_set(void* dev_ptr) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_frame_span), &dev_ptr, sizeof(dev_ptr)));
     return RT_OK;
 }
 #endif

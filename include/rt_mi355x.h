@@ -514,7 +514,9 @@ typedef enum {
     RT_TUNE_KERNEL_TIMING_EVERY = 15, /* rt_renderer frames: the render kernel's start event (kernel times) in one
                                     frame of this many (4); an event before every kernel held each
                                     dispatch ~5 us */
-    RT_TUNE_COUNT = 16
+    RT_TUNE_RECORD_GREEDY = 16,  /* frustum records grown by expanding the largest-area entry (1, default)
+                                    instead of every path to the same depth (0); at scene creation */
+    RT_TUNE_COUNT = 17
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */
 int rt_tuning_set(int id, double value);

@@ -32,7 +32,8 @@ TUNE = {"frustum_arity": 0, "half_waves": 1, "paired_only": 2, "heavy_frac": 3, 
         "cull_coverage": 5, "cull_boxes": 6, "big_scene_bytes": 7, "frustum_stack_cap": 8,
         "peer_timeout_s": 9, "renderer_threads": 10, "copy_engine": 11,
         "quant_records": 12, "prepass_gate": 13,
-        "overlap_frames": 14, "kernel_timing_every": 15}
+        "overlap_frames": 14, "kernel_timing_every": 15,
+        "record_greedy": 16}
 
 
 class RTError(RuntimeError):

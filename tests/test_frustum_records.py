@@ -1,9 +1,11 @@
 """The camera rays' frustum records (rt_scene_create's build_frustum_records)
 checked on the host through rt_debug_frustum_records: no GPU.
 
-* the records are the expansion a Python restatement of the rule makes (descendants D levels
-  down in SearchBVH's push order; leaves stand for themselves, children naming no valid
-  triangle are skipped), boxes and refs bit for bit;
+* the records are the expansion a Python restatement of the rule makes, boxes and refs bit for
+  bit: by default (RT_TUNE_RECORD_GREEDY = 1) a record's entries grow from its node's two
+  children by replacing, in place, the internal entry of largest surface area by its children
+  until A entries; with 0, the descendants D levels down; in both, SearchBVH's push order,
+  leaves stand for themselves and children naming no valid triangle are skipped;
 * a DFS over the records that passes every box (push the entries in order, hold the last, pop)
   yields the leaves in exactly the order SearchBVH's own DFS does when every box passes
   (G/include/query.h:224-311: push left, push right, pop) -- the order the traversal's
@@ -43,8 +45,10 @@ def build(P, nodes, aabbs, max_log2, cap=64):
 class Model:
     """The rule restated over the reference arrays (rt_bvh_node: parent, left, right, object)."""
 
-    def __init__(self, P, nodes):
+    def __init__(self, P, nodes, aabbs=None, greedy=True):
         self.P, self.nodes = P, np.asarray(nodes, np.int64)
+        self.aabbs = None if aabbs is None else np.asarray(aabbs, np.float32)
+        self.greedy = greedy
         NN = 2 * P - 1
         self.cid = np.full(NN, NO_REF, np.int64)
         ni = nl = 0
@@ -72,13 +76,38 @@ class Model:
         self.expand(int(self.nodes[n, 1]), d - 1, out)
         self.expand(int(self.nodes[n, 2]), d - 1, out)
 
+    def area(self, n):
+        b = self.aabbs[n].astype(np.float64)
+        dx, dy, dz = (max(0.0, float(b[3 + i]) - float(b[i])) for i in range(3))
+        a = dx * dy + dy * dz + dz * dx
+        return a if np.isfinite(a) else 1e300
+
+    def greedy_entries(self, node, A):
+        kids = lambda n: [c for c in (int(self.nodes[n, 1]), int(self.nodes[n, 2])) if self.ref(c) != NO_REF]
+        fr = kids(node)
+        while len(fr) < A:
+            best, ba = -1, -1.0
+            for i, n in enumerate(fr):
+                if self.is_leaf(n):
+                    continue
+                a = self.area(n)
+                if a > ba:
+                    best, ba = i, a
+            if best < 0:
+                break
+            fr[best:best + 1] = kids(fr[best])
+        return fr
+
     def records(self, D):
         recs, fid, ents = [0], {0: 0}, []
         r = 0
         while r < len(recs):
             e = []
-            self.expand(int(self.nodes[recs[r], 1]), D - 1, e)
-            self.expand(int(self.nodes[recs[r], 2]), D - 1, e)
+            if self.greedy:
+                e = self.greedy_entries(recs[r], 1 << D)
+            else:
+                self.expand(int(self.nodes[recs[r], 1]), D - 1, e)
+                self.expand(int(self.nodes[recs[r], 2]), D - 1, e)
             for n in e:
                 if not self.is_leaf(n) and n not in fid:
                     fid[n] = len(recs)
@@ -104,6 +133,23 @@ class Model:
                 if c != NO_REF:
                     st.append(c)
         return out
+
+
+def _greedy():
+    import raytracinginonesemester_amd as rt
+
+    v = rt.get_tuning("record_greedy")
+    return v is None or v > 0.5
+
+
+@pytest.fixture(params=[1, 0], ids=["greedy", "fixed_depth"], autouse=True)
+def record_rule(request):
+    """Every test here runs under both record rules (RT_TUNE_RECORD_GREEDY)."""
+    import raytracinginonesemester_amd as rt
+
+    rt.set_tuning("record_greedy", request.param)
+    yield request.param
+    rt.reset_tuning()
 
 
 def records_leaf_order(log2, rec):
@@ -132,7 +178,7 @@ def records_leaf_order(log2, rec):
 
 
 def check(P, nodes, aabbs, max_log2=4, cap=64):
-    m = Model(P, nodes)
+    m = Model(P, nodes, aabbs, greedy=_greedy())
     log2, bound, nrec, rec = build(P, nodes, aabbs, max_log2, cap)
     if log2 == 2:
         return m, log2, bound
@@ -239,16 +285,22 @@ def first_leaf_depth(log2, rec):
 
 
 @pytest.mark.parametrize("L,want_log2", [(15, 5), (30, 4), (35, 3)])
-def test_spine_trees_fall_back_to_narrower_records(L, want_log2):
-    """tests/spine_bvh.py trees: the 32-ary records' DFS bound grows ~31 per five spine levels.
-    L = 15: 32-ary, bound in (64, 128] (the traversal's second stack VGPR); L = 30: the 32-ary
-    bound exceeds 128 and the builder falls back to 16-ary (bound in (64, 128]); L = 35: to
-    8-ary.  The records are the rule's, their leaf order SearchBVH's, and the centre rays of the
-    scene really reach more than 64 stack entries before their first leaf."""
+def test_spine_trees_fall_back_to_narrower_records(L, want_log2, record_rule):
+    """tests/spine_bvh.py trees, built for the fixed-depth rule: the 32-ary records' DFS bound
+    grows ~31 per five spine levels.  L = 15: 32-ary, bound in (64, 128] (the traversal's second
+    stack VGPR); L = 30: the 32-ary bound exceeds 128 and the builder falls back to 16-ary (bound
+    in (64, 128]); L = 35: to 8-ary.  The records are the rule's, their leaf order SearchBVH's,
+    and the centre rays of the scene really reach more than 64 stack entries before their first
+    leaf.  (The greedy rule spends the records' entries on the spine's large boxes and keeps the
+    stack shallow here: its records are checked against the rule only.)"""
     import spine_bvh
 
     a = spine_bvh.as_arrays(spine_bvh.spine_scene(L))
     P, nodes, aabbs = a["P"], a["nodes"], a["aabbs"]
+    if record_rule == 1:
+        _, log2, bound = check(P, nodes, aabbs, 5, 128)
+        assert log2 == 5 and bound <= 128
+        return
     _, log2, bound = check(P, nodes, aabbs, 5, 128)
     assert log2 == want_log2 and 64 < bound <= 128
     if want_log2 < 5:  # the wider arities do not fit

@@ -667,14 +667,16 @@ def _fuzz_cameras(hs, rng, n, W=96, H=64):
         yield k, rt.Camera(tuple(pos), tuple(target), up, float(rng.choice([8.0, 35.0, 600.0])), 24.0, W, H)
 
 
+@pytest.mark.parametrize("greedy", [1, 0])
 @pytest.mark.parametrize("arity", [None, 5, 4, 3])
 @pytest.mark.parametrize("scene", ["frog.json", "cornell.json", "sphere_single.json"])
-def test_frustum_fuzz_cameras(scene, arity, tune):
+def test_frustum_fuzz_cameras(scene, arity, greedy, tune):
     """The frustum traversal's wave-level box test must pass whenever some lane's exact test
     does (adversarial cameras, _fuzz_cameras): frames (hits, t, colour) bit-identical to the
     binary-record traversal, which tests every box for every lane.  At the shipped arity (None,
-    5: 32-ary records, frog's bound 91) the DFS uses the stack's second VGPR."""
-    tune(frustum_arity=arity)
+    5: 32-ary records, frog's bound 94 greedy / 91 fixed-depth) the DFS uses the stack's second
+    VGPR.  Both record rules (RT_TUNE_RECORD_GREEDY)."""
+    tune(frustum_arity=arity, record_greedy=greedy)
     hs = host_scene(scene)
     ds = rt.DeviceScene.from_host(hs, device=0)
     for k, cam in _fuzz_cameras(hs, np.random.default_rng(7), 36):
@@ -716,12 +718,14 @@ def _spine(L):
 
 
 @pytest.mark.parametrize("L,log2", [(15, 5), (30, 4), (35, 3)])
-def test_spine_trees_deep_frustum_stack(L, log2):
+def test_spine_trees_deep_frustum_stack(L, log2, tune):
     """Trees whose frustum DFS goes past 64 stack entries (tests/spine_bvh.py): 32-ary records
     with bound 109, and trees whose 32-ary bound exceeds the 128-entry stack, which take 16-ary
     (bound 124) or 8-ary records instead.  The centre rays reach more than 64 entries before
     their first leaf (tests/test_frustum_records.py).  Frames bit-identical to the binary-record
-    traversal and to the oracle; no device fault."""
+    traversal and to the oracle; no device fault.  (Records by the fixed-depth rule,
+    RT_TUNE_RECORD_GREEDY = 0, which these trees were built to push past 64 entries.)"""
+    tune(record_greedy=0)
     a, ds, cam = _spine(L)
     try:
         info = ds.traversal_info()
@@ -746,7 +750,7 @@ def test_frustum_stack_overflow_guard_is_loud(tune):
     spine tree's centre rays; the traversal drops the pushes instead of wrapping a lane index,
     raises RT_FAULT_FRUSTUM_STACK, and rt_render fails with RT_ERR_INTERNAL instead of
     returning a wrong frame."""
-    tune(frustum_stack_cap=10**6)
+    tune(frustum_stack_cap=10**6, record_greedy=0)
     a, ds, cam = _spine(30)
     try:
         info = ds.traversal_info()

@@ -121,6 +121,9 @@ def binding(i):
     name, frac = max(pipes.items(), key=lambda kv: kv[1])
     if frac >= 0.8:
         return f"{name} ({frac:.2f} of peak)"
+    if not a.kernel.startswith("render_tiles"):
+        return (f"latency: VALU issue {i['valu_issue']:.2f}, SALU issue {i['salu_issue']:.2f}; waves waiting "
+                f"{i['wait_any']:.2f} of their cycles at {i['waves_per_simd']:.1f} waves/SIMD")
     return (f"latency and scalar issue: the per-wave chain scalar node load -> box tests -> ballot -> "
             f"push/pop; the busiest pipe is the per-CU scalar unit (SALU {i['salu_issue']:.2f} of its "
             f"rate before the stack's v_readlane/v_writelane, which share it), VALU issue "

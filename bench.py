@@ -64,9 +64,11 @@ def parse():
                          "launcher this process drives GPUs 0..N-1 itself")
     ap.add_argument("--steps", type=int, default=100)  # ~35 ms of frames: a steadier average
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--preroll-ms", type=float, default=100.0,
-                    help="untimed frames for about this much GPU time before the W warmup frames (clocks; "
-                         "0: none); the frames run are reported as warmup_frames_run")
+    ap.add_argument("--preroll-ms", type=float, default=1500.0,
+                    help="untimed frames for about this much wall time before the W warmup frames (GPU "
+                         "clocks, and the device-to-host copies, which run at half speed for the first "
+                         "~0.45 s of sustained traffic in a process; 0: none); the frames run are reported "
+                         "as warmup_frames_run")
     ap.add_argument("--config", default="c3", choices=sorted(configs.G_CONFIGS) + sorted(configs.HW1_CONFIGS),
                     help="c1 / c2: the HW1 path (HW1/src/render.cpp:72-116) on one GPU (hw1_main)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "wave", "lane"])
@@ -215,11 +217,14 @@ def timed_native(r, cam, opts, steps, warmup, depth, ctx, preroll_ms=0.0):
     that much GPU time.  The GPU's clocks rise only under sustained load: a c3 frame's render
     kernel takes 0.22 ms in the first frames after an idle period and 0.18 ms after ~100 of them
     (`scripts/profile_frames.py --series`, profiles/r03/exp/clock_ramp_series.log), so a
-    few-millisecond timed region that starts cold measures the ramp.  The count is agreed over
-    the ranks (every rank renders every frame) and reported as warmup_frames_run."""
+    few-millisecond timed region that starts cold measures the ramp.  The device-to-host copies
+    ramp too, later: the first process on a fresh box copied c3's 6.2 MB P6 body in 0.238 ms for
+    its first ~0.45 s of frames, then in 0.1136 ms (scripts/deliver_ramp.py,
+    profiles/r05/exp/deliver_ramp_c3.log), so the default pre-roll is 1.5 s.  The count is agreed
+    over the ranks (every rank renders every frame) and reported as warmup_frames_run."""
     n_pre, chunk = 0, 2
     t0 = time.perf_counter()
-    while preroll_ms > 0 and n_pre < 5000:  # chunks of ~10 ms of frames; the ranks agree on each step
+    while preroll_ms > 0 and n_pre < 200000:  # chunks of ~10 ms of frames; the ranks agree on each step
         tc = time.perf_counter()
         run_frames(r, cam, opts, chunk, depth)
         n_pre += chunk

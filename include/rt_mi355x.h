@@ -516,7 +516,10 @@ typedef enum {
                                     dispatch ~5 us */
     RT_TUNE_RECORD_GREEDY = 16,  /* frustum records grown by expanding the largest-area entry (1, default)
                                     instead of every path to the same depth (0); at scene creation */
-    RT_TUNE_COUNT = 17
+    RT_TUNE_WIDE4_GREEDY = 17,   /* the 4-ary records (shadow and bounce rays) grown by expanding the
+                                    largest-area entry (1, default) instead of the grandchildren (0);
+                                    at scene creation */
+    RT_TUNE_COUNT = 18
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */
 int rt_tuning_set(int id, double value);

@@ -3496,8 +3496,55 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     // slab tests being monotone in the box), checked here; the wave path falls back to the
     // binary records otherwise, or when the 4-ary DFS stack would exceed 64 entries.
     auto ref_of0 = [&](uint32_t n) -> uint32_t { return n == NO_REF ? NO_REF : cid[n]; };
+    // RT_TUNE_WIDE4_GREEDY (default 1): the 4-ary records' entries grown from the node's children
+    // by expanding, in place, the internal entry of largest surface area (up to 4 entries); 0:
+    // the grandchildren.  Exact for the reasons the grandchildren are (every box contains its
+    // children's, checked below for every parent-child pair; the DFS order is SearchBVH's; no
+    // leaf is tested between an expanded node's pop and its children's in the reference).
+    // c3 0.1390 vs 0.1419 ms, c3b 1.2455 vs 1.2986, c5 40.35 vs 40.82
+    // (profiles/r05/exp/wide4_greedy_ab.log)
+    const bool wide4_greedy = rt::tuning(RT_TUNE_WIDE4_GREEDY, 1.0) > 0.5;
+    auto box_area = [&](uint32_t n) {
+        const rt_aabb& b = aabbs[n];
+        const double dx = std::max(0.0, double(b.max_corner.x) - b.min_corner.x);
+        const double dy = std::max(0.0, double(b.max_corner.y) - b.min_corner.y);
+        const double dz = std::max(0.0, double(b.max_corner.z) - b.min_corner.z);
+        const double a = dx * dy + dy * dz + dz * dx;
+        return std::isfinite(a) ? a : 1e300;
+    };
     auto wide_entries = [&](const rt_bvh_node& nd, uint32_t* e) {
         int k = 0;
+        if (wide4_greedy) {
+            for (const uint32_t c : {nd.left_idx, nd.right_idx})
+                if (ref_of0(c) != NO_REF) e[k++] = c;
+            while (k < 4) {
+                int best = -1;
+                double ba = -1.0;
+                for (int i = 0; i < k; ++i) {
+                    if (ref_of0(e[i]) & LEAF_BIT) continue;
+                    const double a = box_area(e[i]);
+                    if (a > ba) {
+                        ba = a;
+                        best = i;
+                    }
+                }
+                if (best < 0) break;
+                uint32_t kids[2];
+                int nk = 0;
+                for (const uint32_t g : {nodes[e[best]].left_idx, nodes[e[best]].right_idx})
+                    if (ref_of0(g) != NO_REF) kids[nk++] = g;
+                uint32_t grown[4];
+                int t = 0;
+                for (int i = 0; i < k; ++i) {
+                    if (i != best) grown[t++] = e[i];
+                    else
+                        for (int j = 0; j < nk; ++j) grown[t++] = kids[j];
+                }
+                for (int i = 0; i < t; ++i) e[i] = grown[i];
+                k = t;
+            }
+            return k;
+        }
         for (const uint32_t c : {nd.left_idx, nd.right_idx}) {
             if (ref_of0(c) == NO_REF) continue;
             if (ref_of0(c) & LEAF_BIT) {

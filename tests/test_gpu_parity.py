@@ -825,3 +825,25 @@ def test_c5_quantised_records_auto(tune):
     fr = rt.DeviceScene.from_host(host_scene("frog.json"), device=0)
     fr.render(host_scene("frog.json").camera(64, 48), spp=1, max_depth=1)
     assert not fr.kernel_name().startswith("render_tiles_kernel<433,"), fr.kernel_name()
+
+
+@pytest.mark.parametrize("wide4,frustum", [(0, 1), (1, 0), (0, 0)])
+@pytest.mark.parametrize("name", ["c3_small", "frog_bounce", "sphere_single", "cornell", "c5_small", "c3b_small"])
+def test_record_rules_parity(name, wide4, frustum, tune):
+    """The record rules off their defaults (greedy 32-ary frustum records and greedy 4-ary
+    records, RT_TUNE_RECORD_GREEDY / RT_TUNE_WIDE4_GREEDY; the fixed-depth forms): every
+    combination gives the reference's hits, t and frame bit for bit (the shadow rays and the
+    bounce rays walk the 4-ary records)."""
+    tune(wide4_greedy=wide4, record_greedy=frustum)
+    meta = golden_meta(name)
+    hs = host_scene(G_SCENES[name])
+    cam = hs.camera(meta["width"], meta["height"])
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    rgb, hi, ht = ds.render(cam, spp=meta["spp"], max_depth=meta["max_depth"],
+                            diffuse_bounce=bool(meta["diffuse_bounce"]), miss_color=hexv(meta["miss_color"]),
+                            aov=True)
+    assert ds.faults() == 0
+    assert np.array_equal(hi.reshape(-1), golden_array(name, "hits.i32.gz", np.int32))
+    assert np.array_equal(ht.reshape(-1).view(np.uint32),
+                          golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
+    _check_fb(rgb, golden_array(name, "fb.f32.gz", np.float32))

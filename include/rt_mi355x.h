@@ -514,11 +514,12 @@ typedef enum {
     RT_TUNE_KERNEL_TIMING_EVERY = 15, /* rt_renderer frames: the render kernel's start event (kernel times) in one
                                     frame of this many (4); an event before every kernel held each
                                     dispatch ~5 us */
-    RT_TUNE_RECORD_GREEDY = 16,  /* frustum records grown by expanding the largest-area entry (1, default)
-                                    instead of every path to the same depth (0); at scene creation */
+    RT_TUNE_RECORD_GREEDY = 16,  /* frustum records grown by expanding the entry of largest weight: 2
+                                    (default) surface area x sqrt(leaves below), 1 surface area;
+                                    0: every path to the same depth; at scene creation */
     RT_TUNE_WIDE4_GREEDY = 17,   /* the 4-ary records (shadow and bounce rays) grown by expanding the
-                                    largest-area entry (1, default) instead of the grandchildren (0);
-                                    at scene creation */
+                                    largest-area entry (1, default; 2: x sqrt(leaves below)) instead
+                                    of the grandchildren (0); at scene creation */
     RT_TUNE_COUNT = 18
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */

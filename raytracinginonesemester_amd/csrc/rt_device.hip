@@ -3276,6 +3276,37 @@ extern "C" int rt_device_count(int* n) {
 // cid: compact ids as rt_scene_create makes them (LEAF_BIT | slot, internal index, or NO_REF).
 // (Leaf-pair entries, an internal node with two leaf children tested in one pop, measured no
 // faster: c3 0.1517 vs 0.1517 ms, c5 48.2 vs 45.9; profiles/r04/exp/pairs_stack128_ab_*.log.)
+// Valid leaves under each node (the greedy record rules' weights): a post-order walk from the
+// root over the nodes rt_scene_create gave ids (cid: NO_REF for nodes naming no valid triangle).
+static std::vector<uint32_t> subtree_leaves(const rt_bvh_node* nodes, size_t NN, const uint32_t* cid) {
+    std::vector<uint32_t> leaves(NN, 0u);
+    std::vector<uint8_t> seen(NN, 0);  // each node expanded once (the tree is checked elsewhere)
+    auto ref_of0 = [&](uint32_t n) -> uint32_t { return n == NO_REF || n >= NN ? NO_REF : cid[n]; };
+    std::vector<std::pair<uint32_t, bool>> st{{0u, false}};
+    while (!st.empty()) {
+        auto [v, post] = st.back();
+        st.pop_back();
+        if (ref_of0(v) == NO_REF) continue;
+        if (ref_of0(v) & LEAF_BIT) {
+            leaves[v] = 1;
+            continue;
+        }
+        if (!post) {
+            if (seen[v]) continue;
+            seen[v] = 1;
+            st.push_back({v, true});
+            for (uint32_t c : {nodes[v].left_idx, nodes[v].right_idx})
+                if (c != NO_REF) st.push_back({c, false});
+        } else {
+            uint32_t sum = 0;
+            for (uint32_t c : {nodes[v].left_idx, nodes[v].right_idx})
+                if (c != NO_REF && ref_of0(c) != NO_REF) sum += leaves[c];
+            leaves[v] = sum;
+        }
+    }
+    return leaves;
+}
+
 struct FrustumRecords {
     int log2 = 2;
     int bound = 0;  // the DFS stack bound of the records (root record)
@@ -3286,18 +3317,25 @@ static FrustumRecords build_frustum_records(const rt_bvh_node* nodes, size_t NN,
                                             const rt_aabb* aabbs, int dmax, int cap) {
     FrustumRecords out;
     auto ref_of0 = [&](uint32_t n) -> uint32_t { return n == NO_REF ? NO_REF : cid[n]; };
-    // RT_TUNE_RECORD_GREEDY (default 1): a record's entries are grown from its node's children
-    // by expanding, in place (the DFS order stays the reference's), the internal entry of
-    // largest surface area until A entries; 0: every path to the same depth.  Larger boxes are
-    // the ones rays reach: c3 0.1412 vs 0.1452 ms, c5 41.0 vs 42.9 (frog 3,416 records vs 3,854,
-    // bound 94 vs 91; profiles/r05/exp/record_greedy_ab_c*.log)
-    const bool greedy = rt::tuning(RT_TUNE_RECORD_GREEDY, 1.0) > 0.5;
+    // RT_TUNE_RECORD_GREEDY: a record's entries are grown from its node's children by expanding,
+    // in place (the DFS order stays the reference's), the internal entry of largest weight until
+    // A entries: 2 (default) surface area x sqrt(valid leaves below), 1 surface area (3: x
+    // log2(leaves + 1), 4: x leaves); 0: every path to the same depth.  Larger boxes are the ones
+    // rays reach: c3 0.1412 vs 0.1452 ms, c5 41.0 vs 42.9 with the area (frog 3,416 records vs
+    // 3,854, bound 94 vs 91; profiles/r05/exp/record_greedy_ab_c*.log); the leaf weight: c5
+    // 39.3-39.9 vs 40.8-41.1, c3 within noise (record_rules_ab.log)
+    const int greedy_rule = int(rt::tuning(RT_TUNE_RECORD_GREEDY, 2.0) + 0.5);
+    const bool greedy = greedy_rule > 0;
+    const std::vector<uint32_t> leaves = greedy_rule >= 2 ? subtree_leaves(nodes, NN, cid) : std::vector<uint32_t>();
     auto area = [&](uint32_t n) {
         const rt_aabb& b = aabbs[n];
         const double dx = std::max(0.0, double(b.max_corner.x) - b.min_corner.x);
         const double dy = std::max(0.0, double(b.max_corner.y) - b.min_corner.y);
         const double dz = std::max(0.0, double(b.max_corner.z) - b.min_corner.z);
-        const double a = dx * dy + dy * dz + dz * dx;
+        double a = dx * dy + dy * dz + dz * dx;
+        if (greedy_rule == 2) a *= std::sqrt(double(leaves[n]));
+        if (greedy_rule == 3) a *= std::log2(double(leaves[n]) + 1.0);
+        if (greedy_rule == 4) a *= double(leaves[n]);
         return std::isfinite(a) ? a : 1e300;
     };
     for (int D = std::min(dmax, 5); D >= 3; --D) {
@@ -3503,13 +3541,16 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
     // leaf is tested between an expanded node's pop and its children's in the reference).
     // c3 0.1390 vs 0.1419 ms, c3b 1.2455 vs 1.2986, c5 40.35 vs 40.82
     // (profiles/r05/exp/wide4_greedy_ab.log)
-    const bool wide4_greedy = rt::tuning(RT_TUNE_WIDE4_GREEDY, 1.0) > 0.5;
+    const int wide4_rule = int(rt::tuning(RT_TUNE_WIDE4_GREEDY, 1.0) + 0.5);
+    const bool wide4_greedy = wide4_rule > 0;
+    const std::vector<uint32_t> wleaves = wide4_rule == 2 ? subtree_leaves(nodes, NN, cid.data()) : std::vector<uint32_t>();
     auto box_area = [&](uint32_t n) {
         const rt_aabb& b = aabbs[n];
         const double dx = std::max(0.0, double(b.max_corner.x) - b.min_corner.x);
         const double dy = std::max(0.0, double(b.max_corner.y) - b.min_corner.y);
         const double dz = std::max(0.0, double(b.max_corner.z) - b.min_corner.z);
-        const double a = dx * dy + dy * dz + dz * dx;
+        double a = dx * dy + dy * dz + dz * dx;
+        if (wide4_rule == 2) a *= std::sqrt(double(wleaves[n]));
         return std::isfinite(a) ? a : 1e300;
     };
     auto wide_entries = [&](const rt_bvh_node& nd, uint32_t* e) {

@@ -45,10 +45,11 @@ def build(P, nodes, aabbs, max_log2, cap=64):
 class Model:
     """The rule restated over the reference arrays (rt_bvh_node: parent, left, right, object)."""
 
-    def __init__(self, P, nodes, aabbs=None, greedy=True):
+    def __init__(self, P, nodes, aabbs=None, greedy=2):
         self.P, self.nodes = P, np.asarray(nodes, np.int64)
         self.aabbs = None if aabbs is None else np.asarray(aabbs, np.float32)
-        self.greedy = greedy
+        self.greedy = greedy  # 0 fixed depth, 1 area, 2 area x sqrt(leaves below)
+        self._leaves = {}
         NN = 2 * P - 1
         self.cid = np.full(NN, NO_REF, np.int64)
         ni = nl = 0
@@ -76,10 +77,29 @@ class Model:
         self.expand(int(self.nodes[n, 1]), d - 1, out)
         self.expand(int(self.nodes[n, 2]), d - 1, out)
 
+    def leaves(self, n):
+        if n in self._leaves:
+            return self._leaves[n]
+        out, st = 0, [n]
+        while st:
+            v = st.pop()
+            if self.ref(v) == NO_REF:
+                continue
+            if self.is_leaf(v):
+                out += 1
+                continue
+            st += [c for c in (int(self.nodes[v, 1]), int(self.nodes[v, 2])) if c != NO_REF]
+        self._leaves[n] = out
+        return out
+
     def area(self, n):
+        import math
+
         b = self.aabbs[n].astype(np.float64)
         dx, dy, dz = (max(0.0, float(b[3 + i]) - float(b[i])) for i in range(3))
         a = dx * dy + dy * dz + dz * dx
+        if self.greedy == 2:
+            a *= math.sqrt(float(self.leaves(n)))
         return a if np.isfinite(a) else 1e300
 
     def greedy_entries(self, node, A):
@@ -139,10 +159,10 @@ def _greedy():
     import raytracinginonesemester_amd as rt
 
     v = rt.get_tuning("record_greedy")
-    return v is None or v > 0.5
+    return 2 if v is None else int(v + 0.5)
 
 
-@pytest.fixture(params=[1, 0], ids=["greedy", "fixed_depth"], autouse=True)
+@pytest.fixture(params=[2, 1, 0], ids=["greedy_leaf_weight", "greedy_area", "fixed_depth"], autouse=True)
 def record_rule(request):
     """Every test here runs under both record rules (RT_TUNE_RECORD_GREEDY)."""
     import raytracinginonesemester_amd as rt
@@ -297,7 +317,7 @@ def test_spine_trees_fall_back_to_narrower_records(L, want_log2, record_rule):
 
     a = spine_bvh.as_arrays(spine_bvh.spine_scene(L))
     P, nodes, aabbs = a["P"], a["nodes"], a["aabbs"]
-    if record_rule == 1:
+    if record_rule >= 1:
         _, log2, bound = check(P, nodes, aabbs, 5, 128)
         assert log2 == 5 and bound <= 128
         return

@@ -245,3 +245,10 @@ def test_tuning_knobs_are_explicit():
     finally:
         rt.reset_tuning()
     assert all(rt.get_tuning(k) is None for k in _lib.TUNE)
+    # the Python table names the header's enum, id for id
+    import re
+
+    hdr = (REPO / "include" / "rt_mi355x.h").read_text()
+    ids = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"RT_TUNE_([A-Z0-9_]+) = (\d+)", hdr)}
+    ids.pop("count")
+    assert ids == _lib.TUNE

@@ -85,6 +85,9 @@ def parse():
     # frames in flight: 2 on one GPU (render k+1 while frame k's P6 is copied: 0.2170 vs 0.2233
     # ms per frame at 3, 0.328 at 6); 3 over N GPUs
     ap.add_argument("--depth", type=int, default=None)
+    ap.add_argument("--pair", type=int, default=0, choices=[0, 1],
+                    help="1: the frames are submitted two at a time (rt_renderer_submit_pair: one render "
+                         "launch renders both where the pair kernel fits them); 0: one at a time")
     ap.add_argument("--comm", default="native", choices=["native", "torch"],
                     help="native: rt_renderer (librt_mi355x); torch: torch.distributed gather (alternate launcher)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -196,14 +199,24 @@ def sync_all(dev, world):
     torch.cuda.synchronize(dev)
 
 
+PAIR = {"on": False}
+
+
 def run_frames(r, cam, opts, n, depth):
-    """Submit n frames, waiting for every one of them (host memory on rank 0)."""
+    """Submit n frames, waiting for every one of them (host memory on rank 0), at most depth in
+    flight; with --pair 1 two at a time (rt_renderer_submit_pair), an odd last one alone."""
     pend = []
     last = None
-    for _ in range(n):
-        pend.append(r.submit(cam, opts))
-        if len(pend) >= depth:
+    i = 0
+    while i < n:
+        two = PAIR["on"] and depth >= 2 and n - i >= 2
+        while len(pend) > depth - (2 if two else 1):
             last = r.wait(pend.pop(0))
+        if two:
+            pend += list(r.submit_pair(cam, cam, opts))
+        else:
+            pend.append(r.submit(cam, opts))
+        i += 2 if two else 1
     for t in pend:
         last = r.wait(t)
     return last
@@ -756,10 +769,13 @@ def main():
     hs = rt.HostScene.load_json(sp, REPO if sp.parent == configs.SCENES else sp.parent)
     cam = hs.camera(cfg["width"], cfg["height"])
     W, H, spp = cam.pixel_width, cam.pixel_height, cfg["spp"]
+    PAIR["on"] = bool(a.pair)
     if a.depth is None:  # frames in flight (N = 1: depth 3 keeps the host's waits off the critical
         # path; the driver's 20-step command: 0.171 ms/step vs 0.174-0.262 at depth 2 with SDMA copies,
-        # profiles/r05/exp/driver_cmd_depth_ab.log)
-        a.depth = 3
+        # profiles/r05/exp/driver_cmd_depth_ab.log); pairs: 6, the host two pairs ahead (at 4 the next
+        # pair's submit waited for the previous pair's copies: 0.157-0.165 ms/step vs 0.151 at 6,
+        # profiles/r05/exp/pair_ab_c3.log)
+        a.depth = 6 if a.pair else 3
 
     comm = a.comm
     fallback = None
@@ -835,7 +851,8 @@ def main():
         "copy_engine": (("sdma: P6 copies queued through the HSA runtime on a DMA engine once each frame's "
                          "render event fires (no CU slots)" if res.get("copy_engine") == "sdma" else
                          "runtime: hipMemcpyAsync (blit kernels on the CUs)") if comm == "native" else None),
-        "pipeline_depth": a.depth if comm == "native" else 2, "kernel": a.kernel}
+        "pipeline_depth": a.depth if comm == "native" else 2, "kernel": a.kernel,
+        "frames_per_submit": 2 if (a.pair and comm == "native") else 1}
     if a.share_gpu and world > 1:
         line["config"]["rehearsal"] = "--share-gpu: ranks share GPUs (not a multi-GPU measurement)"
     if a.tune:
@@ -851,7 +868,10 @@ def main():
     traffic = tr.get("bytes_per_launch") if tr else None
     roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": traffic,
             "kernel": instance or "render_tiles_kernel", "kernel_ms": round(kernel_ms, 4),
-            "frame_ms": round(frame_ms, 4)}
+            "frame_ms": round(frame_ms, 4),
+            # a pair kernel (rt_renderer_submit_pair) renders two frames per launch: its kernel_ms
+            # and bytes per launch are both per two frames
+            "frames_per_launch": 2 if (instance or "").startswith("render_pair_kernel") else 1}
     if traffic:
         ach = traffic / (kernel_ms / 1e3) / 1e9
         roof.update(achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
@@ -864,7 +884,8 @@ def main():
         roof.update(achieved=None, frac=None,
                     achieved_from=f"no PMC traffic profiled for {instance} on {a.config} (profiles/traffic.json)")
     if bps:
-        roof["reference_equivalent_GBps"] = round(bps * per_gpu_samples / (kernel_ms / 1e3) / 1e9, 2)
+        roof["reference_equivalent_GBps"] = round(bps * per_gpu_samples * roof["frames_per_launch"] /
+                                                  (kernel_ms / 1e3) / 1e9, 2)
         roof["reference_equivalent_note"] = (f"SURVEY.md §8(d) reference-layout model, {bps:.2f} B/sample: the "
                                              "bytes the reference's per-ray traversal would fetch, not this "
                                              "kernel's traffic")

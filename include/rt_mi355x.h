@@ -243,6 +243,15 @@ int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_render_opts*
                         float* rgb_dev, int32_t* hit_idx_dev, float* hit_t_dev, uint8_t* p6_dev,
                         void* hip_stream);
 
+/* Two frames of one scene with the same options (two cameras of the same pixel size, e.g. the
+ * next two frames of a sequence), as rt_render_device_p6 twice (frame a, then frame b; the
+ * same images), rendered by one launch of the render kernel where it fits them
+ * (RT_TUNE_PAIR_FRAMES): the second frame's work fills the first's tail and the launch gap
+ * between two frames goes.  Outputs of a and b must not overlap. */
+int rt_render_device_pair(rt_scene* s, const rt_camera* cam_a, const rt_camera* cam_b,
+                          const rt_render_opts* opt, float* rgb_a_dev, uint8_t* p6_a_dev,
+                          float* rgb_b_dev, uint8_t* p6_b_dev, void* hip_stream);
+
 /* Synchronous convenience: render into host memory (rows*W*3 floats, + optional AOVs). */
 int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts* opt,
               float* rgb_host, int32_t* hit_idx_host, float* hit_t_host);
@@ -356,6 +365,11 @@ void rt_renderer_destroy(rt_renderer* r);
 /* Enqueue one frame (opts: its band fields are the renderer's).  Blocks only to reuse the
  * buffers of frame ticket-depth, which must then be complete.  *ticket numbers the frames. */
 int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt_render_opts* opts, uint64_t* ticket);
+/* Enqueue two frames (tickets *ticket_a, *ticket_a + 1) with the same options, rendered by one
+ * launch per local rank (rt_render_device_pair); delivered as two rt_renderer_submit calls
+ * would deliver them.  Needs depth >= 2; blocks to reuse both frames' buffers. */
+int rt_renderer_submit_pair(rt_renderer* r, const rt_camera* cam_a, const rt_camera* cam_b,
+                            const rt_render_opts* opts, uint64_t* ticket_a);
 /* Wait for frame `ticket` (one of the last `depth` submitted, and not from before a change of
  * the frame size, which reallocates the buffers).  On the process holding rank 0,
  * *frame / *bytes give the delivered frame: pinned host memory (RT_DELIVER_P6/F32) or rank 0's
@@ -520,7 +534,13 @@ typedef enum {
     RT_TUNE_WIDE4_GREEDY = 17,   /* the 4-ary records (shadow and bounce rays) grown by expanding the
                                     largest-area entry (1, default; 2: x sqrt(leaves below)) instead
                                     of the grandchildren (0); at scene creation */
-    RT_TUNE_COUNT = 18
+    RT_TUNE_PAIR_FRAMES = 18,    /* rt_render_device_pair / rt_renderer_submit_pair: 1 (default) renders the
+                                    two frames in one launch of the render kernel where it is
+                                    instantiated for them (depth-1 sample kernels of the wave
+                                    traversal, scene within RT_TUNE_BIG_SCENE_BYTES); 0 two launches */
+    RT_TUNE_PAIR_RESERVE = 19,   /* pair kernels: block slots per CU left free for the next pair's pre-passes
+                                    (0 default) */
+    RT_TUNE_COUNT = 20
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */
 int rt_tuning_set(int id, double value);

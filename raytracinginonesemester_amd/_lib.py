@@ -33,7 +33,7 @@ TUNE = {"frustum_arity": 0, "half_waves": 1, "paired_only": 2, "heavy_frac": 3, 
         "peer_timeout_s": 9, "renderer_threads": 10, "copy_engine": 11,
         "quant_records": 12, "prepass_gate": 13,
         "overlap_frames": 14, "kernel_timing_every": 15,
-        "record_greedy": 16, "wide4_greedy": 17}
+        "record_greedy": 16, "wide4_greedy": 17, "pair_frames": 18, "pair_reserve": 19}
 
 
 class RTError(RuntimeError):
@@ -152,6 +152,7 @@ SIGNATURES = {
     "rt_shard_rows": (I, [I, I, I, I]),
     "rt_render_device": (I, [P, P, P, P, P, P, P]),
     "rt_render_device_p6": (I, [P, P, P, P, P, P, P, P]),
+    "rt_render_device_pair": (I, [P, P, P, P, P, P, P, P, P]),
     "rt_render": (I, [P, P, P, P, P, P]),
     "rt_count_rays": (I, [P, P, P, P]),
     "rt_count_rays_ex": (I, [P, P, P, P]),
@@ -162,6 +163,7 @@ SIGNATURES = {
     "rt_renderer_create": (I, [SZ, P, P, P, P, P, I, P, I, P, P]),
     "rt_renderer_destroy": (None, [P]),
     "rt_renderer_submit": (I, [P, P, P, P]),
+    "rt_renderer_submit_pair": (I, [P, P, P, P, P]),
     "rt_renderer_wait": (I, [P, C.c_uint64, P, P]),
     "rt_renderer_render": (I, [P, P, P, P, SZ]),
     "rt_renderer_scene": (P, [P, I]),

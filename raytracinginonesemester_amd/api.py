@@ -289,6 +289,13 @@ class DeviceScene:
         check(lib().rt_render_device_p6(self._handle(), C.byref(camera.c), C.byref(opts), rgb_dev_ptr, hit_idx_ptr,
                                         hit_t_ptr, p6_dev_ptr, stream))
 
+    def render_device_pair(self, camera_a: Camera, camera_b: Camera, opts, rgb_a=None, p6_a=None, rgb_b=None,
+                           p6_b=None, stream: Optional[int] = None) -> None:
+        """Two frames with one launch of the render kernel where it fits them
+        (rt_render_device_pair): the images of two render_device calls."""
+        check(lib().rt_render_device_pair(self._handle(), C.byref(camera_a.c), C.byref(camera_b.c), C.byref(opts),
+                                          rgb_a, p6_a, rgb_b, p6_b, stream))
+
     def kernel_times(self, max_launches: int = 256) -> np.ndarray:
         """ms of the render kernel for the most recent launches (HIP events on its stream)."""
         out = np.zeros(max_launches, np.float32)
@@ -425,6 +432,13 @@ class Renderer:
         t = C.c_uint64()
         check(lib().rt_renderer_submit(self._h, C.byref(camera.c), C.byref(opts), C.byref(t)))
         return t.value
+
+    def submit_pair(self, camera_a: Camera, camera_b: Camera, opts) -> tuple:
+        """Two frames, one render launch per local rank (rt_renderer_submit_pair): their tickets."""
+        t = C.c_uint64()
+        check(lib().rt_renderer_submit_pair(self._h, C.byref(camera_a.c), C.byref(camera_b.c), C.byref(opts),
+                                            C.byref(t)))
+        return t.value, t.value + 1
 
     def wait(self, ticket: int):
         """(address, bytes) of the delivered frame on rank 0's process, else (None, 0)."""

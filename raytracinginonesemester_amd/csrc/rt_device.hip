@@ -133,7 +133,7 @@ struct RenderParams {
     uint32_t* live_count;                             // [k * COUNTER_STRIDE], tile_cull_kernel
     int32_t* live_tiles;                              // nqueues lists of queue_cap entries
     int32_t* cut_tiles;   // tile_cut_kernel's survivors (not culled, not heavy), per list (sc.ncut > 0)
-    uint32_t* next_count; // the other counter set, zeroed by tile_cull_kernel for the next frame
+    uint32_t* next_count; // the counter set of the frame after next, zeroed by tile_cull_kernel
     int32_t cut_force;    // test every candidate in tile_cut_kernel (no pass-through)
     int32_t nqueues;
     int32_t queue_cap;
@@ -2113,9 +2113,9 @@ __device__ __forceinline__ void cull_tiles(const RenderParams& P, int tile) {
 // Pass 1, one lane per tile: the root test; the survivors go to the live lists.
 __global__ __launch_bounds__(BLOCK) void tile_cull_kernel(RenderParams P) {
     __builtin_amdgcn_s_setprio(3);  // ahead of the previous frame's render waves (see Launch)
-    // Counter sets rotate over three frames (no reset launch): this frame's set was zeroed by
-    // the previous frame's pass; zero the next frame's (its last user, frame k-2, has finished:
-    // the scene's prep stream waited for it).
+    // Counter sets rotate over six frames (no reset launch): this frame's set was zeroed by the
+    // pass of the frame two before it; zero the set of the frame two after it (its last user,
+    // frame k-4, has finished: the scene's prep stream waited for it).
     if (blockIdx.x == 0 && threadIdx.x < COUNTER_SLOTS) P.next_count[threadIdx.x * COUNTER_STRIDE] = 0u;
 #ifdef RT_FRAME_SPAN
     if (threadIdx.x == 0 && g_frame_span) atomicMin(&g_frame_span[4 * (P.drain_tag & 255u) + 2], wall_clock64());
@@ -2448,10 +2448,81 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, uin
 #define RT_RENDER_WAVES_BIG 8
 #endif
 constexpr size_t kBigSceneBytes = size_t(64) << 20;
+// Two frames in one launch (RT_TUNE_PAIR_FRAMES, rt_renderer_submit_pair): frame A's parameters,
+// then frame B's, one kernel argument.
+struct PairParams {
+    RenderParams f[2];
+};
+
+// Two frames in one render launch (render_pair_kernel) take their pre-passes in one launch
+// each too: four dependent launches in the previous pair kernel's tail measured 51 us between
+// pair kernels (profiles/r05/exp/pair_timeline_c3.log).  The frames' counter sets and lists are
+// disjoint (a cull pass zeroes the set two frames ahead, rt_scene::kSets).
+// tile_cull_kernel over both frames: frame A's blocks, then frame B's.
+__global__ __launch_bounds__(BLOCK) void tile_cull_pair_kernel(PairParams PP) {
+    __builtin_amdgcn_s_setprio(3);
+    const int nba = (PP.f[0].tiles_total + BLOCK - 1) / BLOCK;
+    const bool b = (int)blockIdx.x >= nba;
+    const RenderParams& P = b ? PP.f[1] : PP.f[0];
+    const int bx = b ? (int)blockIdx.x - nba : (int)blockIdx.x;
+    if (bx == 0 && threadIdx.x < COUNTER_SLOTS) P.next_count[threadIdx.x * COUNTER_STRIDE] = 0u;
+    cull_tiles(P, bx * BLOCK + (int)threadIdx.x);
+}
+
+// tile_cut_kernel over both frames: every wave takes its (list, group) units of frame A, then
+// of frame B.
+__global__ __launch_bounds__(BLOCK) void tile_cut_pair_kernel(PairParams PP) {
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t lane = lane_id();
+    const int waves = (int)(gridDim.x * (BLOCK / 64));
+    for (int f = 0; f < 2; ++f) {
+        const RenderParams& P = f ? PP.f[1] : PP.f[0];
+        float box[6] = {0.f, 0.f, 0.f, -1.f, -1.f, -1.f};
+        int max_len;
+        const bool test = cut_setup(P, lane, box, max_len);
+        for (int p = (int)(blockIdx.x * (BLOCK / 64) + threadIdx.x / 64);; p += waves) {
+            const int q = p % P.nqueues, g = p / P.nqueues;
+            if (CUT_GROUP * g >= max_len) break;
+            (void)cut_unit(P, lane, q, g, test, box);
+        }
+    }
+}
+
+// The pair kernel's item e of queue q: the two frames' heavy lists class by class (A's class k,
+// then B's, so the heaviest items of both start first), then A's survivors, then B's.  which:
+// the frame; returns the tile, cls its class as work_tile's.
+__device__ __forceinline__ int pair_tile(const RenderParams& A, const RenderParams& B, int q, int e, int& which,
+                                         int& cls) {
+    for (int k = 0; k < NCLASS; ++k) {
+        const int na = A.heavy_cap > 0 ? min((int)ldc_u32(A.live_count + heavy_counter(k, q)), A.heavy_cap) : 0;
+        if (e < na) {
+            which = 0;
+            cls = k;
+            return (int)ldc_u32(reinterpret_cast<const uint32_t*>(A.heavy_tiles) + ((size_t)k * 8 + q) * A.heavy_cap + e);
+        }
+        e -= na;
+        const int nb = B.heavy_cap > 0 ? min((int)ldc_u32(B.live_count + heavy_counter(k, q)), B.heavy_cap) : 0;
+        if (e < nb) {
+            which = 1;
+            cls = k;
+            return (int)ldc_u32(reinterpret_cast<const uint32_t*>(B.heavy_tiles) + ((size_t)k * 8 + q) * B.heavy_cap + e);
+        }
+        e -= nb;
+    }
+    cls = NCLASS;
+    const int ra = (int)ldc_u32(&A.live_count[(A.sc.ncut > 0 ? CUT_SLOT0 + q : q) * COUNTER_STRIDE]);
+    which = e < ra ? 0 : 1;
+    const RenderParams& X = e < ra ? A : B;
+    if (e >= ra) e -= ra;
+    return (int)ldc_u32(reinterpret_cast<const uint32_t*>(X.sc.ncut > 0 ? X.cut_tiles : X.live_tiles) +
+                        (size_t)q * X.queue_cap + e);
+}
+
 // Heavy-first dispatch: the queues hand out the heavy lists first; the waves record their
-// items' costs.
-template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0>
-__global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
+// items' costs.  PAIR: the kernel argument is a PairParams; the items of both frames come from
+// frame A's queue heads (pair_tile), and frame B's parameters carry the pre-pass gate.
+template <int MODE, bool SAMPLES, bool D1, int WAVES, int LS, bool PAIR>
+__device__ __forceinline__ void render_tiles_body() {
     constexpr int WPT = BLOCK / 64;  // waves per tile
     __shared__ float col[SAMPLES ? BLOCK * 3 : 1];
     __shared__ int kpix[SAMPLES ? BLOCK : 1];
@@ -2476,14 +2547,15 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
         KernargP pp = (KernargP)__builtin_amdgcn_kernarg_segment_ptr();
         uint32_t bx = blockIdx.x;
         asm volatile("" : "+s"(pp), "+s"(bx));
-        const RenderParams& R = *(const RenderParams*)pp;
+        const RenderParams& R0 = *(const RenderParams*)pp;
+        const RenderParams& RG = PAIR ? *(const RenderParams*)(pp + 1) : R0;  // the gate's frame
         const int g = (int)(bx & 7);
-        const int q = R.nqueues == 1 ? 0 : g;
-        uint32_t* head = R.live_count + (HEAD_SLOT0 + g) * COUNTER_STRIDE;
-        const bool blockwise = SAMPLES && R.spp > 64;
+        const int q = R0.nqueues == 1 ? 0 : g;
+        uint32_t* head = R0.live_count + (HEAD_SLOT0 + g) * COUNTER_STRIDE;
+        const bool blockwise = SAMPLES && R0.spp > 64;
         const uint32_t lane = fresh_lane_id();
 #ifdef RT_FRAME_SPAN
-        if (first && lane == 0 && g_frame_span) atomicMin(&g_frame_span[4 * (R.drain_tag & 255u)], wall_clock64());
+        if (first && lane == 0 && g_frame_span) atomicMin(&g_frame_span[4 * (RG.drain_tag & 255u)], wall_clock64());
 #endif
         const int tid = (int)((wv << 6) | lane);
         const uint32_t per_queue = (gridDim.x >> 3) * (blockwise ? 1u : (uint32_t)WPT);  // first items
@@ -2500,25 +2572,38 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
             j = per_queue + dequeue(head, lane);
         }
         int heavy;
-        const int n = work_length(R, q, heavy);
-        const int e = (R.nqueues == 1 ? g : 0) + (R.nqueues == 1 ? 8 : 1) * (int)(blockwise ? j : j / WPT);
+        int n = work_length(R0, q, heavy);
+        if constexpr (PAIR) {
+            int hb;
+            n += work_length(RG, q, hb);
+        }
+        const int e = (R0.nqueues == 1 ? g : 0) + (R0.nqueues == 1 ? 8 : 1) * (int)(blockwise ? j : j / WPT);
         // the waves at the queue's gate item (its items are handed out in order, so every queue
         // has them; gate_q8 = 256: the first waves past its end) open the next frame's
         // pre-passes (a vector store to host memory)
-        if (R.drained && lane == 0) {
-            const int ge = (int)(((int64_t)n * R.gate_q8) >> 8);
-            if (e >= ge && e < ge + (R.nqueues == 1 ? 8 : 1))
-                __hip_atomic_store(R.drained, R.drain_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (RG.drained && lane == 0) {
+            const int ge = (int)(((int64_t)n * RG.gate_q8) >> 8);
+            if (e >= ge && e < ge + (R0.nqueues == 1 ? 8 : 1))
+                __hip_atomic_store(RG.drained, RG.drain_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if (e >= n) {
 #ifdef RT_FRAME_SPAN
-            if (lane == 0 && g_frame_span) atomicMax(&g_frame_span[4 * (R.drain_tag & 255u) + 1], wall_clock64());
+            if (lane == 0 && g_frame_span) atomicMax(&g_frame_span[4 * (RG.drain_tag & 255u) + 1], wall_clock64());
 #endif
             break;
         }
         const uint32_t qw = blockwise ? wv : j % WPT;
         int cls;
-        const int tile = work_tile(R, q, e, heavy, cls);
+        KernargP pr = pp;  // the item's frame
+        int tile;
+        if constexpr (PAIR) {
+            int which;
+            tile = pair_tile(R0, RG, q, e, which, cls);
+            pr = pp + which;
+        } else {
+            tile = work_tile(R0, q, e, heavy, cls);
+        }
+        const RenderParams& R = *(const RenderParams*)pr;
         // Issue priority by cost class: every SIMD keeps all its wave slots busy until the queues
         // drain, so the heaviest items (the kernel's critical path, started first) would share
         // their SIMD with six other waves throughout; ahead of the rest they finish sooner
@@ -2576,6 +2661,16 @@ __global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams
         }
 #endif
     }
+}
+
+template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0>
+__global__ __launch_bounds__(BLOCK, WAVES) void render_tiles_kernel(RenderParams P) {
+    render_tiles_body<MODE, SAMPLES, D1, WAVES, LS, false>();
+}
+
+template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0>
+__global__ __launch_bounds__(BLOCK, WAVES) void render_pair_kernel(PairParams P) {
+    render_tiles_body<MODE, SAMPLES, D1, WAVES, LS, true>();
 }
 
 // ---- HW1 brute force (HW1/src/render.cpp:72-116) ----------------------------------------
@@ -3191,6 +3286,9 @@ struct rt_scene {
     // written, ~5 us between back-to-back kernels (scripts/micro/kernel_gap.hip); the
     // renderer's frames time one in RT_TUNE_KERNEL_TIMING_EVERY
     bool timed[kRing] = {};
+    // frames of the slot's render launch: 2 for the frames of a pair (rt::render_pair; frame A's
+    // events bracket the pair kernel, frame B's ev1 is recorded after it), else 1
+    uint8_t span[kRing] = {};
     // evq: recorded on the caller's stream at the start of a frame; the prep stream waits for it
     // so the pre-passes (which write the culled tiles' pixels into the caller's buffers) come
     // after everything the caller queued on that stream before the call.  A caller that orders
@@ -3208,11 +3306,14 @@ struct rt_scene {
     uint64_t drain_frame = ~0ull;
     uint64_t est_next = 0;  // the oldest frame not yet seen finished (heavy-threshold estimate)
     size_t bytes = 0;
-    // Work buffers rotate over kSets per frame (frame k: set k % 3; its cull pass zeroes the
-    // counters of set k+1, last used by frame k-2).  A frame launched on another stream than
-    // the previous one first waits for that frame.  A frame whose launches failed part-way
-    // leaves the counter sets unknown: the next frame zeroes them all.
-    static constexpr int kSets = 3;
+    // Work buffers rotate over kSets per frame (frame k: set k % 6; its cull pass zeroes the
+    // counters of set k+2, last used by frame k-4, so the two frames of a pair never touch each
+    // other's sets and their pre-passes run side by side).  Six sets: the two frames of a
+    // running pair kernel, the next pair's two, whose pre-passes run in its tail, and the two
+    // sets those zero.  A frame launched on another stream than the previous one first waits for
+    // that frame.  A frame whose launches failed part-way leaves the counter sets unknown: the
+    // next frame zeroes them all.
+    static constexpr int kSets = 6;
     hipStream_t last_stream = nullptr;
     bool counters_dirty = false;
     // the previous frame's output ranges (device byte ranges): overlapping outputs serialise
@@ -3993,6 +4094,43 @@ void launch_render(const RenderParams& P, const Launch& L) {
     hipExtLaunchKernelGGL(KERNEL, grid, dim3(BLOCK), 0, L.st, L.start, L.stop, 0, P);
 }
 
+// Two frames, one persistent grid (render_pair_kernel): the grid launch_render gives one frame,
+// at most one block per tile of the two.
+template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0>
+void launch_render_pair(const RenderParams& A, const RenderParams& B, const Launch& L) {
+    constexpr auto KERNEL = render_pair_kernel<MODE, SAMPLES, D1, WAVES, LS>;
+    static const int per_cu = [] {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, KERNEL, BLOCK, 0) != hipSuccess || n < 1) n = 1;
+        return n;
+    }();
+    static const std::string name = "render_pair_kernel<" + std::to_string(MODE) + (SAMPLES ? ", true" : ", false") +
+                                    (D1 ? ", true, " : ", false, ") + std::to_string(WAVES) + ", " +
+                                    std::to_string(LS) + ">";
+    if (L.name) *L.name = name.c_str();
+    const int tiles8 = (A.tiles_total + B.tiles_total + 7) / 8 * 8;
+    // RT_TUNE_PAIR_RESERVE: block slots per CU left to the next pair's pre-passes
+    const int reserve = int(std::clamp(rt::tuning(RT_TUNE_PAIR_RESERVE, 0.0), 0.0, double(per_cu - 1)));
+    const dim3 grid((unsigned)std::max(8, std::min(tiles8, L.cus * (per_cu - reserve) / 8 * 8)));
+    PairParams PP;
+    PP.f[0] = A;
+    PP.f[1] = B;
+    hipExtLaunchKernelGGL(KERNEL, grid, dim3(BLOCK), 0, L.st, L.start, L.stop, 0, PP);
+}
+
+// The frames a pair kernel is instantiated for: depth-1 sample kernels of the 4-ary-record wave
+// traversal on a scene within kBigSceneBytes, full or half waves (c3 and its band shards).
+// Anything else renders a pair as two launches.
+bool pair_kernel_fits(const RenderParams& P, bool samples, bool wave_wide, bool big) {
+    return samples && wave_wide && !big && P.max_depth == 1 && P.nqueues == 8 && P.spp <= 64 && !P.ray_count &&
+           P.lane_samples == 1;
+}
+void launch_pair(const RenderParams& A, const RenderParams& B, const Launch& L) {
+    constexpr int M = RT_KERNEL_WAVE | MODE_WIDE | MODE_PK;  // launch_mode's D1_MODE for these
+    if (A.half_waves) launch_render_pair<M, true, true, RT_RENDER_WAVES, 1>(A, B, L);
+    else launch_render_pair<M, true, true>(A, B, L);
+}
+
 template <int MODE, bool SAMPLES>
 void launch_mode(const RenderParams& P, const Launch& L) {
     // depth-1 kernels of the wave traversal: packed box tests (box_ends_pk)
@@ -4102,8 +4240,79 @@ extern "C" int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_rend
     return rt_render_device_p6(s, cam, o, rgb, hit_idx, hit_t, nullptr, stream);
 }
 
+namespace {
+// Two frames in one render launch (rt::render_pair).  Frame A's call runs its pre-passes and,
+// when the pair kernel fits it (pair_kernel_fits, RT_TUNE_PAIR_FRAMES on), keeps its parameters
+// here instead of launching; frame B's call runs its pre-passes and launches both.  A frame B
+// that cannot join (another tile geometry or cut, a failed call) launches A on its own first.
+struct PairStage {
+    int phase = 0;          // 0: frame A's call, 1: frame B's
+    bool deferred = false;  // frame A's render launch is held here
+    RenderParams A;
+    Launch LA{};
+    uint64_t kA = 0;
+    hipStream_t stream = nullptr;
+};
+
+// A frame's pre-passes on the scene's prep stream; ev0 / pdone: their start and end, recorded
+// by the dispatches themselves.
+int launch_prepasses(rt_scene* s, const RenderParams& P, int slot) {
+    const bool cut = P.cull && P.sc.ncut > 0;
+    hipExtLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s->prep,
+                          s->ev0[slot], cut ? nullptr : s->pdone[slot], 0, P);
+    HIP_TRY(hipGetLastError());
+    if (cut) {
+        // 16 waves per CU; each takes (list, group) pairs grid-stride (c3: about one each)
+        const int cut_blocks = 4 * s->cus;
+        hipExtLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, s->prep, nullptr, s->pdone[slot], 0, P);
+        HIP_TRY(hipGetLastError());
+    }
+    return RT_OK;
+}
+
+int flush_pair_a(rt_scene* s, PairStage& ps) {
+    if (!ps.deferred) return RT_OK;
+    ps.deferred = false;
+    const int slot = int(ps.kA % rt_scene::kRing);
+    s->span[slot] = 1;
+    if (int rc = launch_prepasses(s, ps.A, slot); rc != RT_OK) return rc;
+    HIP_TRY(hipStreamWaitEvent(ps.LA.st, s->pdone[slot], 0));
+    launch<RT_KERNEL_WAVE | MODE_WIDE>(ps.A, true, ps.LA);
+    HIP_TRY(hipGetLastError());
+    if (ps.A.drained) s->drain_frame = ps.kA;
+    return RT_OK;
+}
+
+int render_frame(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, float* rgb, int32_t* hit_idx,
+                 float* hit_t, uint8_t* p6, void* stream, PairStage* ps);
+}  // namespace
+
 extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, float* rgb,
                                    int32_t* hit_idx, float* hit_t, uint8_t* p6, void* stream) {
+    return render_frame(s, cam, o, rgb, hit_idx, hit_t, p6, stream, nullptr);
+}
+
+extern "C" int rt_render_device_pair(rt_scene* s, const rt_camera* cam_a, const rt_camera* cam_b,
+                                     const rt_render_opts* o, float* rgb_a, uint8_t* p6_a, float* rgb_b,
+                                     uint8_t* p6_b, void* stream) {
+    if (!s || !cam_a || !cam_b || !o || (!rgb_a && !p6_a) || (!rgb_b && !p6_b))
+        return set_error(RT_ERR_ARG, "rt_render_device_pair: null argument");
+    PairStage ps;
+    int rc = render_frame(s, cam_a, o, rgb_a, nullptr, nullptr, p6_a, stream, &ps);
+    if (rc != RT_OK) return rc;
+    ps.phase = 1;
+    rc = render_frame(s, cam_b, o, rgb_b, nullptr, nullptr, p6_b, stream, &ps);
+    if (ps.deferred) {  // frame B failed before its launch: frame A still renders
+        DeviceGuard g(s->device);
+        const int rc2 = flush_pair_a(s, ps);
+        if (rc == RT_OK) rc = rc2;
+    }
+    return rc;
+}
+
+namespace {
+int render_frame(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, float* rgb, int32_t* hit_idx,
+                 float* hit_t, uint8_t* p6, void* stream, PairStage* ps) {
     if (!s || !cam || !o || (!rgb && !p6)) return set_error(RT_ERR_ARG, "rt_render_device: null argument");
     if (o->spp < 1) return set_error(RT_ERR_ARG, "spp must be >= 1");
     if ((hit_idx == nullptr) != (hit_t == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
@@ -4245,11 +4454,26 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     // scanned forward from the oldest one not yet seen finished (amortised one query per
     // frame), so a caller that submits many frames ahead of the GPU still gets an estimate once
     // its first frames finish (a look-back over the last three frames found none: all in flight).
+    // frame B of a pair whose frame A waits in ps: its tiles and cut must be A's
+    bool pair_b = ps && ps->phase == 1 && ps->deferred;
+    if (pair_b) {
+        const RenderParams& A = ps->A;
+        const bool same = A.tiles_total == P.tiles_total && A.tiles_x == P.tiles_x && A.W == P.W && A.rows == P.rows &&
+                          A.spp == P.spp && A.half_waves == P.half_waves && A.sc.ncut == P.sc.ncut && A.cull == P.cull &&
+                          A.heavy_cap == P.heavy_cap && A.queue_cap == P.queue_cap && A.nqueues == P.nqueues &&
+                          A.max_depth == P.max_depth && A.band_index == P.band_index &&
+                          A.band_count == P.band_count && ps->stream == static_cast<hipStream_t>(stream);
+        if (!same) {
+            pair_b = false;
+            if ((rc = flush_pair_a(s, *ps)) != RT_OK) return rc;
+        }
+    }
     bool cost_reset = false;
     if (costs) {
         uint64_t f = std::max<uint64_t>(s->est_next, k >= uint64_t(rt_scene::kRing) ? k - (rt_scene::kRing - 1) : 0);
         int64_t last = -1;
-        for (; f < k; ++f) {
+        const uint64_t f_end = ps && ps->deferred ? k - 1 : k;  // frame A's events are not recorded yet
+        for (; f < f_end; ++f) {
             if (hipEventQuery(s->ev1[f % rt_scene::kRing]) != hipSuccess) break;
             last = int64_t(f);
         }
@@ -4257,11 +4481,14 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         if (last >= 0) {
             const int fl = int(uint64_t(last) % rt_scene::kRing);
             // the render kernel's time, or the frame period when shorter (overlapping frames:
-            // RT_FLAG_OVERLAP starts a kernel while the previous one still runs)
+            // RT_FLAG_OVERLAP starts a kernel while the previous one still runs); a pair
+            // kernel's time per frame
             float ms = 0.f, period = 0.f;
             if (s->timed[fl] && hipEventElapsedTime(&ms, s->evm[fl], s->ev1[fl]) == hipSuccess) {
                 const int f0 = int(uint64_t(last - 1) % rt_scene::kRing);
-                if (last >= 1 && hipEventElapsedTime(&period, s->ev1[f0], s->ev1[fl]) == hipSuccess && period > 0.f)
+                if (s->span[fl] > 1) ms /= float(s->span[fl]);
+                else if (last >= 1 && s->span[f0] == 1 &&
+                         hipEventElapsedTime(&period, s->ev1[f0], s->ev1[fl]) == hipSuccess && period > 0.f)
                     ms = std::min(ms, period);
                 s->kernel_ms_est = ms;
             }
@@ -4314,6 +4541,16 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     for (const auto& a : out_now)
         for (const auto& b : s->prev_out)
             overlap = overlap || (a.lo < a.hi && b.lo < b.hi && a.lo < b.hi && b.lo < a.hi);
+    if (pair_b && overlap) {  // frame B writes over frame A: A renders first, on its own
+        pair_b = false;
+        if ((rc = flush_pair_a(s, *ps)) != RT_OK) return rc;
+    }
+    const size_t big_bytes = size_t(std::max(0.0, rt::tuning(RT_TUNE_BIG_SCENE_BYTES, double(kBigSceneBytes))));
+    const bool ovl = s->caller_ordered && rt::tuning(RT_TUNE_OVERLAP_FRAMES, 0.0) > 0.5;
+    // frame A of a pair: its launch waits for frame B's call (PairStage)
+    const bool pair_a = ps && ps->phase == 0 && rt::tuning(RT_TUNE_PAIR_FRAMES, 1.0) > 0.5 && !ovl &&
+                        pair_kernel_fits(P, samples, !s->deep && mode == RT_KERNEL_WAVE && P.sc.wide != 0,
+                                         s->bytes > big_bytes);
     // the previous frame of this scene ran on another stream: wait for it.  (Letting two frames'
     // render kernels overlap on two streams, the next filling the CUs the last waves of the
     // previous one leave idle, measured slower for rt_renderer: 0.257 vs 0.246 ms per c3 frame.)
@@ -4323,7 +4560,7 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         if (k > 1) HIP_TRY(hipStreamWaitEvent(st, ev1_of(k - 2), 0));
     }
     s->last_stream = st;
-    const int set = int(k % rt_scene::kSets), nset = int((k + 1) % rt_scene::kSets);
+    const int set = int(k % rt_scene::kSets), nset = int((k + 2) % rt_scene::kSets);
     char* base = static_cast<char*>(s->work.p);
     char* lists = base + rt_scene::kSets * kCounterBytes + set * set_bytes;
     P.live_count = reinterpret_cast<uint32_t*>(base + set * kCounterBytes);
@@ -4337,8 +4574,16 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     auto frame = [&]() -> int {
         hipStream_t pp = s->prep;
         P.drain_tag = uint32_t(k + 1);
-        // set k was last read by frame k-3, set k+1 (zeroed by this cull pass) by frame k-2
-        if (k >= 2) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 2), 0));
+        // set k was last read by frame k-6, set k+2 (zeroed by this cull pass) by frame k-4: a
+        // frame waits for frame k-2 (the render kernel before the one its pre-passes overlap).
+        // Frame A of a pair, k, waits for frame k-3 (the pair before the one running: frames
+        // up to k-3 used the sets the pair reads and zeroes) and covers frame B: the pair's
+        // pre-passes are launched together, after B's call has set B up.
+        if (pair_a) {
+            if (k >= 3) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 3), 0));
+        } else if (!pair_b && k >= 2) {
+            HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 2), 0));
+        }
         if (k >= 1 && overlap) HIP_TRY(hipStreamWaitEvent(pp, ev1_of(k - 1), 0));
         // the pre-pass gate: frame k-1's render kernel opens it when its first queue drains
         if (k >= 1 && s->drain_frame == k - 1)
@@ -4352,29 +4597,45 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
             s->counters_dirty = false;
         }
         if (cost_reset) HIP_TRY(hipMemsetAsync(s->cost.p, 0, s->cost.n, pp));  // no heavy tiles yet
-        // ev0 / pdone: the pre-passes' start and end, recorded by the dispatches themselves
-        const bool cut = P.cull && P.sc.ncut > 0;
-        hipExtLaunchKernelGGL(tile_cull_kernel, dim3((P.tiles_total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, pp,
-                              s->ev0[slot], cut ? nullptr : s->pdone[slot], 0, P);
-        HIP_TRY(hipGetLastError());
-        if (cut) {
-            // 16 waves per CU; each takes (list, group) pairs grid-stride (c3: about one each)
-            const int cut_blocks = 4 * s->cus;
-            hipExtLaunchKernelGGL(tile_cut_kernel, dim3(cut_blocks), dim3(BLOCK), 0, pp, nullptr, s->pdone[slot], 0, P);
+        // frame A of a pair: its pre-passes go out with frame B's (pair_b below, or flush_pair_a)
+        if (pair_b) {
+            // both frames' passes in one cull and one cut launch (the same cut: the pair's tile
+            // geometry check); frame A's events bracket them, frame B's follow
+            const int slot_a = int(ps->kA % rt_scene::kRing);
+            PairParams PP;
+            PP.f[0] = ps->A;
+            PP.f[1] = P;
+            // (frame B's pdone is the last launch's own end event: the render stream waits for it)
+            const bool cut = P.cull && P.sc.ncut > 0;
+            HIP_TRY(hipEventRecord(s->ev0[slot], pp));  // both frames' pre-pass times span the pair's
+            hipExtLaunchKernelGGL(tile_cull_pair_kernel,
+                                  dim3((ps->A.tiles_total + BLOCK - 1) / BLOCK + (P.tiles_total + BLOCK - 1) / BLOCK),
+                                  dim3(BLOCK), 0, pp, s->ev0[slot_a], cut ? nullptr : s->pdone[slot], 0, PP);
             HIP_TRY(hipGetLastError());
+            if (cut) {
+                // 32 waves per CU (the cut kernel's occupancy): the pair's cut mostly runs after
+                // the previous pair kernel has left the GPU, latency-bound per unit
+                hipExtLaunchKernelGGL(tile_cut_pair_kernel, dim3(8 * s->cus), dim3(BLOCK), 0, pp, nullptr,
+                                      s->pdone[slot], 0, PP);
+                HIP_TRY(hipGetLastError());
+            }
+            HIP_TRY(hipEventRecord(s->pdone[slot_a], pp));
+        } else if (!pair_a) {
+            if ((rc = launch_prepasses(s, P, slot)) != RT_OK) return rc;
         }
         // RT_TUNE_OVERLAP_FRAMES: the render kernel on one of the scene's two render streams (the
         // caller orders its buffers itself; its stream then waits for the kernel), else on the
         // caller's stream
-        const bool ovl = s->caller_ordered && rt::tuning(RT_TUNE_OVERLAP_FRAMES, 0.0) > 0.5;
         const hipStream_t rs = ovl ? s->rstream[k & 1] : st;
-        HIP_TRY(hipStreamWaitEvent(rs, s->pdone[slot], 0));
-        const size_t big_bytes = size_t(std::max(0.0, rt::tuning(RT_TUNE_BIG_SCENE_BYTES, double(kBigSceneBytes))));
+        // (frame A of a pair: frame B's pdone, later on the same prep stream, covers both)
+        if (!pair_a) HIP_TRY(hipStreamWaitEvent(rs, s->pdone[slot], 0));
         const bool qr = P.sc.qent != nullptr && P.sc.f_log2 > 2;
         // RT_TUNE_KERNEL_TIMING_EVERY: the caller-ordered (rt_renderer) frames record the render
-        // kernel's start event in one frame of this many (direct calls: every frame)
+        // kernel's start event in one frame of this many (direct calls: every frame); a pair
+        // kernel's start is frame A's (frame B's slot is never timed)
         const uint64_t every = uint64_t(std::clamp(rt::tuning(RT_TUNE_KERNEL_TIMING_EVERY, 4.0), 1.0, 256.0));
-        s->timed[slot] = !s->caller_ordered || k % every == 0;
+        s->timed[slot] = !pair_b && (!s->caller_ordered || k % every == 0 || (pair_a && (k + 1) % every == 0));
+        s->span[slot] = pair_a || pair_b ? 2 : 1;
         const Launch L{rs, s->timed[slot] ? s->evm[slot] : nullptr, s->ev1[slot], s->cus, s->bytes > big_bytes, qr,
                        &s->last_kernel};
         // RT_TUNE_PREPASS_GATE f in (0, 1]: this kernel opens the next frame's pre-passes when
@@ -4387,6 +4648,29 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
         P.drained = gate ? s->drain : nullptr;
         P.drain_tag = uint32_t(k + 1);
         P.gate_q8 = int(std::clamp(gate_f, 0.0, 1.0) * 256.0 + 0.5);
+        if (pair_a) {  // held for frame B's call
+            ps->A = P;
+            ps->LA = L;
+            ps->kA = k;
+            ps->stream = st;
+            ps->deferred = true;
+            return RT_OK;
+        }
+        if (pair_b) {
+            // one grid over both frames: frame A's events bracket it (its start event when A is a
+            // timed frame), frame B's end event follows; frame B's parameters carry the gate
+            const int slot_a = int(ps->kA % rt_scene::kRing);
+            RenderParams A = ps->A;
+            A.drained = nullptr;
+            const Launch LP{rs, s->timed[slot_a] ? s->evm[slot_a] : nullptr, s->ev1[slot_a], s->cus, false, false,
+                            &s->last_kernel};
+            ps->deferred = false;
+            launch_pair(A, P, LP);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(s->ev1[slot], rs));
+            if (gate) s->drain_frame = k;
+            return RT_OK;
+        }
         if (s->deep) launch<MODE_DEEP>(P, samples, L);
         else if (mode == RT_KERNEL_LANE) launch<RT_KERNEL_LANE>(P, samples, L);
         else if (P.sc.wide) launch<RT_KERNEL_WAVE | MODE_WIDE>(P, samples, L);
@@ -4403,15 +4687,16 @@ extern "C" int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_r
     if (rc != RT_OK) s->counters_dirty = true;
     return rc;
 }
+}  // namespace
 
 void rt::scene_set_caller_ordered(rt_scene* s, bool on) {
     if (s) s->caller_ordered = on;
 }
 
-void rt::scene_frame_events(const rt_scene* s, hipEvent_t* first, hipEvent_t* last) {
+void rt::scene_frame_events(const rt_scene* s, hipEvent_t* first, hipEvent_t* last, int back) {
     hipEvent_t a = nullptr, b = nullptr;
-    if (s && s->launches > 0) {
-        const int slot = int((s->launches - 1) % rt_scene::kRing);
+    if (s && s->launches > uint64_t(back)) {
+        const int slot = int((s->launches - 1 - uint64_t(back)) % rt_scene::kRing);
         a = s->ev0[slot];
         b = s->ev1[slot];
     }

@@ -67,7 +67,8 @@ struct DeviceGuard {
 // before its first launch and after its render kernel, both on the frame's stream and owned
 // by the scene (valid for the scene's next 255 frames); nullptr before the first frame.
 // rt_renderer synchronises on these instead of recording events of its own on that stream.
-void scene_frame_events(const rt_scene* s, hipEvent_t* first, hipEvent_t* last);
+// back: the frame that many frames before the most recent (1: frame A of a pair just rendered).
+void scene_frame_events(const rt_scene* s, hipEvent_t* first, hipEvent_t* last, int back = 0);
 // A caller that orders the reuse of its output buffers itself (rt_renderer: host waits per
 // frame slot) lets a scene's frame pre-passes skip the wait for the work queued before the
 // frame on its stream, so they overlap the previous frame's render kernel (rt_device.hip).

@@ -988,61 +988,52 @@ extern "C" rt_scene* rt_renderer_scene(rt_renderer* r, int i) {
 }
 extern "C" int rt_renderer_local_ranks(const rt_renderer* r) { return r ? int(r->ranks.size()) : 0; }
 
-extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt_render_opts* opts, uint64_t* ticket) {
-    if (!r || !cam || !opts) return set_error(RT_ERR_ARG, "rt_renderer_submit: null argument");
-    if (cam->pixel_width < 1 || cam->pixel_height < 1) return set_error(RT_ERR_ARG, "camera has no pixels");
-    int rc = ensure_geometry(r, cam->pixel_width, cam->pixel_height);
+namespace {
+// rt_renderer_submit (nf = 1) and rt_renderer_submit_pair (nf = 2: frames t and t+1 in two
+// slots, one render launch per local rank, rt_render_device_pair).
+int submit_frames(rt_renderer* r, const rt_camera* const* cams, int nf, const rt_render_opts* opts, uint64_t* ticket) {
+    for (int f = 0; f < nf; ++f) {
+        if (!r || !cams[f] || !opts) return set_error(RT_ERR_ARG, "rt_renderer_submit: null argument");
+        if (cams[f]->pixel_width < 1 || cams[f]->pixel_height < 1) return set_error(RT_ERR_ARG, "camera has no pixels");
+    }
+    int rc = ensure_geometry(r, cams[0]->pixel_width, cams[0]->pixel_height);
     if (rc != RT_OK) return rc;
-    const uint64_t t = r->next;
-    const int s = int(t % uint64_t(r->depth));
-    // The slot's previous frame is waited for here, on the host: the streams below need no
-    // waits for buffer reuse (every wait or event on the compute stream costs GPU time between
-    // the frame's kernels).
-    if ((rc = wait_slot(r, s)) != RT_OK) return rc;
-    const int ring = int(t % kTimeRing);
+    const uint64_t t0 = r->next;
+    uint64_t tk[2];
+    int sl[2], rg[2];
+    char* dsts[2] = {nullptr, nullptr};
     const bool f32 = r->deliver == RT_DELIVER_F32;
     const bool rccl_mode = r->uses_rccl();
     const bool self_send = rccl_mode && (r->flags & RT_RENDERER_SELF_SEND);
     const bool shared = r->host_shared();
     LocalRank& R0 = r->ranks[0];
-    // HOST_SHARED: rank 0's caller gives up frame t - depth with this submit
-    if (shared && r->rank0_local && t + 1 >= uint64_t(r->depth))
-        SharedFrames::raise_to(r->shared->word(kOffReleased), t + 1 - uint64_t(r->depth));
-    for (int k = 0; k < 3; ++k) r->ta[k][ring] = r->tb[k][ring] = nullptr;
     const hipMemcpyKind kind = r->deliver == RT_DELIVER_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    char* dst = nullptr;
-    if (r->deliver != RT_DELIVER_NONE && (r->rank0_local || shared))
-        dst = static_cast<char*>(r->deliver == RT_DELIVER_DEVICE ? r->dev_frame[s].p : r->host[s]);
-    for (LocalRank& L : r->ranks) L.rendered[s] = L.released[s] = nullptr;
-    if (r->rank0_local) r->delivered[s] = nullptr;
-    // 1. every local rank renders its bands into strip[s] (the scene's frame and nothing else on
-    // its compute stream); DIRECT / HOST_SHARED: then copies its own bands into their rows of
+    for (int f = 0; f < nf; ++f) {
+        const uint64_t t = tk[f] = t0 + uint64_t(f);
+        const int s = sl[f] = int(t % uint64_t(r->depth));
+        // The slot's previous frame is waited for here, on the host: the streams below need no
+        // waits for buffer reuse (every wait or event on the compute stream costs GPU time
+        // between the frame's kernels).
+        if ((rc = wait_slot(r, s)) != RT_OK) return rc;
+        const int ring = rg[f] = int(t % kTimeRing);
+        // HOST_SHARED: rank 0's caller gives up frame t - depth with this submit
+        if (shared && r->rank0_local && t + 1 >= uint64_t(r->depth))
+            SharedFrames::raise_to(r->shared->word(kOffReleased), t + 1 - uint64_t(r->depth));
+        for (int k = 0; k < 3; ++k) r->ta[k][ring] = r->tb[k][ring] = nullptr;
+        if (r->deliver != RT_DELIVER_NONE && (r->rank0_local || shared))
+            dsts[f] = static_cast<char*>(r->deliver == RT_DELIVER_DEVICE ? r->dev_frame[s].p : r->host[s]);
+        for (LocalRank& L : r->ranks) L.rendered[s] = L.released[s] = nullptr;
+        if (r->rank0_local) r->delivered[s] = nullptr;
+    }
+    // 1. every local rank renders its bands into strip[s] (the scene's frames and nothing else
+    // on its compute stream); DIRECT / HOST_SHARED: then copies its own bands into their rows of
     // the host frame over its own PCIe link (the same job, so with several GPUs in this process
     // each rank's host work runs on its own thread).
     const bool copies = !rccl_mode && r->deliver != RT_DELIVER_NONE;
-    auto rank_job = [&](int i) -> int {
-        LocalRank& L = r->ranks[i];
-        const bool own = &L == &R0 && r->rank0_local;  // rank 0's copy: delivered_ev below
-        if (L.rows > 0) {
-            DeviceGuard g(L.device);
-            rt_render_opts o = *opts;
-            o.band_rows = r->band_rows;
-            o.band_index = L.rank;
-            o.band_count = r->world;
-            void* buf = L.strip[s].p;
-            // the renderer waits for buffer reuse on the host: its own frames skip the scene's
-            // wait for work queued before them on the compute stream (there is none but its
-            // frames).  Only for this call: a borrowed view (rt_renderer_scene) stays stream-ordered.
-            rt::scene_set_caller_ordered(L.scene, true);
-            int q = rt_render_device_p6(L.scene, cam, &o, f32 ? static_cast<float*>(buf) : nullptr, nullptr, nullptr,
-                                        f32 ? nullptr : static_cast<uint8_t*>(buf), L.compute);
-            rt::scene_set_caller_ordered(L.scene, false);
-            if (q != RT_OK) return q;
-            hipEvent_t first = nullptr;
-            rt::scene_frame_events(L.scene, &first, &L.rendered[s]);
-            if (own) r->ta[RT_TIME_FRAME][ring] = first;
-        }
-        if (!copies) return RT_OK;
+    auto copy_job = [&](LocalRank& L, bool own, int f) -> int {
+        const uint64_t t = tk[f];
+        const int s = sl[f], ring = rg[f];
+        char* dst = dsts[f];
         // With a frame shared by the job's processes, a rank other than 0's first waits for rank
         // 0's caller to give up this slot's previous frame (rank 0 publishes that at its submit).
         if (shared && !r->rank0_local && t + 1 >= uint64_t(r->depth) && L.rendered[s]) {
@@ -1073,105 +1064,172 @@ extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt
         }
         return RT_OK;
     };
-    if ((rc = r->pool.run(int(r->ranks.size()), rank_job)) != RT_OK) return rc;
-    r->slot_ticket[s] = t + 1;
-    r->next = t + 1;
-    if (ticket) *ticket = t;
-    if (r->deliver == RT_DELIVER_NONE) {
-        for (LocalRank& L : r->ranks) L.released[s] = L.rendered[s];
-        if (r->rank0_local) r->delivered[s] = r->tb[RT_TIME_FRAME][ring] = R0.rendered[s];
-        return RT_OK;
-    }
-    if (rccl_mode) {
-        // 2. strips -> rank 0 (one group: every send and receive of this process)
-        const Rccl& N = rccl();
-        for (LocalRank& L : r->ranks) {
+    auto rank_job = [&](int i) -> int {
+        LocalRank& L = r->ranks[i];
+        const bool own = &L == &R0 && r->rank0_local;  // rank 0's copy: delivered_ev below
+        if (L.rows > 0) {
             DeviceGuard g(L.device);
-            if (L.rendered[s]) HIP_TRY(hipStreamWaitEvent(L.comm, L.rendered[s], 0));
-            if (&L == &R0 && r->rank0_local) HIP_TRY(hipEventRecord(r->tg0[ring], L.comm));
-        }
-        NCCL_TRY(N.GroupStart());
-        for (LocalRank& L : r->ranks) {
-            if (L.rank == 0 && !self_send) continue;
-            const size_t bytes = size_t(L.rows) * r->row_bytes;
-            if (bytes == 0) continue;
-            const ncclResult_t e = N.Send(L.strip[s].p, bytes, ncclUint8, 0, L.nccl, L.comm);
-            if (e != ncclSuccess) {
-                (void)N.GroupEnd();
-                return nccl_error(e, "ncclSend");
+            rt_render_opts o = *opts;
+            o.band_rows = r->band_rows;
+            o.band_index = L.rank;
+            o.band_count = r->world;
+            void* buf[2] = {L.strip[sl[0]].p, L.strip[sl[nf - 1]].p};
+            // the renderer waits for buffer reuse on the host: its own frames skip the scene's
+            // wait for work queued before them on the compute stream (there is none but its
+            // frames).  Only for this call: a borrowed view (rt_renderer_scene) stays stream-ordered.
+            rt::scene_set_caller_ordered(L.scene, true);
+            int q;
+            if (nf == 2)
+                q = rt_render_device_pair(L.scene, cams[0], cams[1], &o, f32 ? static_cast<float*>(buf[0]) : nullptr,
+                                          f32 ? nullptr : static_cast<uint8_t*>(buf[0]),
+                                          f32 ? static_cast<float*>(buf[1]) : nullptr,
+                                          f32 ? nullptr : static_cast<uint8_t*>(buf[1]), L.compute);
+            else
+                q = rt_render_device_p6(L.scene, cams[0], &o, f32 ? static_cast<float*>(buf[0]) : nullptr, nullptr,
+                                        nullptr, f32 ? nullptr : static_cast<uint8_t*>(buf[0]), L.compute);
+            rt::scene_set_caller_ordered(L.scene, false);
+            if (q != RT_OK) return q;
+            for (int f = 0; f < nf; ++f) {
+                hipEvent_t first = nullptr;
+                rt::scene_frame_events(L.scene, &first, &L.rendered[sl[f]], nf - 1 - f);
+                if (own) r->ta[RT_TIME_FRAME][rg[f]] = first;
             }
         }
-        if (r->rank0_local) {
-            char* g0 = static_cast<char*>(r->gathered[s].p);
-            for (int q = self_send ? 0 : 1; q < r->world; ++q) {
-                const size_t bytes = size_t(rt_shard_rows(r->H, r->band_rows, q, r->world)) * r->row_bytes;
+        if (!copies) return RT_OK;
+        for (int f = 0; f < nf; ++f)
+            if (int q = copy_job(L, own, f); q != RT_OK) return q;
+        return RT_OK;
+    };
+    if ((rc = r->pool.run(int(r->ranks.size()), rank_job)) != RT_OK) return rc;
+    for (int f = 0; f < nf; ++f) r->slot_ticket[sl[f]] = tk[f] + 1;
+    r->next = t0 + uint64_t(nf);
+    if (ticket) *ticket = t0;
+    // 2. per frame: the gather (RCCL) or the completion of the copies
+    auto finish = [&](int f) -> int {
+        const uint64_t t = tk[f];
+        const int s = sl[f], ring = rg[f];
+        char* dst = dsts[f];
+        if (r->deliver == RT_DELIVER_NONE) {
+            for (LocalRank& L : r->ranks) L.released[s] = L.rendered[s];
+            if (r->rank0_local) r->delivered[s] = r->tb[RT_TIME_FRAME][ring] = R0.rendered[s];
+            return RT_OK;
+        }
+        if (rccl_mode) {
+            // 2. strips -> rank 0 (one group: every send and receive of this process)
+            const Rccl& N = rccl();
+            for (LocalRank& L : r->ranks) {
+                DeviceGuard g(L.device);
+                if (L.rendered[s]) HIP_TRY(hipStreamWaitEvent(L.comm, L.rendered[s], 0));
+                if (&L == &R0 && r->rank0_local) HIP_TRY(hipEventRecord(r->tg0[ring], L.comm));
+            }
+            NCCL_TRY(N.GroupStart());
+            for (LocalRank& L : r->ranks) {
+                if (L.rank == 0 && !self_send) continue;
+                const size_t bytes = size_t(L.rows) * r->row_bytes;
                 if (bytes == 0) continue;
-                const ncclResult_t e = N.Recv(g0 + size_t(q) * r->strip_cap, bytes, ncclUint8, q, R0.nccl, R0.comm);
+                const ncclResult_t e = N.Send(L.strip[s].p, bytes, ncclUint8, 0, L.nccl, L.comm);
                 if (e != ncclSuccess) {
                     (void)N.GroupEnd();
-                    return nccl_error(e, "ncclRecv");
+                    return nccl_error(e, "ncclSend");
                 }
             }
-        }
-        NCCL_TRY(N.GroupEnd());
-        for (LocalRank& L : r->ranks) {
-            if ((L.rank != 0 || self_send) && L.rows > 0) {  // the send was the strip's last reader
-                DeviceGuard g(L.device);
-                HIP_TRY(hipEventRecord(L.released_ev[s], L.comm));
-                L.released[s] = L.released_ev[s];
+            if (r->rank0_local) {
+                char* g0 = static_cast<char*>(r->gathered[s].p);
+                for (int q = self_send ? 0 : 1; q < r->world; ++q) {
+                    const size_t bytes = size_t(rt_shard_rows(r->H, r->band_rows, q, r->world)) * r->row_bytes;
+                    if (bytes == 0) continue;
+                    const ncclResult_t e = N.Recv(g0 + size_t(q) * r->strip_cap, bytes, ncclUint8, q, R0.nccl, R0.comm);
+                    if (e != ncclSuccess) {
+                        (void)N.GroupEnd();
+                        return nccl_error(e, "ncclRecv");
+                    }
+                }
             }
+            NCCL_TRY(N.GroupEnd());
+            for (LocalRank& L : r->ranks) {
+                if ((L.rank != 0 || self_send) && L.rows > 0) {  // the send was the strip's last reader
+                    DeviceGuard g(L.device);
+                    HIP_TRY(hipEventRecord(L.released_ev[s], L.comm));
+                    L.released[s] = L.released_ev[s];
+                }
+            }
+            // 3. rank 0: every strip to its image rows
+            if (r->rank0_local) {
+                DeviceGuard g(R0.device);
+                HIP_TRY(hipEventRecord(r->tg1[ring], R0.comm));
+                HIP_TRY(hipStreamWaitEvent(R0.copy, r->tg1[ring], 0));
+                if (!self_send && R0.rendered[s]) HIP_TRY(hipStreamWaitEvent(R0.copy, R0.rendered[s], 0));
+                HIP_TRY(hipEventRecord(r->td0[ring], R0.copy));
+                const char* g0 = static_cast<const char*>(r->gathered[s].p);
+                for (int q = 0; q < r->world; ++q) {
+                    const char* src = (q == 0 && !self_send) ? static_cast<const char*>(R0.strip[s].p)
+                                                             : g0 + size_t(q) * r->strip_cap;
+                    HIP_TRY(scatter_strip(dst, src, q, r->world, r->H, r->band_rows, r->row_bytes, kind, R0.copy));
+                }
+                HIP_TRY(hipEventRecord(r->td1[ring], R0.copy));
+                HIP_TRY(hipEventRecord(r->delivered_ev[s], R0.copy));
+                r->delivered[s] = r->delivered_ev[s];
+                if (!self_send && R0.rows > 0) R0.released[s] = r->delivered_ev[s];
+                r->ta[RT_TIME_GATHER][ring] = r->tg0[ring];
+                r->tb[RT_TIME_GATHER][ring] = r->tg1[ring];
+                r->ta[RT_TIME_DELIVER][ring] = r->td0[ring];
+                r->tb[RT_TIME_DELIVER][ring] = r->tb[RT_TIME_FRAME][ring] = r->td1[ring];
+            }
+            return RT_OK;
         }
-        // 3. rank 0: every strip to its image rows
+        // 2'. DIRECT / HOST_SHARED: the copies went out with the ranks' jobs; rank 0's frame is
+        // complete when every local copy is.
+        if (r->dma && R0.rendered[s]) {  // SDMA: the strip is free and the frame delivered with the copy
+            r->delivered[s] = nullptr;
+            R0.released[s] = nullptr;
+            r->ta[RT_TIME_DELIVER][ring] = r->tb[RT_TIME_DELIVER][ring] = r->tb[RT_TIME_FRAME][ring] = nullptr;
+            r->dma_timed[ring] = false;
+            return RT_OK;
+        }
         if (r->rank0_local) {
             DeviceGuard g(R0.device);
-            HIP_TRY(hipEventRecord(r->tg1[ring], R0.comm));
-            HIP_TRY(hipStreamWaitEvent(R0.copy, r->tg1[ring], 0));
-            if (!self_send && R0.rendered[s]) HIP_TRY(hipStreamWaitEvent(R0.copy, R0.rendered[s], 0));
-            HIP_TRY(hipEventRecord(r->td0[ring], R0.copy));
-            const char* g0 = static_cast<const char*>(r->gathered[s].p);
-            for (int q = 0; q < r->world; ++q) {
-                const char* src = (q == 0 && !self_send) ? static_cast<const char*>(R0.strip[s].p)
-                                                         : g0 + size_t(q) * r->strip_cap;
-                HIP_TRY(scatter_strip(dst, src, q, r->world, r->H, r->band_rows, r->row_bytes, kind, R0.copy));
-            }
+            for (size_t i = 1; i < r->ranks.size(); ++i)  // the frame is complete when every local copy is
+                if (r->ranks[i].released[s]) HIP_TRY(hipStreamWaitEvent(R0.copy, r->ranks[i].released[s], 0));
             HIP_TRY(hipEventRecord(r->td1[ring], R0.copy));
             HIP_TRY(hipEventRecord(r->delivered_ev[s], R0.copy));
             r->delivered[s] = r->delivered_ev[s];
-            if (!self_send && R0.rows > 0) R0.released[s] = r->delivered_ev[s];
-            r->ta[RT_TIME_GATHER][ring] = r->tg0[ring];
-            r->tb[RT_TIME_GATHER][ring] = r->tg1[ring];
+            if (R0.rendered[s]) R0.released[s] = r->delivered_ev[s];
             r->ta[RT_TIME_DELIVER][ring] = r->td0[ring];
             r->tb[RT_TIME_DELIVER][ring] = r->tb[RT_TIME_FRAME][ring] = r->td1[ring];
         }
+        if (shared) {
+            maybe_unlink(r);
+            // ranks with no rows have nothing to copy: their share of frame t is complete
+            for (const LocalRank& L : r->ranks)
+                if (!L.rendered[s]) SharedFrames::raise_to(r->shared->done(L.rank), t + 1);
+        }
         return RT_OK;
-    }
-    // 2'. DIRECT / HOST_SHARED: the copies went out with the ranks' jobs; rank 0's frame is
-    // complete when every local copy is.
-    if (r->dma && R0.rendered[s]) {  // SDMA: the strip is free and the frame delivered with the copy
-        r->delivered[s] = nullptr;
-        R0.released[s] = nullptr;
-        r->ta[RT_TIME_DELIVER][ring] = r->tb[RT_TIME_DELIVER][ring] = r->tb[RT_TIME_FRAME][ring] = nullptr;
-        r->dma_timed[ring] = false;
-        return RT_OK;
-    }
-    if (r->rank0_local) {
-        DeviceGuard g(R0.device);
-        for (size_t i = 1; i < r->ranks.size(); ++i)  // the frame is complete when every local copy is
-            if (r->ranks[i].released[s]) HIP_TRY(hipStreamWaitEvent(R0.copy, r->ranks[i].released[s], 0));
-        HIP_TRY(hipEventRecord(r->td1[ring], R0.copy));
-        HIP_TRY(hipEventRecord(r->delivered_ev[s], R0.copy));
-        r->delivered[s] = r->delivered_ev[s];
-        if (R0.rendered[s]) R0.released[s] = r->delivered_ev[s];
-        r->ta[RT_TIME_DELIVER][ring] = r->td0[ring];
-        r->tb[RT_TIME_DELIVER][ring] = r->tb[RT_TIME_FRAME][ring] = r->td1[ring];
-    }
-    if (shared) {
-        maybe_unlink(r);
-        // ranks with no rows have nothing to copy: their share of frame t is complete
-        for (const LocalRank& L : r->ranks)
-            if (!L.rendered[s]) SharedFrames::raise_to(r->shared->done(L.rank), t + 1);
-    }
+    };
+    for (int f = 0; f < nf; ++f)
+        if ((rc = finish(f)) != RT_OK) return rc;
     return RT_OK;
+}
+}  // namespace
+
+extern "C" int rt_renderer_submit(rt_renderer* r, const rt_camera* cam, const rt_render_opts* opts, uint64_t* ticket) {
+    const rt_camera* cams[1] = {cam};
+    return submit_frames(r, cams, 1, opts, ticket);
+}
+
+extern "C" int rt_renderer_submit_pair(rt_renderer* r, const rt_camera* cam_a, const rt_camera* cam_b,
+                                       const rt_render_opts* opts, uint64_t* ticket_a) {
+    if (!r || !cam_a || !cam_b || !opts) return set_error(RT_ERR_ARG, "rt_renderer_submit_pair: null argument");
+    if (r->depth < 2) return set_error(RT_ERR_ARG, "rt_renderer_submit_pair: needs depth >= 2 (two frame slots)");
+    // one frame size: else as two submits
+    if (cam_a->pixel_width != cam_b->pixel_width || cam_a->pixel_height != cam_b->pixel_height) {
+        uint64_t t = 0;
+        int rc = rt_renderer_submit(r, cam_a, opts, &t);
+        if (rc == RT_OK) rc = rt_renderer_submit(r, cam_b, opts, nullptr);
+        if (ticket_a) *ticket_a = t;
+        return rc;
+    }
+    const rt_camera* cams[2] = {cam_a, cam_b};
+    return submit_frames(r, cams, 2, opts, ticket_a);
 }
 
 extern "C" int rt_renderer_wait(rt_renderer* r, uint64_t ticket, const void** frame, size_t* bytes) {

@@ -12,7 +12,7 @@ import numpy as np
 rows = list(csv.DictReader(open(sys.argv[1])))
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows), key=lambda x: x[0])
-ren = [k for k in ks if "render_tiles_kernel" in k[2]]
+ren = [k for k in ks if "render_tiles_kernel" in k[2] or "render_pair_kernel" in k[2]]
 pre = [k for k in ks if "tile_cull_kernel" in k[2] or "tile_cut_kernel" in k[2]]
 gaps, durs, out = [], [], []
 for i in range(max(1, len(ren) - n), len(ren)):

@@ -3,7 +3,7 @@
 # per frame the render kernel, the gap before it and where the pre-passes ran.
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$ROOT/gpurun_out/trace_bench
+OUT=$ROOT/gpurun_out/trace_bench${TRACE_TAG:-}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$OUT" -o run -- \

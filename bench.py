@@ -85,9 +85,11 @@ def parse():
     # frames in flight: 2 on one GPU (render k+1 while frame k's P6 is copied: 0.2170 vs 0.2233
     # ms per frame at 3, 0.328 at 6); 3 over N GPUs
     ap.add_argument("--depth", type=int, default=None)
-    ap.add_argument("--pair", type=int, default=0, choices=[0, 1],
-                    help="1: the frames are submitted two at a time (rt_renderer_submit_pair: one render "
-                         "launch renders both where the pair kernel fits them); 0: one at a time")
+    ap.add_argument("--pair", type=int, default=None, choices=[0, 1],
+                    help="1: the frames are submitted two at a time (rt_renderer_submit_pair: one render launch "
+                         "renders both where the pair kernel fits them); 0: one at a time (lower frame latency); "
+                         "default 1 for the configs the pair kernel takes (depth-1 frames of a scene within "
+                         "RT_TUNE_BIG_SCENE_BYTES: c3 and its band shards), else 0")
     ap.add_argument("--comm", default="native", choices=["native", "torch"],
                     help="native: rt_renderer (librt_mi355x); torch: torch.distributed gather (alternate launcher)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -552,10 +554,15 @@ def load_traffic(path: Path, config: str, instance: str):
     the same kernel instantiation the timed frames launched (profiles/traffic.json records the
     instantiation rocprofv3 named); otherwise None: a line never cites another kernel's bytes."""
     try:
-        tr = json.loads(path.read_text()).get(config)
+        data = json.loads(path.read_text())
     except Exception:
         return None
-    return tr if tr and instance and tr.get("kernel_instance") == instance else None
+    # "<config>" (render_tiles_kernel) or "<config>/<kernel>" (e.g. c3/render_pair_kernel)
+    for key in [config] + sorted(k for k in data if k.startswith(config + "/")):
+        tr = data.get(key)
+        if tr and instance and tr.get("kernel_instance") == instance:
+            return tr
+    return None
 
 
 def primary_hit_parity(ds, cam, cfg, hs, golden: str) -> dict:
@@ -769,6 +776,8 @@ def main():
     hs = rt.HostScene.load_json(sp, REPO if sp.parent == configs.SCENES else sp.parent)
     cam = hs.camera(cfg["width"], cfg["height"])
     W, H, spp = cam.pixel_width, cam.pixel_height, cfg["spp"]
+    if a.pair is None:  # the pair kernel's configs (c5's 345 MB scene takes the big-scene kernels)
+        a.pair = 1 if cfg["max_depth"] == 1 and a.config != "c5" else 0
     PAIR["on"] = bool(a.pair)
     if a.depth is None:  # frames in flight (N = 1: depth 3 keeps the host's waits off the critical
         # path; the driver's 20-step command: 0.171 ms/step vs 0.174-0.262 at depth 2 with SDMA copies,

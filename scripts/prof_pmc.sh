@@ -15,7 +15,7 @@ case "$CFG" in c1|c2) DRIVER=profile_hw1.py ;; esac  # the HW1 path (rt_hw1_scen
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- \
-      python3 "$ROOT/scripts/$DRIVER" --config "$CFG" --frames "$FRAMES" --mode serial > "$OUT/$name.log" 2>&1
+      python3 "$ROOT/scripts/$DRIVER" --config "$CFG" --frames "$FRAMES" --mode serial ${PROF_ARGS:-} > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"
   if [ $rc -ge 124 ]; then exit $rc; fi

@@ -32,6 +32,8 @@ ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--mode", default="serial", choices=["serial", "none", "p6"])
 ap.add_argument("--series", action="store_true", help="also print every timed frame's render-kernel ms")
 ap.add_argument("--busy-ms", type=float, default=0.0, help="keep the GPU busy (matmuls) this long first")
+ap.add_argument("--pair", action="store_true",
+                help="serial: two frames per render launch (rt_render_device_pair), each pair run alone")
 a = ap.parse_args()
 
 cfg = configs.G_CONFIGS[a.config]
@@ -52,12 +54,17 @@ if a.mode == "serial":
     ds = rt.DeviceScene.from_host(hs)
     o, _j = ds.make_opts(**kw)
     buf = torch.empty((cam.pixel_height * cam.pixel_width * 3,), dtype=torch.uint8, device="cuda")
+    buf2 = torch.empty_like(buf)
     st = torch.cuda.current_stream().cuda_stream
     for k in range(n):
         if k == a.warmup:
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-        ds.render_device(cam, o, 0, stream=st, p6_dev_ptr=buf.data_ptr())
+        if a.pair:  # frames = pairs here; nothing overlaps a pair's launches
+            ds.render_device_pair(cam, cam, o, None, buf.data_ptr(), None, buf2.data_ptr(), stream=st)
+            torch.cuda.synchronize()
+        else:
+            ds.render_device(cam, o, 0, stream=st, p6_dev_ptr=buf.data_ptr())
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     sc = ds

@@ -28,7 +28,8 @@ a = ap.parse_args()
 
 
 def short(name):
-    for k in ("render_tiles_kernel", "render_samples_kernel", "tile_cull_kernel", "tile_cut_kernel",
+    for k in ("render_tiles_kernel", "render_pair_kernel", "tile_cull_pair_kernel", "tile_cut_pair_kernel",
+              "render_samples_kernel", "tile_cull_kernel", "tile_cut_kernel",
               "render_hw1_kernel", "render_hw1_chunks_kernel", "hw1_rect_count_kernel", "hw1_scan_chunks_kernel",
               "hw1_fill_kernel", "hw1_resolve_kernel", "copyBuffer", "fillBuffer", "elementwise"):
         if k in name:
@@ -121,7 +122,7 @@ def binding(i):
     name, frac = max(pipes.items(), key=lambda kv: kv[1])
     if frac >= 0.8:
         return f"{name} ({frac:.2f} of peak)"
-    if not a.kernel.startswith("render_tiles"):
+    if not a.kernel.startswith(("render_tiles", "render_pair")):
         return (f"latency: VALU issue {i['valu_issue']:.2f}, SALU issue {i['salu_issue']:.2f}; waves waiting "
                 f"{i['wait_any']:.2f} of their cycles at {i['waves_per_simd']:.1f} waves/SIMD")
     return (f"latency and scalar issue: the per-wave chain scalar node load -> box tests -> ballot -> "
@@ -138,19 +139,20 @@ if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
     write = k["WRITE_SIZE"] * 1024
     tf = REPO / "profiles" / "traffic.json"
     data = json.loads(tf.read_text()) if tf.exists() else {}
-    data[a.config] = {"kernel": a.kernel, "kernel_instance": instance, "bytes_per_launch": round(fetch + write),
+    key = a.config if a.kernel == "render_tiles_kernel" else f"{a.config}/{a.kernel}"  # bench.py load_traffic
+    data[key] = {"kernel": a.kernel, "kernel_instance": instance, "bytes_per_launch": round(fetch + write),
                       "fetch_bytes": round(fetch), "write_bytes": round(write),
                       "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
                                 f"{os.path.basename(a.prof.rstrip('/'))}; FETCH_SIZE x2 (gfx950), KiB->B"}
     # every kernel of the profiled frames (the HW1 path's frame is five launches)
-    data[a.config]["per_kernel"] = {
+    data[key]["per_kernel"] = {
         kn: {"bytes_per_launch": round(2 * cs["FETCH_SIZE"] * 1024 + cs["WRITE_SIZE"] * 1024)}
         for kn, cs in summary.items() if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs}
     iss = issue(k)
     if iss:
-        data[a.config]["issue"] = iss
-        data[a.config]["binding"] = binding(iss)
+        data[key]["issue"] = iss
+        data[key]["binding"] = binding(iss)
     tf.write_text(json.dumps(data, indent=1) + "\n")
-    print(json.dumps(data[a.config]))
+    print(json.dumps(data[key]))
 for name, cs in summary.items():
     print(name, {c: round(v, 1) for c, v in cs.items()})

@@ -180,6 +180,63 @@ def test_shared_host_frame_two_processes(depth, others_wait):
     assert not list(Path("/dev/shm").glob(name[1:] + ".g*")), "shared frames left behind"
 
 
+def _shared_pair_worker(rank, world, port, name, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    rt.set_tuning("peer_timeout_s", 60)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hs = host_scene("frog.json")
+        cams = [hs.camera(W, H), _moved(hs.camera(W, H))]
+        r = rt.Renderer.from_host(hs, devices=(0,), world_size=world, rank0=rank, gather=rt.RT_GATHER_HOST_SHARED,
+                                  host_frame_name=name, depth=4)
+        o, _j = rt.DeviceScene.make_opts(spp=SPP, max_depth=1)
+        got, pend = [], []
+        for k, (a, b) in enumerate([(0, 1), (1, 0), (0, 0), (1, 1), (0, 1)]):
+            while len(pend) > 2:
+                kk, t = pend.pop(0)
+                addr, n = r.wait(t)
+                if rank == 0:
+                    got.append((kk, bytes((C.c_uint8 * n).from_address(addr))))
+            ta, tb = r.submit_pair(cams[a], cams[b], o)
+            pend += [(a, ta), (b, tb)]
+        for kk, t in pend:
+            addr, n = r.wait(t)
+            if rank == 0:
+                got.append((kk, bytes((C.c_uint8 * n).from_address(addr))))
+        r.close()
+        if rank == 0:
+            q.put(got)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shared_host_frame_pairs_two_processes():
+    """rt_renderer_submit_pair in two processes (one band rank each, the pair kernel on each
+    rank's shard) into the shared host frame: every frame the single-frame image."""
+    hs = host_scene("frog.json")
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    want = [_p6_body(ds.render(c, spp=SPP, max_depth=1)) for c in (hs.camera(W, H), _moved(hs.camera(W, H)))]
+    ds.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    name = f"/rt_test_pair_{os.getpid()}"
+    procs = [ctx.Process(target=_shared_pair_worker, args=(rk, 2, port, name, q)) for rk in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert len(got) == 10
+    for k, body in got:
+        assert body == want[k], f"camera {k}"
+    assert not list(Path("/dev/shm").glob(name[1:] + ".g*")), "shared frames left behind"
+
+
 def test_shared_host_frame_needs_a_name():
     hs = host_scene("frog.json")
     with pytest.raises(rt.RTError) as e:

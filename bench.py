@@ -204,6 +204,12 @@ def sync_all(dev, world):
 PAIR = {"on": False}
 
 
+def PAIR_CONFIGS(a, cfg) -> bool:
+    """The configs the pair kernel takes (depth-1 frames of a scene within RT_TUNE_BIG_SCENE_BYTES:
+    c3 and its band shards; c5's 345 MB scene takes the big-scene kernels)."""
+    return cfg["max_depth"] == 1 and a.config != "c5"
+
+
 def run_frames(r, cam, opts, n, depth):
     """Submit n frames, waiting for every one of them (host memory on rank 0), at most depth in
     flight; with --pair 1 two at a time (rt_renderer_submit_pair), an odd last one alone."""
@@ -393,6 +399,19 @@ def native(a, hs, cam, cfg, ctx):
     # secondary: render only (strips stay in HBM), the rate the round-1 bench reported
     rn = make_renderer(hs, ctx, a, rt.RT_DELIVER_NONE, gather, a.depth)
     res["render_only_s"], _ = timed_native(rn, cam, opts, a.steps, a.warmup, a.depth, ctx, a.preroll_ms)
+    # secondary: the other submission mode (two frames per render launch, or one), same frames
+    # and delivery, depth 6 for pairs / 3 for single frames
+    if PAIR_CONFIGS(a, cfg):
+        was = PAIR["on"]
+        PAIR["on"] = not was
+        dp = 6 if PAIR["on"] else 3
+        rp = make_renderer(hs, ctx, a, deliver, gather, dp)
+        el, _ = timed_native(rp, cam, opts, a.steps, a.warmup, dp, ctx, a.preroll_ms)
+        res["other_mode"] = {"pair": PAIR["on"], "s": el, "depth": dp,
+                             "frame_latency_ms": (float(rp.times(rt.RT_TIME_FRAME, a.steps).mean())
+                                                  if ctx.rank == 0 else None)}
+        rp.close()
+        PAIR["on"] = was
     rn.close()
     # secondary: the other payload (f32 = the reference's Vec3 framebuffer), also the float parity
     other = rt.RT_DELIVER_P6 if deliver == rt.RT_DELIVER_F32 else rt.RT_DELIVER_F32
@@ -776,8 +795,13 @@ def main():
     hs = rt.HostScene.load_json(sp, REPO if sp.parent == configs.SCENES else sp.parent)
     cam = hs.camera(cfg["width"], cfg["height"])
     W, H, spp = cam.pixel_width, cam.pixel_height, cfg["spp"]
-    if a.pair is None:  # the pair kernel's configs (c5's 345 MB scene takes the big-scene kernels)
-        a.pair = 1 if cfg["max_depth"] == 1 and a.config != "c5" else 0
+    if a.pair is None:
+        # One frame per launch: the driver's 20-step window is dominated by pipeline fill and
+        # drain, where a pair's two copies come back to back (20 steps: 0.1587-0.1649 ms/step
+        # with pairs vs ~0.16 single; 100 steps: 0.1484 vs 0.1551), and pairs raise the frame
+        # latency (0.76 vs 0.44 ms).  The other mode is measured beside the headline
+        # (timing.other_submission); --pair 1 makes pairs the headline.
+        a.pair = 0
     PAIR["on"] = bool(a.pair)
     if a.depth is None:  # frames in flight (N = 1: depth 3 keeps the host's waits off the critical
         # path; the driver's 20-step command: 0.171 ms/step vs 0.174-0.262 at depth 2 with SDMA copies,
@@ -811,6 +835,8 @@ def main():
     if "render_only_s" in res:
         vals.append(res["render_only_s"])
         vals.append(res["other_payload"]["s"])
+    if "other_mode" in res:
+        vals.append(res["other_mode"]["s"])
     m = ctx.max(vals)
     elapsed, kernel_ms, frame_ms = m[0], m[1], m[2]
     per_rank = None
@@ -935,6 +961,13 @@ def main():
         extra["render_only_value"] = round(samples * a.steps / m[3] / 1e6, 3)
         op = res["other_payload"]
         extra[f"{op['deliver']}_host_value"] = round(samples * op["steps"] / m[4] / 1e6, 3)
+    if "other_mode" in res:
+        om = res["other_mode"]
+        extra["other_submission"] = {
+            "mode": "two frames per render launch (rt_renderer_submit_pair)" if om["pair"] else "one frame per launch",
+            "depth": om["depth"], "value": round(samples * a.steps / m[5] / 1e6, 3),
+            "ms_per_step": round(m[5] / a.steps * 1e3, 4),
+            "frame_latency_ms": None if om["frame_latency_ms"] is None else round(om["frame_latency_ms"], 4)}
     extra["live_tiles"] = res.get("live_tiles")
     if "prepass_ms" in res:
         extra["prepass_ms"] = round(res["prepass_ms"], 4)

@@ -244,8 +244,9 @@ int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_render_opts*
                         void* hip_stream);
 
 /* Two frames of one scene with the same options (two cameras of the same pixel size, e.g. the
- * next two frames of a sequence), as rt_render_device_p6 twice (frame a, then frame b; the
- * same images), rendered by one launch of the render kernel where it fits them
+ * next two frames of a sequence: two iterations of the reference's per-frame render() loop,
+ * G/src/main.cu:362-378), as rt_render_device_p6 twice (frame a, then frame b; the same
+ * images), rendered by one launch of the render kernel where it fits them
  * (RT_TUNE_PAIR_FRAMES): the second frame's work fills the first's tail and the launch gap
  * between two frames goes.  Outputs of a and b must not overlap. */
 int rt_render_device_pair(rt_scene* s, const rt_camera* cam_a, const rt_camera* cam_b,

@@ -1,0 +1,9 @@
+# Round-end check: the whole GPU suite and smoke() on the final build.
+set -u
+mkdir -p gpurun_out
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > gpurun_out/final_gpu_suite.log 2>&1 || { tail -30 gpurun_out/final_gpu_suite.log; exit 1; }
+tail -1 gpurun_out/final_gpu_suite.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/final_smoke.log 2>&1 \
+  || { tail -20 gpurun_out/final_smoke.log; exit 1; }
+tail -1 gpurun_out/final_smoke.log

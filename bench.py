@@ -89,7 +89,8 @@ def parse():
                     help="1: the frames are submitted two at a time (rt_renderer_submit_pair: one render launch "
                          "renders both where the pair kernel fits them); 0: one at a time (lower frame latency); "
                          "default 1 for the configs the pair kernel takes (depth-1 frames of a scene within "
-                         "RT_TUNE_BIG_SCENE_BYTES: c3 and its band shards), else 0")
+                         "RT_TUNE_BIG_SCENE_BYTES: c3 and its band shards), else 0; the other mode is measured "
+                         "beside the headline")
     ap.add_argument("--comm", default="native", choices=["native", "torch"],
                     help="native: rt_renderer (librt_mi355x); torch: torch.distributed gather (alternate launcher)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -796,12 +797,14 @@ def main():
     cam = hs.camera(cfg["width"], cfg["height"])
     W, H, spp = cam.pixel_width, cam.pixel_height, cfg["spp"]
     if a.pair is None:
-        # One frame per launch: the driver's 20-step window is dominated by pipeline fill and
-        # drain, where a pair's two copies come back to back (20 steps: 0.1587-0.1649 ms/step
-        # with pairs vs ~0.16 single; 100 steps: 0.1484 vs 0.1551), and pairs raise the frame
-        # latency (0.76 vs 0.44 ms).  The other mode is measured beside the headline
-        # (timing.other_submission); --pair 1 makes pairs the headline.
-        a.pair = 0
+        # Two frames per launch where the pair kernel takes them: the band
+        # shards of an N-GPU frame gain most (8 shards: render kernel 0.0506 vs 0.0745 ms per
+        # frame, 2 shards 0.0731 vs 0.0922, scripts/pair_shards.py, profiles/r05/exp/pair_shards_c3.log);
+        # one GPU 0.1484 vs 0.1551 ms/step over 100 steps, and even in the driver's 20-step window
+        # (0.1587 / 0.1649 vs ~0.16: its fill and drain eat most of the gain).  The price is frame
+        # latency (0.76 vs 0.44 ms); the single-frame mode is measured beside the headline
+        # (timing.other_submission), and --pair 0 makes it the headline.
+        a.pair = 1 if PAIR_CONFIGS(a, cfg) else 0
     PAIR["on"] = bool(a.pair)
     if a.depth is None:  # frames in flight (N = 1: depth 3 keeps the host's waits off the critical
         # path; the driver's 20-step command: 0.171 ms/step vs 0.174-0.262 at depth 2 with SDMA copies,

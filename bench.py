@@ -464,10 +464,12 @@ def rccl_leg(a, hs, cam, cfg, ctx) -> dict:
 
 def band_shards(hs, cam, cfg, local, steps=20):
     """Each rank's share of a frame at N = 2/4/8, rendered alone on this GPU (the per-rank
-    compute a multi-GPU run will show): frame_ms (cull + cut + render) and kernel_ms."""
+    compute a multi-GPU run will show): frame_ms (cull + cut + render) and kernel_ms, and the
+    render kernel's ms per frame when the shard's frames go two per launch (the bench's default)."""
     ds = rt.DeviceScene.from_host(hs, device=local)
     H, W = cam.pixel_height, cam.pixel_width
     p6 = torch.zeros((H * W * 3,), dtype=torch.uint8, device=torch.device("cuda", local))
+    p6b = torch.zeros_like(p6)
     out = {}
     for n in (2, 4, 8):
         per = []
@@ -483,9 +485,17 @@ def band_shards(hs, cam, cfg, local, steps=20):
             for _ in range(steps):
                 ds.render_device(cam, o, 0, stream=None, p6_dev_ptr=p6.data_ptr())
             torch.cuda.synchronize()
-            per.append((float(ds.frame_times(steps).mean()), float(ds.kernel_times(steps).mean())))
+            kt = float(ds.kernel_times(steps).mean())
+            ft = float(ds.frame_times(steps).mean())
+            # the same shard two frames per launch (rt_render_device_pair): kernel ms per frame
+            for _ in range(steps // 2):
+                ds.render_device_pair(cam, cam, o, None, p6.data_ptr(), None, p6b.data_ptr())
+            torch.cuda.synchronize()
+            kp = float(ds.kernel_times(steps // 2).mean()) / (2 if ds.kernel_name().startswith("render_pair") else 1)
+            per.append((ft, kt, kp))
         fr = [p[0] for p in per]
         out[str(n)] = {"frame_ms": [round(x, 4) for x in fr], "kernel_ms": [round(p[1], 4) for p in per],
+                       "kernel_ms_per_frame_pairs": [round(p[2], 4) for p in per],
                        "max_over_mean": round(max(fr) / (sum(fr) / len(fr)), 4)}
     ds.close()
     return out

@@ -23,7 +23,10 @@ from raytracinginonesemester_amd import _lib as L, configs  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--bands", type=int, default=8)
 ap.add_argument("--frames", type=int, default=200)
+ap.add_argument("--tune", action="append", default=[], help="knob=value (repeatable)")
 a = ap.parse_args()
+for kv in a.tune:
+    rt.set_tuning(kv.split("=")[0], float(kv.split("=")[1]))
 
 cfg = configs.G_CONFIGS["c3"]
 sp = configs.scene_path(cfg["scene"])
@@ -60,7 +63,7 @@ for idx in range(a.bands):
                      "kernel": ds.kernel_name()}
     out.append(row)
     print(json.dumps(row), flush=True)
-print(json.dumps({"bands": a.bands,
+print(json.dumps({"bands": a.bands, "tune": a.tune,
                   "max_kernel_ms_per_frame": {m: max(r[m]["kernel_ms_per_frame"] for r in out) for m in ("single", "pair")},
                   "max_ms_per_frame": {m: max(r[m]["ms_per_frame"] for r in out) for m in ("single", "pair")}}))
 ds.close()

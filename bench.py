@@ -925,6 +925,10 @@ def main():
         roof.update(achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
                     achieved_from="measured HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
                                   f"{tr.get('source', '?')}) / live kernel_ms")
+        if roof["frames_per_launch"] > 1:
+            # a pair launch fetches about what one frame's launch does (the scene's records once),
+            # so its GB/s falls while the bytes per frame halve
+            roof["traffic_per_frame"] = round(traffic / roof["frames_per_launch"])
         if tr.get("compulsory_bytes_per_launch"):
             roof["compulsory_bytes_per_launch"] = tr["compulsory_bytes_per_launch"]
             roof["compulsory_GBps"] = round(tr["compulsory_bytes_per_launch"] / (kernel_ms / 1e3) / 1e9, 2)

@@ -438,7 +438,7 @@ def rccl_leg(a, hs, cam, cfg, ctx) -> dict:
     for name, dl in (("device", rt.RT_DELIVER_DEVICE), ("host_p6", rt.RT_DELIVER_P6)):
         rr, err = None, ""
         try:
-            rr = make_renderer(hs, ctx, a, dl, rt.RT_GATHER_RCCL, 3)
+            rr = make_renderer(hs, ctx, a, dl, rt.RT_GATHER_RCCL, 6 if PAIR["on"] else 3)
         except rt.RTError as e:
             err = str(e)
         if ctx.max([1.0 if err else 0.0])[0] > 0:  # some rank failed: no rank runs the leg
@@ -446,7 +446,7 @@ def rccl_leg(a, hs, cam, cfg, ctx) -> dict:
             if rr is not None:
                 rr.close()
             continue
-        el, last = timed_native(rr, cam, opts, a.steps, a.warmup, 3, ctx)
+        el, last = timed_native(rr, cam, opts, a.steps, a.warmup, 6 if PAIR["on"] else 3, ctx)
         el = ctx.max([el])[0]
         d = {"value": round(cfg["spp"] * cam.pixel_width * cam.pixel_height * a.steps / el / 1e6, 3),
              "ms_per_step": round(el / a.steps * 1e3, 4)}

@@ -967,6 +967,9 @@ def main():
         line["rays_unit"] = ("Mrays/s: total = camera + shadow + bounce rays; traced = the same with only the "
                              "camera rays of tiles the exact culling passes leave to the render kernel")
     extra = {"kernel_ms": round(kernel_ms, 4), "frame_ms": round(frame_ms, 4)}
+    if roof.get("frames_per_launch", 1) > 1:  # kernel_ms is per launch: two frames
+        extra["kernel_ms_per_frame"] = round(kernel_ms / roof["frames_per_launch"], 4)
+        extra["kernel_ms_note"] = "kernel_ms: one render_pair_kernel launch, two frames (DESIGN.md §4.15)"
     for k in ("gather_ms", "deliver_ms", "frame_latency_ms"):
         if k in res:
             extra[k] = round(res[k], 4)

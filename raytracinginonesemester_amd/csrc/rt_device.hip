@@ -4112,8 +4112,10 @@ void launch_render_pair(const RenderParams& A, const RenderParams& B, const Laun
     // RT_TUNE_PAIR_RESERVE: block slots per CU left to the next pair's pre-passes, which then run
     // beside this kernel instead of after it (c3: 0.148 ms per delivered frame vs 0.151 with
     // none and 0.157 with two, profiles/r05/exp/pair_knobs_c3.log)
-    const int reserve = int(std::clamp(rt::tuning(RT_TUNE_PAIR_RESERVE, 1.0), 0.0, double(per_cu - 1)));
-    const dim3 grid((unsigned)std::max(8, std::min(tiles8, L.cus * (per_cu - reserve) / 8 * 8)));
+    // (fractions: that many slots per CU on average, e.g. 0.5 = one on every other CU)
+    const double reserve = std::clamp(rt::tuning(RT_TUNE_PAIR_RESERVE, 1.0), 0.0, double(per_cu - 1));
+    const int blocks = L.cus * per_cu - int(std::lround(reserve * L.cus));
+    const dim3 grid((unsigned)std::max(8, std::min(tiles8, blocks / 8 * 8)));
     PairParams PP;
     PP.f[0] = A;
     PP.f[1] = B;

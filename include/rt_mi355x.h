@@ -540,7 +540,7 @@ typedef enum {
                                     instantiated for them (depth-1 sample kernels of the wave
                                     traversal, scene within RT_TUNE_BIG_SCENE_BYTES); 0 two launches */
     RT_TUNE_PAIR_RESERVE = 19,   /* pair kernels: block slots per CU left free for the next pair's pre-passes
-                                    (1 default) */
+                                    (1 default; fractions: that many per CU on average) */
     RT_TUNE_COUNT = 20
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */

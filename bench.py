@@ -206,9 +206,10 @@ PAIR = {"on": False}
 
 
 def PAIR_CONFIGS(a, cfg) -> bool:
-    """The configs the pair kernel takes (depth-1 frames of a scene within RT_TUNE_BIG_SCENE_BYTES:
-    c3 and its band shards; c5's 345 MB scene takes the big-scene kernels)."""
-    return cfg["max_depth"] == 1 and a.config != "c5"
+    """The configs the pair kernel takes: depth-1 frames of a scene within RT_TUNE_BIG_SCENE_BYTES
+    (c3 and its band shards; c5's 345 MB scene takes the big-scene kernels) and one-light
+    multi-bounce frames on the paired-only bounce kernels (c3b)."""
+    return a.config in ("c3", "c3b")
 
 
 def run_frames(r, cam, opts, n, depth):

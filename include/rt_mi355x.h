@@ -538,9 +538,11 @@ typedef enum {
     RT_TUNE_PAIR_FRAMES = 18,    /* rt_render_device_pair / rt_renderer_submit_pair: 1 (default) renders the
                                     two frames in one launch of the render kernel where it is
                                     instantiated for them (depth-1 sample kernels of the wave
-                                    traversal, scene within RT_TUNE_BIG_SCENE_BYTES); 0 two launches */
+                                    traversal and the paired-only bounce kernels, scene within
+                                    RT_TUNE_BIG_SCENE_BYTES); 0 two launches */
     RT_TUNE_PAIR_RESERVE = 19,   /* pair kernels: block slots per CU left free for the next pair's pre-passes
-                                    (1 default; fractions: that many per CU on average) */
+                                    (default 1 for depth-1 frames, 0 for the bounce kernels'
+                                    pairs; fractions: that many per CU on average) */
     RT_TUNE_COUNT = 20
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */

@@ -4097,7 +4097,7 @@ void launch_render(const RenderParams& P, const Launch& L) {
 // Two frames, one persistent grid (render_pair_kernel): the grid launch_render gives one frame,
 // at most one block per tile of the two.
 template <int MODE, bool SAMPLES, bool D1, int WAVES = RT_RENDER_WAVES, int LS = 0>
-void launch_render_pair(const RenderParams& A, const RenderParams& B, const Launch& L) {
+void launch_render_pair(const RenderParams& A, const RenderParams& B, const Launch& L, double reserve_default) {
     constexpr auto KERNEL = render_pair_kernel<MODE, SAMPLES, D1, WAVES, LS>;
     static const int per_cu = [] {
         int n = 0;
@@ -4111,9 +4111,11 @@ void launch_render_pair(const RenderParams& A, const RenderParams& B, const Laun
     const int tiles8 = (A.tiles_total + B.tiles_total + 7) / 8 * 8;
     // RT_TUNE_PAIR_RESERVE: block slots per CU left to the next pair's pre-passes, which then run
     // beside this kernel instead of after it (c3: 0.148 ms per delivered frame vs 0.151 with
-    // none and 0.157 with two, profiles/r05/exp/pair_knobs_c3.log)
-    // (fractions: that many slots per CU on average, e.g. 0.5 = one on every other CU)
-    const double reserve = std::clamp(rt::tuning(RT_TUNE_PAIR_RESERVE, 1.0), 0.0, double(per_cu - 1));
+    // none and 0.157 with two, profiles/r05/exp/pair_knobs_c3.log; fractions: that many slots
+    // per CU on average).  The bounce kernels' pairs reserve none by default: a 1.2 ms kernel
+    // hides its pre-passes anyway, and a slot is a quarter of their 4 waves per SIMD (c3b 1.53
+    // ms per frame with one, 1.13 with none, profiles/r05/exp/pair_c3b.log).
+    const double reserve = std::clamp(rt::tuning(RT_TUNE_PAIR_RESERVE, reserve_default), 0.0, double(per_cu - 1));
     const int blocks = L.cus * per_cu - int(std::lround(reserve * L.cus));
     const dim3 grid((unsigned)std::max(8, std::min(tiles8, blocks / 8 * 8)));
     PairParams PP;
@@ -4125,14 +4127,20 @@ void launch_render_pair(const RenderParams& A, const RenderParams& B, const Laun
 // The frames a pair kernel is instantiated for: depth-1 sample kernels of the 4-ary-record wave
 // traversal on a scene within kBigSceneBytes, full or half waves (c3 and its band shards).
 // Anything else renders a pair as two launches.
+// Multi-bounce frames take it too where launch_mode picks the paired-only bounce kernels (one
+// light, half waves, LS = 3: c3b): their longest items bound a launch, and a pair overlaps two
+// frames' longest items.
 bool pair_kernel_fits(const RenderParams& P, bool samples, bool wave_wide, bool big) {
-    return samples && wave_wide && !big && P.max_depth == 1 && P.nqueues == 8 && P.spp <= 64 && !P.ray_count &&
+    const bool d1 = P.max_depth == 1;
+    const bool bounce = P.max_depth > 1 && P.half_waves && P.paired_only;
+    return samples && wave_wide && !big && (d1 || bounce) && P.nqueues == 8 && P.spp <= 64 && !P.ray_count &&
            P.lane_samples == 1;
 }
 void launch_pair(const RenderParams& A, const RenderParams& B, const Launch& L) {
     constexpr int M = RT_KERNEL_WAVE | MODE_WIDE | MODE_PK;  // launch_mode's D1_MODE for these
-    if (A.half_waves) launch_render_pair<M, true, true, RT_RENDER_WAVES, 1>(A, B, L);
-    else launch_render_pair<M, true, true>(A, B, L);
+    if (A.max_depth > 1) launch_render_pair<RT_KERNEL_WAVE | MODE_WIDE, true, false, RT_PAIRED_WAVES, 3>(A, B, L, 0.0);
+    else if (A.half_waves) launch_render_pair<M, true, true, RT_RENDER_WAVES, 1>(A, B, L, 1.0);
+    else launch_render_pair<M, true, true>(A, B, L, 1.0);
 }
 
 template <int MODE, bool SAMPLES>
@@ -4465,7 +4473,7 @@ int render_frame(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, flo
         const bool same = A.tiles_total == P.tiles_total && A.tiles_x == P.tiles_x && A.W == P.W && A.rows == P.rows &&
                           A.spp == P.spp && A.half_waves == P.half_waves && A.sc.ncut == P.sc.ncut && A.cull == P.cull &&
                           A.heavy_cap == P.heavy_cap && A.queue_cap == P.queue_cap && A.nqueues == P.nqueues &&
-                          A.max_depth == P.max_depth && A.band_index == P.band_index &&
+                          A.max_depth == P.max_depth && A.paired_only == P.paired_only && A.band_index == P.band_index &&
                           A.band_count == P.band_count && ps->stream == static_cast<hipStream_t>(stream);
         if (!same) {
             pair_b = false;

@@ -133,14 +133,58 @@ def test_pair_band_shards(frog, band_count, band_index):
         ds.close()
 
 
+def test_pair_multi_bounce(frog):
+    """The paired-only bounce kernels (one light, half waves: c3b's) as a pair kernel: pipelined
+    pairs of 8-bounce diffuse frames, each its single-frame image."""
+    ds = rt.DeviceScene.from_host(frog, device=0)
+    try:
+        cams = _cams(frog, 480, 270)
+        for kw in (dict(spp=16, max_depth=8), dict(spp=4, max_depth=3), dict(spp=16, max_depth=8, diffuse_bounce=False)):
+            o, _j = rt.DeviceScene.make_opts(miss_color=frog.settings["miss_color"], **kw)
+            want = _singles(ds, cams, ["base", "moved"], o, 270, 480)
+            bufs = _bufs(6, 270, 480)
+            seq = [("base", "moved"), ("moved", "base"), ("base", "base")]
+            for i, (a, b) in enumerate(seq):
+                (ra, pa), (rb, pb) = bufs[2 * i], bufs[2 * i + 1]
+                ds.render_device_pair(cams[a], cams[b], o, ra.data_ptr(), pa.data_ptr(), rb.data_ptr(), pb.data_ptr())
+            torch.cuda.synchronize()
+            assert ds.kernel_name() == "render_pair_kernel<17, true, false, 4, 3>", (kw, ds.kernel_name())
+            for i, (a, b) in enumerate(seq):
+                for k, nm in ((2 * i, a), (2 * i + 1, b)):
+                    rgb, p6 = bufs[k]
+                    assert p6.cpu().numpy().tobytes() == want[nm][1], (kw, i, nm)
+                    assert rgb.cpu().numpy().view(np.uint32).tobytes() == want[nm][0], (kw, i, nm)
+    finally:
+        ds.close()
+
+
+def test_pair_c3b_full_frames(frog):
+    """c3b (frog.json as shipped: 8 diffuse bounces, 1080p x 16 spp) as pairs: both frames the
+    reference's own image (tests/golden/scenes/c3b_full)."""
+    ppm = gzip.open(GOLDEN / "scenes" / "c3b_full" / "image.ppm.gz").read()
+    ds = rt.DeviceScene.from_host(frog, device=0)
+    try:
+        cam = frog.camera(W, H)
+        o, _j = rt.DeviceScene.make_opts(spp=SPP, max_depth=8, miss_color=frog.settings["miss_color"])
+        bufs = _bufs(4, H)
+        for i in range(2):
+            (ra, pa), (rb, pb) = bufs[2 * i], bufs[2 * i + 1]
+            ds.render_device_pair(cam, cam, o, ra.data_ptr(), pa.data_ptr(), rb.data_ptr(), pb.data_ptr())
+        torch.cuda.synchronize()
+        assert ds.kernel_name().startswith("render_pair_kernel<17,"), ds.kernel_name()
+        for rgb, p6 in bufs:
+            assert p6.cpu().numpy().tobytes() == ppm[17:]
+    finally:
+        ds.close()
+
+
 def test_pair_outside_the_pair_kernel(frog):
-    """Frames the pair kernel is not instantiated for (multi-bounce, small spp on another tile
-    shape, the LANE kernel) render as two launches with the single-frame images."""
+    """Frames the pair kernel is not instantiated for (small spp on another tile shape, the LANE
+    kernel, 128 spp whole-block items) render as two launches with the single-frame images."""
     ds = rt.DeviceScene.from_host(frog, device=0)
     try:
         cams = _cams(frog, 320, 180)
-        for kw in (dict(spp=4, max_depth=3), dict(spp=4, max_depth=1, kernel=rt.RT_KERNEL_LANE),
-                   dict(spp=128, max_depth=1)):
+        for kw in (dict(spp=4, max_depth=1, kernel=rt.RT_KERNEL_LANE), dict(spp=128, max_depth=1)):
             o, _j = rt.DeviceScene.make_opts(miss_color=frog.settings["miss_color"], **kw)
             want = _singles(ds, cams, ["base", "moved"], o, 180, 320)
             (ra, pa), (rb, pb) = _bufs(2, 180, 320)

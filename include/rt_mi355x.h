@@ -25,7 +25,9 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2  /* 2: rt_renderer_opts.host_frame_name, RT_GATHER_HOST_SHARED */
+#define RT_ABI_VERSION 3  /* 2: rt_renderer_opts.host_frame_name, RT_GATHER_HOST_SHARED;
+                              3: RT_ERR_INTERNAL, rt_scene_faults, rt_tuning_* (RT_TUNE_*) in place of
+                                 environment variables, frame pairs, the resident HW1 scene */
 
 enum {
     RT_OK = 0,
@@ -244,11 +246,12 @@ int rt_render_device_p6(rt_scene* s, const rt_camera* cam, const rt_render_opts*
                         void* hip_stream);
 
 /* Two frames of one scene with the same options (two cameras of the same pixel size, e.g. the
- * next two frames of a sequence: two iterations of the reference's per-frame render() loop,
- * G/src/main.cu:362-378), as rt_render_device_p6 twice (frame a, then frame b; the same
+ * next two frames of a sequence), as rt_render_device_p6 twice (frame a, then frame b; the same
  * images), rendered by one launch of the render kernel where it fits them
  * (RT_TUNE_PAIR_FRAMES): the second frame's work fills the first's tail and the launch gap
- * between two frames goes.  Outputs of a and b must not overlap. */
+ * between two frames goes.  This batching is this library's own: the reference renders one
+ * frame per render() call (G/src/main.cu:362-378 is a 1x1 warm-up launch, then one timed
+ * render).  Outputs of a and b must not overlap. */
 int rt_render_device_pair(rt_scene* s, const rt_camera* cam_a, const rt_camera* cam_b,
                           const rt_render_opts* opt, float* rgb_a_dev, uint8_t* p6_a_dev,
                           float* rgb_b_dev, uint8_t* p6_b_dev, void* hip_stream);
@@ -495,7 +498,7 @@ int rt_scene_traversal_info(const rt_scene* s, int64_t info[4]);
  * scene's work): bit 0 = a camera-ray frustum traversal needed more than its 128 stack
  * entries (the host bound makes this impossible for records built with the default cap; the
  * wave's answers were poisoned: no hit).  clear != 0 resets the flags.  rt_render
- * returns RT_ERR_INTERNAL when a frame raised one. */
+ * returns RT_ERR_INTERNAL when its frame raised one (it clears the flags when the frame starts). */
 int rt_scene_faults(rt_scene* s, uint32_t* flags, int clear);
 
 /* ---- Tuning knobs (process-wide; read when a scene is created or a frame is set up) ----
@@ -523,7 +526,8 @@ typedef enum {
     RT_TUNE_PREPASS_GATE = 13,   /* f in (0, 1]: a frame's render kernel opens the next frame's cull/cut
                                     pre-passes when its first work queue has handed out the fraction
                                     f of its items (0.5 default; 1: drained, they then fill its
-                                    tail); 0: they start when the frame before it has finished */
+                                    tail); 0: they start when the frame before it has finished.
+                                    Off while RT_TUNE_OVERLAP_FRAMES is on */
     RT_TUNE_OVERLAP_FRAMES = 14, /* rt_renderer frames: 1 lets a frame's render kernel start while the previous
                                     one's tail still runs (two render streams per scene); 0 (default) */
     RT_TUNE_KERNEL_TIMING_EVERY = 15, /* rt_renderer frames: the render kernel's start event (kernel times) in one
@@ -543,7 +547,10 @@ typedef enum {
     RT_TUNE_PAIR_RESERVE = 19,   /* pair kernels: block slots per CU left free for the next pair's pre-passes
                                     (default 1 for depth-1 frames, 0 for the bounce kernels'
                                     pairs; fractions: that many per CU on average) */
-    RT_TUNE_COUNT = 20
+    RT_TUNE_CUT_SUB = 20,        /* sub-boxes per box of the tile-culling cut, tested for the tiles whose rays
+                                    may reach that box (16; a power of two <= 64; < 2: one level);
+                                    at scene creation */
+    RT_TUNE_COUNT = 21
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */
 int rt_tuning_set(int id, double value);

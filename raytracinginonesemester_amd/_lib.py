@@ -33,7 +33,8 @@ TUNE = {"frustum_arity": 0, "half_waves": 1, "paired_only": 2, "heavy_frac": 3, 
         "peer_timeout_s": 9, "renderer_threads": 10, "copy_engine": 11,
         "quant_records": 12, "prepass_gate": 13,
         "overlap_frames": 14, "kernel_timing_every": 15,
-        "record_greedy": 16, "wide4_greedy": 17, "pair_frames": 18, "pair_reserve": 19}
+        "record_greedy": 16, "wide4_greedy": 17, "pair_frames": 18, "pair_reserve": 19,
+        "cut_sub": 20}
 
 
 class RTError(RuntimeError):

@@ -109,6 +109,8 @@ struct SceneView {
     int32_t lane_wide;   // ... and the 4-ary DFS fits them too: traverse_lane_lds_wide
     const float* __restrict__ cut;  // tile culling: boxes of a cut of the tree (6 floats each)
     int32_t ncut;
+    const float* __restrict__ cut2;  // 2^cut_sub_log2 boxes of a cut of each cut box's subtree
+    int32_t cut_sub_log2;            // 0: no second level
     const float4* __restrict__ tri;  // deep trees: v0 | e1, e2.x | e2.y, e2.z by triangle index (brute force)
     uint32_t* fault;  // RT_FAULT_* bits the kernels OR in (rt_scene_faults)
 };
@@ -2155,6 +2157,36 @@ __device__ __forceinline__ bool cut_setup(const RenderParams& P, uint32_t lane, 
     return test;
 }
 
+// The cut's second level for one tile: hm = the cut boxes some ray of the tile may reach (a
+// wave-uniform mask).  Their sub-boxes (sc.cut2: S = 2^cut_sub_log2 per cut box, a cut of its
+// subtree) are tested 64 at a time, 64 / S cut boxes per pass, lane l taking sub-box l % S of
+// the (l / S)-th remaining box of hm.  True when a sub-box may be reached; false when every one
+// is provably missed by every ray of the tile, which, with the cut boxes outside hm, proves that
+// no ray reaches any leaf (each leaf has an ancestor-or-self among the tested boxes, and
+// SearchBVH reaches a triangle only after every ancestor's box test passed).
+__device__ __forceinline__ bool tile_cut_sub(const RenderParams& P, const TileDirsF& T, uint64_t hm, uint32_t lane) {
+    const int sl = P.sc.cut_sub_log2;
+    const int per = 64 >> sl;
+    const int gi = (int)(lane >> sl);
+    const uint32_t c = lane & ((1u << sl) - 1u);
+    while (hm != 0) {
+        int mine = -1;
+        for (int k = 0; k < per && hm != 0; ++k) {
+            const int b = __builtin_ctzll(hm);
+            if (gi == k) mine = b;
+            hm &= hm - 1;
+        }
+        bool reach = false;
+        if (mine >= 0) {
+            const float* p = P.sc.cut2 + 6 * (((size_t)mine << sl) | c);
+            const float bx[6] = {p[0], p[1], p[2], p[3], p[4], p[5]};
+            reach = !tile_misses_box_f(T, bx);
+        }
+        if (ballot(reach) != 0) return true;
+    }
+    return false;
+}
+
 // One unit of the cut pass: group g (CUT_GROUP consecutive slots) of live list q; false when
 // the group is past the list's end.
 __device__ __forceinline__ bool cut_unit(const RenderParams& P, uint32_t lane, int q, int g, bool test,
@@ -2181,7 +2213,8 @@ __device__ __forceinline__ bool cut_unit(const RenderParams& P, uint32_t lane, i
             if (g_cut_counts && lane == 0) g_cut_counts[tile] = __popcll(hm);
         }
 #endif
-        if (ballot(hit) == 0) {
+        const uint64_t hm = ballot(hit);
+        if (hm == 0 || (P.sc.cut_sub_log2 > 0 && !tile_cut_sub(P, T, hm, lane))) {
             write_culled_tile(P, tile, (int)lane, 64);
             culled |= 1ull << j;
         }
@@ -2439,7 +2472,7 @@ __device__ __forceinline__ void pixels_tile(const RenderParams& P, int tile, uin
 // Scenes whose data (records, leaves, normals) exceed kBigSceneBytes do not stay in the L2s and
 // MALL: their depth-1 wave kernels run 8 waves per SIMD (64 VGPRs, a few spills outside the
 // traversal loops), more waves to hide the record loads' latency (c5, 345 MB: DESIGN.md §4.2).
-// RT_BIG_SCENE_BYTES overrides the threshold (A/B).
+// RT_TUNE_BIG_SCENE_BYTES (rt_tuning_set) overrides the threshold (A/B).
 // The paired-only bounce kernels (one light, half waves: paired_bounces and nothing else).
 #ifndef RT_PAIRED_WAVES
 #define RT_PAIRED_WAVES 4
@@ -3258,6 +3291,8 @@ struct rt_scene {
     DevBuf fault;     // one word: RT_FAULT_* bits the kernels OR in (rt_scene_faults)
     DevBuf cut;  // tile culling: boxes of a cut of the tree (6 floats each)
     int ncut = 0;
+    DevBuf cut2;  // 2^cut_sub_log2 boxes below each cut box (tile_cut_sub), 6 floats each
+    int cut_sub_log2 = 0;
     bool deep = false;  // the DFS may need more than STACK_CAP entries: MODE_DEEP kernels
     DevBuf tri;         // deep: triangles by index (brute-force completion)
     bool wide = false;
@@ -3888,6 +3923,47 @@ extern "C" int rt_scene_create(int device, size_t P, const rt_bvh_node* nodes, c
             }
             if ((rc = s->cut.upload(hc.data(), hc.size() * sizeof(float))) != RT_OK) return rc;
             s->ncut = int(cutn.size());
+            // Second level (RT_TUNE_CUT_SUB sub-boxes per cut box, a power of two <= 64): the
+            // same rule inside each cut node's subtree, so the tiles whose rays reach a cut box
+            // are tested against the boxes below it (tile_cut_sub).  Unused slots repeat the
+            // node's first sub-box: a duplicate changes no "every box missed" decision.
+            const int sub = int(std::clamp(rt::tuning(RT_TUNE_CUT_SUB, 16.0), 0.0, 64.0));
+            int sl = 0;
+            while ((2 << sl) <= sub) ++sl;
+            if (sub >= 2) {
+                const int S = 1 << sl;
+                std::vector<float> h2(size_t(6) * S * cutn.size());
+                for (size_t i = 0; i < cutn.size(); ++i) {
+                    std::vector<uint32_t> sn{cutn[i]};
+                    while (int(sn.size()) < S) {
+                        int best = -1;
+                        double ba = -1.0;
+                        for (int j = 0; j < int(sn.size()); ++j) {
+                            if (cid[sn[j]] & LEAF_BIT) continue;
+                            const double a = area(sn[j]);
+                            if (a > ba) { ba = a; best = j; }
+                        }
+                        if (best < 0) break;
+                        const rt_bvh_node& nd = nodes[sn[best]];
+                        std::vector<uint32_t> kids;
+                        if (nd.left_idx != NO_REF && cid[nd.left_idx] != NO_REF) kids.push_back(nd.left_idx);
+                        if (nd.right_idx != NO_REF && cid[nd.right_idx] != NO_REF) kids.push_back(nd.right_idx);
+                        if (int(sn.size()) - 1 + int(kids.size()) > S) break;
+                        sn.erase(sn.begin() + best);
+                        sn.insert(sn.end(), kids.begin(), kids.end());
+                        if (sn.empty()) break;
+                    }
+                    if (sn.empty()) sn.push_back(cutn[i]);
+                    for (int j = 0; j < S; ++j) {
+                        const rt_aabb& bb = aabbs[sn[size_t(j) < sn.size() ? j : 0]];
+                        const float v6[6] = {bb.min_corner.x, bb.min_corner.y, bb.min_corner.z,
+                                             bb.max_corner.x, bb.max_corner.y, bb.max_corner.z};
+                        std::memcpy(&h2[6 * (i * S + j)], v6, sizeof(v6));
+                    }
+                }
+                if ((rc = s->cut2.upload(h2.data(), h2.size() * sizeof(float))) != RT_OK) return rc;
+                s->cut_sub_log2 = sl;
+            }
         }
     }
     if ((rc = s->inode.upload(hin.data(), hin.size() * sizeof(float4))) != RT_OK) return rc;
@@ -3971,6 +4047,7 @@ extern "C" int rt_scene_clone(const rt_scene* src, int device, rt_scene** out) {
     std::memcpy(s->root_box, src->root_box, sizeof(s->root_box));
     std::memcpy(s->bmax, src->bmax, sizeof(s->bmax));
     s->ncut = src->ncut;
+    s->cut_sub_log2 = src->cut_sub_log2;
     s->wide = src->wide;
     s->lane_stack = src->lane_stack;
     s->lane_wide = src->lane_wide;
@@ -3986,7 +4063,8 @@ extern "C" int rt_scene_clone(const rt_scene* src, int device, rt_scene** out) {
                                                       {&s->ibox, &src->ibox},   {&s->leaf, &src->leaf},
                                                       {&s->tnorm, &src->tnorm}, {&s->objids, &src->objids},
                                                       {&s->mats, &src->mats},   {&s->lights, &src->lights},
-                                                      {&s->cut, &src->cut},     {&s->tri, &src->tri}};
+                                                      {&s->cut, &src->cut},     {&s->cut2, &src->cut2},
+                                                      {&s->tri, &src->tri}};
     for (const auto& [d, q] : bufs) {
         if ((rc = d->alloc(q->n)) != RT_OK) return rc;
         if (q->n) HIP_TRY(hipMemcpyPeer(d->p, device, q->p, src->device, q->n));
@@ -4361,6 +4439,8 @@ int render_frame(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, flo
     P.sc.root_ref = s->root_ref;
     std::memcpy(P.sc.root_box, s->root_box, sizeof(P.sc.root_box));
     P.sc.cut = static_cast<const float*>(s->cut.p);
+    P.sc.cut2 = static_cast<const float*>(s->cut2.p);
+    P.sc.cut_sub_log2 = s->cut2.p ? s->cut_sub_log2 : 0;
     P.sc.tri = static_cast<const float4*>(s->tri.p);
     P.sc.fault = static_cast<uint32_t*>(s->fault.p);
     // RT_TUNE_CULL_COVERAGE: tests force the cut pass on (>= 1: always, untested candidates none)
@@ -4400,7 +4480,7 @@ int render_frame(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, flo
     // bound by its longest waves, and halving their rays shortens them (c3 band shards on one
     // GPU, max over the 8: kernel 0.101 -> 0.095 ms, frame 0.122 -> 0.116; at 4 and fewer shards
     // the doubled wave count costs more: N = 4 0.106 -> 0.116, N = 1 0.211 -> 0.373;
-    // scripts/half_waves_ab.py).  RT_HALF_WAVES=0/1 overrides.  (Quarter waves,
+    // scripts/half_waves_ab.py).  RT_TUNE_HALF_WAVES = 0/1 overrides.  (Quarter waves,
     // 16 samples, measured slower at N = 8 and were dropped.)
     // The multi-bounce kernels take half waves at any split: a wave's bounce paths end with its
     // longest lane's, and the longest waves bound the kernel (c3b 1.96 vs 2.37 ms per frame).
@@ -4439,7 +4519,7 @@ int render_frame(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, flo
     // (RT_TILES_XCD_CHUNK): tiles_x * ceil(tiles_y / 8) bounds both
     P.queue_cap = P.tile_order == RT_TILES_LINEAR ? P.tiles_total : P.tiles_x * ((tiles_y + 7) / 8);
     // Heavy-first dispatch needs the cut pass (it builds the heavy lists) and the 8 lists.
-    // RT_HEAVY_FRAC (speed experiments): a tile is in heavy class c when one of its waves took
+    // RT_TUNE_HEAVY_FRAC (speed experiments): a tile is in heavy class c when one of its waves took
     // at least 2^(2-c) times this fraction of the latest finished frame's render kernel
     // (0: off).
     // c3 (frustum traversal, profiles/r04/exp/heavy_frac_ab_c3*.log): 0.05 0.153, 0.06 0.149,
@@ -4655,7 +4735,10 @@ int render_frame(rt_scene* s, const rt_camera* cam, const rt_render_opts* o, flo
         // 0 they start once the frame before this one has finished
         // (0.5: c3 0.1557-0.157 ms per delivered frame vs 0.1587-0.1593 at 1.0, the pre-passes
         // then finishing well before this kernel does; profiles/r05/exp/prepass_gate_frac_c3.log)
-        const double gate_f = rt::tuning(RT_TUNE_PREPASS_GATE, 0.5);
+        // The gate word takes plain stores, so it needs one writer kernel at a time: with
+        // overlapping frames (ovl: two render streams) a late store of frame k-2's kernel could
+        // overwrite frame k-1's tag after frame k had started waiting for it, so ovl runs ungated.
+        const double gate_f = ovl ? 0.0 : rt::tuning(RT_TUNE_PREPASS_GATE, 0.5);
         const bool gate = gate_f > 0.0;
         P.drained = gate ? s->drain : nullptr;
         P.drain_tag = uint32_t(k + 1);
@@ -4854,6 +4937,10 @@ extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts
         if ((rc = hi.alloc(npx * size_t(o->spp) * sizeof(int32_t))) != RT_OK) return rc;
         if ((rc = ht.alloc(npx * size_t(o->spp) * sizeof(float))) != RT_OK) return rc;
     }
+    // the fault word belongs to this frame: earlier frames finish first, then it is cleared
+    // (rt_scene_faults still sees what this frame raised)
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemset(s->fault.p, 0, sizeof(uint32_t)));
     rc = rt_render_device(s, cam, o, static_cast<float*>(rgb.p), static_cast<int32_t*>(hi.p),
                           static_cast<float*>(ht.p), nullptr);
     if (rc != RT_OK) return rc;

@@ -1,4 +1,4 @@
-"""A/B of half waves (RT_HALF_WAVES: 32 samples per wave) against full waves on band shards of
+"""A/B of half waves (RT_TUNE_HALF_WAVES, set with rt_tuning_set / --tune half_waves=1: 32 samples per wave) against full waves on band shards of
 a c3 frame, one GPU, interleaved rounds: per band count N, every shard's mean kernel and frame
 ms under each setting, the max over shards (the per-rank time an N-GPU frame waits for), and a
 bit-exact check of every shard's P6 and float output between the two settings.

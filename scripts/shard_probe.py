@@ -1,5 +1,5 @@
 """Band shards of one frame rendered alone on this GPU: per shard, render-kernel ms, live and
-heavy tiles, with heavy-first dispatch on and off (RT_HEAVY_FRAC=0), to check that a shard's
+heavy tiles, with heavy-first dispatch on and off (RT_TUNE_HEAVY_FRAC = 0 through rt_tuning_set), to check that a shard's
 work queues get their heavy tiles first like the whole frame's.
     python scripts/shard_probe.py [--config c3b] [--n 2]"""
 import argparse

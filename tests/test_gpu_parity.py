@@ -601,6 +601,40 @@ def test_cut_culling_fuzz_grazing_cameras(scene, tune):
             assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), k
 
 
+@pytest.mark.parametrize("sub", [0, 2, 16, 64])
+@pytest.mark.parametrize("scene", ["frog.json", "cornell.json"])
+def test_cut_sub_boxes_fuzz_grazing_cameras(scene, sub, tune):
+    """The cut's second level (RT_TUNE_CUT_SUB sub-boxes below each of the 64 cut boxes,
+    tile_cut_sub): cameras aimed at the faces, edges and corners of boxes of random internal
+    nodes at every depth of the tree (the sub-boxes' own boxes among them), from near and far,
+    narrow and wide fields of view: culled frames are bit-identical to unculled ones, and to the
+    frames of a scene with one cut level."""
+    tune(cull_coverage=1.0, cut_sub=sub)
+    hs = host_scene(scene)
+    ds = rt.DeviceScene.from_host(hs, device=0)
+    try:
+        internal = np.nonzero(hs.nodes[:, 3] == 0xFFFFFFFF)[0]
+        rng = np.random.default_rng(77 + sub)
+        for k in range(24):
+            n = int(rng.choice(internal))
+            lo = hs.aabbs[n, :3].astype(np.float64)
+            hi = hs.aabbs[n, 3:].astype(np.float64)
+            ext = max(float(np.linalg.norm(hi - lo)), 1e-3)
+            t = rng.choice([0.0, 1.0, 0.5, rng.uniform()], size=3)
+            target = lo + t * (hi - lo)
+            dirn = rng.normal(size=3)
+            dirn /= np.linalg.norm(dirn)
+            pos = target + dirn * ext * rng.choice([0.3, 2.0, 20.0, 400.0])
+            up = (0.0, 0.0, 1.0) if abs(dirn[2]) < 0.9 else (0.0, 1.0, 0.0)
+            cam = rt.Camera(tuple(pos), tuple(target), up, float(rng.choice([8.0, 35.0, 600.0])), 24.0, 80, 48)
+            a = ds.render(cam, spp=4, max_depth=1, aov=True)
+            b = ds.render(cam, spp=4, max_depth=1, aov=True, flags=rt._lib.RT_FLAG_NO_CULL)
+            for x, y in zip(a, b):
+                assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), (k, n)
+    finally:
+        ds.close()
+
+
 def test_hw1_timing_entry_point():
     """rt_render_hw1_ex with kernel timing: a positive device time and the same image."""
     c = configs.HW1_CONFIGS["c1"]
@@ -762,6 +796,12 @@ def test_frustum_stack_overflow_guard_is_loud(tune):
         assert ds.faults() == 0  # cleared by the previous call
         # the binary-record traversal does not use the frustum stack: a valid frame
         ds.render(cam, spp=4, max_depth=1, flags=rt._lib.RT_FLAG_BINARY)
+        # the fault word belongs to the frame that raised it: a faulting frame left uncleared
+        # does not fail the next, valid one
+        with pytest.raises(rt.RTError):
+            ds.render(cam, spp=4, max_depth=1)
+        ds.render(cam, spp=4, max_depth=1, flags=rt._lib.RT_FLAG_BINARY)
+        assert ds.faults() == 0
     finally:
         ds.close()
 

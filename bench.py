@@ -808,14 +808,15 @@ def main():
     cam = hs.camera(cfg["width"], cfg["height"])
     W, H, spp = cam.pixel_width, cam.pixel_height, cfg["spp"]
     if a.pair is None:
-        # Two frames per launch where the pair kernel takes them: the band
-        # shards of an N-GPU frame gain most (8 shards: render kernel 0.0506 vs 0.0745 ms per
-        # frame, 2 shards 0.0731 vs 0.0922, scripts/pair_shards.py, profiles/r05/exp/pair_shards_c3.log);
-        # one GPU 0.1484 vs 0.1551 ms/step over 100 steps, and even in the driver's 20-step window
-        # (0.1587 / 0.1649 vs ~0.16: its fill and drain eat most of the gain).  The price is frame
-        # latency (0.76 vs 0.44 ms); the single-frame mode is measured beside the headline
-        # (timing.other_submission), and --pair 0 makes it the headline.
-        a.pair = 1 if PAIR_CONFIGS(a, cfg) else 0
+        # One frame per launch at N = 1; two frames per launch for the band
+        # shards of an N-GPU frame, which gain most (8 shards: render kernel 0.0506 vs 0.0745 ms
+        # per frame, 2 shards 0.0731 vs 0.0922, scripts/pair_shards.py,
+        # profiles/r05/exp/pair_shards_c3.log).  On one GPU pairs were level with single frames in
+        # the driver's 20-step window (BENCH_r05: 0.162 vs 0.1599 ms/step) and double the frame
+        # latency (0.79 vs 0.42 ms), so the single-frame mode is the N = 1 headline (VERDICT r05
+        # item 2); the other mode is measured beside it (timing.other_submission), --pair 1 / 0
+        # chooses.  A pair renders the config's one camera twice (the workload is one fixed view).
+        a.pair = 1 if PAIR_CONFIGS(a, cfg) and world > 1 else 0
     PAIR["on"] = bool(a.pair)
     if a.depth is None:  # frames in flight (N = 1: depth 3 keeps the host's waits off the critical
         # path; the driver's 20-step command: 0.171 ms/step vs 0.174-0.262 at depth 2 with SDMA copies,
@@ -902,6 +903,9 @@ def main():
                          "runtime: hipMemcpyAsync (blit kernels on the CUs)") if comm == "native" else None),
         "pipeline_depth": a.depth if comm == "native" else 2, "kernel": a.kernel,
         "frames_per_submit": 2 if (a.pair and comm == "native") else 1}
+    if a.pair and comm == "native":
+        line["config"]["pair_cameras"] = ("identical: both frames of a pair are the config's one camera "
+                                          "(DESIGN.md §4.15 measures a pair of two different cameras)")
     if a.share_gpu and world > 1:
         line["config"]["rehearsal"] = "--share-gpu: ranks share GPUs (not a multi-GPU measurement)"
     if a.tune:

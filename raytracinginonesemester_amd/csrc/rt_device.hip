@@ -598,8 +598,9 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
 //   the values at d = dl and d = dh (linear in 1/d, and 1/d is monotone on an interval of one
 //   sign), so min / max over the four products (min - o, max - o) x (1/dl, 1/dh) bound every
 //   lane's near / far end of that axis; an axis whose interval reaches |d| < 1e-8 (where the
-//   reference's test is an inside test) or crosses 0 gives no bound (1/dl, 1/dh = -inf, +inf:
-//   the products are +-inf or NaN, which the min / max drop).  The wave passes a box when
+//   reference's test is an inside test) or crosses 0 gets the one-sided bound of the "loose axes"
+//   below (an axis of coordinates near the float range gets none: 1/dl, 1/dh = -inf, +inf, the
+//   products are +-inf or NaN, which the min / max drop).  The wave passes a box when
 //   max(tmin, max near) <= min(tmax_w, min far), widened by 2^-19 relative (the float rounding
 //   of (b - o), 1/d and the product is < 2^-22 relative; the reference's double ends are within
 //   2^-52), with tmax_w the largest bestT over the live lanes.  So the wave test passes whenever
@@ -623,6 +624,22 @@ __device__ __forceinline__ void traverse_wave_split(const SceneView& sc, const R
 //   entries take the 4-ary records the same way.
 // Scenes whose coordinates come within 1e30 of the float range give no bound on those axes
 // (products stay finite: |b - o| < 1e30, |1/d| <= 1e8).
+// - loose axes (round 6): a wave whose direction interval on an axis reaches |d| < 1e-8 (a 2x2
+//   pixel quad on the camera's own axis plane: any camera off a symmetric position has one such
+//   line of quads across the image) got no bound on that axis, so its family passed every box
+//   its other two axes allowed, a whole slice of the scene (c3 with the camera moved 0.5 mm in x:
+//   0.43 vs 0.13 ms, profiles/r06/exp/loose_axis_*.log).  Such an axis still bounds the near
+//   end from one side: with db = (min - o, max - o), a box with db.lo > 0 is reached only by
+//   lanes with d > 1e-8 (d <= 0 never reaches it; |d| < 1e-8 is the reference's inside test,
+//   which fails), each at t >= db.lo / d >= db.lo / dh; a box with db.hi < 0 only by lanes with
+//   d < -1e-8, at t >= db.hi / dl; a box across the plane gets no bound.  So near =
+//   max(db.lo * ihp, db.hi * iln) with ihp = 1/dh (dh > 0; +inf otherwise: no lane reaches the
+//   box) and iln = 1/dl (dl < 0; -inf otherwise), <= 0 for a box across the plane, and far = +inf.
+//   Waves with a loose axis take a copy of the loop that computes it (LOOSE): the others' loop is
+//   unchanged.
+template <bool PK, bool XL, bool QR, bool LOOSE>
+__device__ __forceinline__ void frustum_loop(const SceneView& sc, const RayPre& r, bool live, HitState& hs,
+                                             const float* o, const v2f* U);
 template <bool PK = false, bool XL = false, bool QR = false>
 __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayPre& r, bool active, HitState& hs) {
     hs.bestT = FLT_MAX;
@@ -649,15 +666,29 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
     // v_rcp_f32 (1 ulp; inside the 2^-19 widening below).
     const float dd[3] = {r.d.x, r.d.y, r.d.z};
     v2f U[3];
+    bool loose = false;  // a loose axis (see above); U = (ihp, iln) on it: U.x > 0 > U.y, which no
+                         // other axis has (bounded: one sign; no bound: -inf, +inf)
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float dl = wave_reduce_f<false>(live ? dd[a] : INFINITY);
         const float dh = wave_reduce_f<true>(live ? dd[a] : -INFINITY);
-        const bool ok = (dl >= 1e-8f || dh <= -1e-8f) && sc.bmax[a] + fabsf(o[a]) < 1e30f;
+        const bool fin = sc.bmax[a] + fabsf(o[a]) < 1e30f;
+        const bool ok = (dl >= 1e-8f || dh <= -1e-8f) && fin;
+        const bool lz = !ok && fin;
+        loose = loose || lz;
         // (made SGPRs: wave-uniform values the VALU computed stay in VGPRs otherwise)
-        U[a] = (v2f){__int_as_float(uni(__float_as_int(ok ? rcp_approx(dl) : -INFINITY))),
-                     __int_as_float(uni(__float_as_int(ok ? rcp_approx(dh) : INFINITY)))};
+        const float u0 = ok ? rcp_approx(dl) : lz ? (dh > 0.0f ? rcp_approx(dh) : INFINITY) : -INFINITY;
+        const float u1 = ok ? rcp_approx(dh) : lz ? (dl < 0.0f ? rcp_approx(dl) : -INFINITY) : INFINITY;
+        U[a] = (v2f){__int_as_float(uni(__float_as_int(u0))), __int_as_float(uni(__float_as_int(u1)))};
     }
+    if (__builtin_amdgcn_readfirstlane((int)loose) != 0) frustum_loop<PK, XL, QR, true>(sc, r, live, hs, o, U);
+    else frustum_loop<PK, XL, QR, false>(sc, r, live, hs, o, U);
+}
+
+// traverse_frustum's DFS over the records (LOOSE: the wave has a loose axis).
+template <bool PK, bool XL, bool QR, bool LOOSE>
+__device__ __forceinline__ void frustum_loop(const SceneView& sc, const RayPre& r, bool live, HitState& hs,
+                                             const float* o, const v2f* U) {
     const float kW = 1.0f / 524288.0f;  // 2^-19
     float tmax_w = FLT_MAX;
     uint32_t ref = sc.root_ref;
@@ -741,6 +772,12 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
                 const v2f p = (v2f){db.x, db.x} * U[a], q = (v2f){db.y, db.y} * U[a];
                 nr[a] = fminf(fminf(p.x, p.y), fminf(q.x, q.y));
                 fr[a] = fmaxf(fmaxf(p.x, p.y), fmaxf(q.x, q.y));
+                if constexpr (LOOSE) {  // U[a] = (ihp, iln) on a loose axis
+                    if (U[a].x > 0.0f && U[a].y < 0.0f) {
+                        nr[a] = fmaxf(p.x, q.y);
+                        fr[a] = INFINITY;
+                    }
+                }
             }
             float Lc = fmaxf(fmaxf(nr[0], nr[1]), nr[2]);
             float Hc = fminf(fminf(fr[0], fr[1]), fr[2]);

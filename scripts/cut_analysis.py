@@ -108,10 +108,15 @@ def main():
     ap.add_argument("--ks", default="64,128,256,512,1024,4096")
     ap.add_argument("--size", default="1920x1080")
     ap.add_argument("--spp", type=int, default=16)
+    ap.add_argument("--move", default="0,0,0", help="camera position offset (x,y,z)")
     a = ap.parse_args()
     W, H = map(int, a.size.split("x"))
     hs = rt.HostScene.load_json(REPO / "assets" / "scenes" / "frog.json", REPO)
     cam = hs.camera(W, H)
+    mv = tuple(float(v) for v in a.move.split(","))
+    if any(mv):
+        cam = rt.Camera(tuple(np.add(cam.pos, mv)), cam.look_at, cam.up, cam.focal_length_mm, cam.sensor_height_mm,
+                        W, H)
     b = cam.basis()
     oc = orc.camera_from_basis(b["center"], b["pixel00_loc"], b["pixel_delta_u"], b["pixel_delta_v"], W, H)
     t0 = time.time()

@@ -1,5 +1,6 @@
 """Traversal statistics from an instrumented build (scripts/build_variant.sh stats -DRT_STATS):
-    RT_MI355X_LIB=build/variants/stats/librt_mi355x.so python scripts/stats.py [c3|c5]"""
+    RT_MI355X_LIB=build/variants/stats/librt_mi355x.so python scripts/stats.py [c3|c5] [dx,dy,dz]
+(dx,dy,dz: the camera's position moved by that offset)"""
 import ctypes as C
 import json
 import sys
@@ -19,6 +20,10 @@ cfg = configs.G_CONFIGS[name]
 sp = configs.scene_path(cfg["scene"])
 hs = rt.HostScene.load_json(sp, REPO if sp.parent == configs.SCENES else sp.parent)
 cam = hs.camera(cfg["width"], cfg["height"])
+if len(sys.argv) > 2:
+    off = tuple(float(v) for v in sys.argv[2].split(","))
+    cam = rt.Camera(tuple(np.add(cam.pos, off)), cam.look_at, cam.up, cam.focal_length_mm, cam.sensor_height_mm,
+                    cfg["width"], cfg["height"])
 ds = rt.DeviceScene.from_host(hs)
 L = _lib.lib()
 out = (C.c_ulonglong * 24)()

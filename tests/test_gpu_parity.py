@@ -601,6 +601,40 @@ def test_cut_culling_fuzz_grazing_cameras(scene, tune):
             assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), k
 
 
+@pytest.mark.parametrize("scene", ["frog.json", "cornell.json", "sphere_single.json"])
+def test_frustum_loose_axis_cameras(scene):
+    """Waves whose direction interval reaches |d| < 1e-8 on an axis (the camera's axis planes cross
+    the image through 2x2-pixel quads) take the frustum loop with a one-sided bound on that axis
+    (traverse_frustum, LOOSE): cameras a little off the scene's symmetric positions, looking along
+    and across the axes, with the planes d.x = 0 / d.y = 0 / d.z = 0 through the image; frames and
+    hit AOVs bit for bit against the binary-record traversal (no frustum) and the oracle."""
+    hs = host_scene(scene)
+    ds = _device_scene(scene)
+    box = np.concatenate([hs.aabbs[0, :3], hs.aabbs[0, 3:]]).astype(np.float64)
+    ctr = (box[:3] + box[3:]) / 2
+    ext = float(np.linalg.norm(box[3:] - box[:3]))
+    base = hs.camera(96, 64)
+    cams = [rt.Camera(tuple(np.add(base.pos, off)), base.look_at, base.up, base.focal_length_mm,
+                      base.sensor_height_mm, 96, 64)
+            for off in [(5e-4 * ext, 0, 0), (0, 0, 3e-3 * ext), (-2e-3 * ext, 1e-3 * ext, 0), (1e-6, 0, 0)]]
+    for k, (axis, up) in enumerate([((0, 1, 0), (0, 0, 1)), ((1, 0, 0), (0, 0, 1)), ((0, 0, 1), (0, 1, 0)),
+                                    ((1, 1, 0), (0, 0, 1))]):
+        d = np.array(axis, np.float64) / np.linalg.norm(axis)
+        for dist_ in (0.7, 2.5):
+            pos = ctr - d * ext * dist_ + np.array([3e-4, -2e-4, 1e-4]) * ext * (k + 1)
+            cams.append(rt.Camera(tuple(pos), tuple(pos + d), up, 20.0, 24.0, 96, 64))
+    for i, cam in enumerate(cams):
+        a = ds.render(cam, spp=4, max_depth=1, aov=True)
+        b = ds.render(cam, spp=4, max_depth=1, aov=True, flags=rt._lib.RT_FLAG_BINARY)
+        for x, y in zip(a, b):
+            assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), i
+        if i % 3 == 0:
+            ref, rhi, _ = orc.render_g(hs.num_triangles, oracle_camera(cam), hs.nodes, hs.aabbs, hs.triangles,
+                                       hs.tri_object_ids, hs.materials, hs.lights, spp=4, max_depth=1, aov=True)
+            assert np.array_equal(a[1], rhi), i
+            _check_fb(a[0], ref)
+
+
 @pytest.mark.parametrize("sub", [0, 2, 16, 64])
 @pytest.mark.parametrize("scene", ["frog.json", "cornell.json"])
 def test_cut_sub_boxes_fuzz_grazing_cameras(scene, sub, tune):

@@ -6,13 +6,15 @@ parity checker / CPU baseline.  The product (raytracinginonesemester_amd) never 
 from __future__ import annotations
 
 import ctypes as C
+import os
 import subprocess
 from pathlib import Path
 
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB = HERE / "liboracle.so"
+# RT_ORACLE_LIB: another build of the same source (tests/test_sanitize.py: the ASan/UBSan one)
+LIB = Path(os.environ.get("RT_ORACLE_LIB", HERE / "liboracle.so"))
 REF_DIR = HERE / "_ref"
 
 

@@ -599,6 +599,8 @@ def build_bvh(positions, indices):
     """CPU LBVH (G/include/bvh.cu:209-317) over an indexed mesh: (nodes (2P-1,4), aabbs (2P-1,6))."""
     pos, idx = _c(positions, np.float32), _c(indices, np.uint32)
     P = idx.size // 3
+    if P == 0:  # what rt_build_bvh answers for an empty mesh (no arrays to size)
+        check(lib().rt_build_bvh(ptr(pos), pos.size // 3, None, 0, None, None))
     nodes = np.zeros((2 * P - 1, 4), np.uint32)
     aabbs = np.zeros((2 * P - 1, 6), np.float32)
     check(lib().rt_build_bvh(ptr(pos), pos.size // 3, ptr(idx), P, ptr(nodes), ptr(aabbs)))

@@ -3660,18 +3660,50 @@ static bool build_quant_records(const FrustumRecords& fr, std::vector<uint32_t>&
 extern "C" int rt_debug_frustum_records(size_t P, const rt_bvh_node* nodes, const rt_aabb* aabbs, int max_log2,
                                         int stack_cap, int64_t* info, float* rec, size_t rec_cap) {
     if (P == 0 || !nodes || !aabbs || !info) return set_error(RT_ERR_ARG, "rt_debug_frustum_records: null argument");
+    if (P > 0x3FFFFFFFull) return set_error(RT_ERR_UNSUPPORTED, "more than 2^30 triangles");
     const size_t NN = 2 * P - 1;
+    // the caller's arrays are checked as rt_scene_create checks them: children in range and no
+    // cycle reachable from the root (tests/test_host_fuzz.py)
+    {
+        std::vector<uint8_t> state(NN, 0);  // 0 new, 1 on the path, 2 done
+        std::vector<std::pair<uint32_t, bool>> st{{0u, false}};
+        while (!st.empty()) {
+            auto [v, post] = st.back();
+            st.pop_back();
+            if (post) {
+                state[v] = 2;
+                continue;
+            }
+            if (state[v] == 1) return set_error(RT_ERR_ARG, "BVH contains a cycle");
+            if (state[v] == 2) continue;
+            state[v] = 1;
+            st.push_back({v, true});
+            const rt_bvh_node& nd = nodes[v];
+            if (nd.object_idx != 0xFFFFFFFFu) continue;
+            for (const uint32_t c : {nd.left_idx, nd.right_idx}) {
+                if (c == NO_REF) continue;
+                if (c >= NN) return set_error(RT_ERR_ARG, "BVH child index out of range");
+                st.push_back({c, false});
+            }
+        }
+    }
     std::vector<uint32_t> cid(NN, NO_REF);
     size_t n_int = 0, n_leaf = 0;
     for (size_t n = 0; n < NN; ++n) {
         if (nodes[n].object_idx == 0xFFFFFFFFu) cid[n] = uint32_t(n_int++);
         else if (nodes[n].object_idx < P) cid[n] = LEAF_BIT | uint32_t(n_leaf++);
     }
+    if (nodes[0].object_idx != 0xFFFFFFFFu) {  // a leaf root: no records (rt_scene_create makes none)
+        info[0] = 2;
+        info[1] = 0;
+        info[2] = 0;
+        return RT_OK;
+    }
     const FrustumRecords fr = build_frustum_records(nodes, NN, cid.data(), aabbs, std::clamp(max_log2, 2, 5), stack_cap);
     info[0] = fr.log2;
     info[1] = fr.bound;
     info[2] = (int64_t)fr.nrec;
-    if (rec && rec_cap >= fr.rec.size()) std::memcpy(rec, fr.rec.data(), fr.rec.size() * sizeof(float));
+    if (rec && rec_cap >= fr.rec.size() && !fr.rec.empty()) std::memcpy(rec, fr.rec.data(), fr.rec.size() * sizeof(float));
     return RT_OK;
 }
 

@@ -176,9 +176,17 @@ bool parse_int(const char*& s, int& out) {
     bool neg = false;
     if (*s == '-') { neg = true; ++s; }
     if (*s < '0' || *s > '9') return false;
-    int v = 0;
-    while (*s >= '0' && *s <= '9') { v = v * 10 + (*s - '0'); ++s; }
-    out = neg ? -v : v;
+    // digits past int's range make no index (the reference's std::stoi throws out_of_range):
+    // the token is refused instead of overflowing (UBSan, tests/test_host_fuzz.py)
+    long long v = 0;
+    bool big = false;
+    while (*s >= '0' && *s <= '9') {
+        if (!big) v = v * 10 + (*s - '0');
+        big = big || v > 2147483647LL;
+        ++s;
+    }
+    if (big) return false;
+    out = neg ? -int(v) : int(v);
     return true;
 }
 
@@ -434,7 +442,7 @@ class JsonReader {
 public:
     explicit JsonReader(const std::string& s) : s_(s) {}
     bool parse(Json& out, std::string& err) {
-        if (!value(out)) { err = err_; return false; }
+        if (!value(out, 0)) { err = err_; return false; }
         ws();
         if (i_ != s_.size()) { err = "Trailing characters"; return false; }
         return true;
@@ -446,12 +454,16 @@ private:
     std::string err_;
     bool fail(const char* m) { err_ = m; return false; }
     void ws() { while (i_ < s_.size() && std::isspace(static_cast<unsigned char>(s_[i_]))) ++i_; }
-    bool value(Json& o) {
+    // Nesting is bounded (the scene dialect needs 4 levels): the reader recurses per level, and
+    // an unbounded depth let a file of 10^5 '[' overflow the C stack (tests/test_host_fuzz.py).
+    static constexpr int kMaxDepth = 256;
+    bool value(Json& o, int depth) {
         ws();
         if (i_ >= s_.size()) return fail("Unexpected end of input");
         const char c = s_[i_];
-        if (c == '{') return object(o);
-        if (c == '[') return array(o);
+        if ((c == '{' || c == '[') && depth >= kMaxDepth) return fail("Nesting too deep");
+        if (c == '{') return object(o, depth);
+        if (c == '[') return array(o, depth);
         if (c == '"') return string(o);
         if (c == 't' || c == 'f') return boolean(o);
         if (c == 'n') {
@@ -461,7 +473,7 @@ private:
         if (c == '-' || (c >= '0' && c <= '9')) return number(o);
         return fail("Unexpected character");
     }
-    bool object(Json& o) {
+    bool object(Json& o, int depth) {
         o.type = Json::Object;
         ++i_;
         ws();
@@ -474,7 +486,7 @@ private:
             if (i_ >= s_.size() || s_[i_] != ':') return fail("Expected ':'");
             ++i_;
             Json v;
-            if (!value(v)) return false;
+            if (!value(v, depth + 1)) return false;
             o.obj.emplace_back(key.str, std::move(v));
             ws();
             if (i_ < s_.size() && s_[i_] == ',') { ++i_; ws(); continue; }
@@ -483,14 +495,14 @@ private:
         }
         return fail("Unterminated object");
     }
-    bool array(Json& o) {
+    bool array(Json& o, int depth) {
         o.type = Json::Array;
         ++i_;
         ws();
         if (i_ < s_.size() && s_[i_] == ']') { ++i_; return true; }
         while (i_ < s_.size()) {
             Json v;
-            if (!value(v)) return false;
+            if (!value(v, depth + 1)) return false;
             o.arr.push_back(std::move(v));
             ws();
             if (i_ < s_.size() && s_[i_] == ',') { ++i_; ws(); continue; }
@@ -551,6 +563,15 @@ private:
     }
 };
 
+// int(x) of a JSON number, as the reference's int conversions give for every value in int's
+// range; outside it (and NaN) the C++ conversion is undefined, so it saturates here instead.
+int json_int(double d) {
+    if (!(d == d)) return 0;
+    if (d >= 2147483647.0) return 2147483647;
+    if (d <= -2147483648.0) return -2147483647 - 1;
+    return int(d);
+}
+
 bool as_vec3(const Json* v, rt_vec3& out) {  // scene.h:230-240
     if (!v || v->type != Json::Array || v->arr.size() != 3) return false;
     for (int k = 0; k < 3; ++k)
@@ -584,7 +605,7 @@ bool read_light(const Json& item, rt_light& lc) {  // scene.h:307-316, 322-330
     as_vec3(item.get("position"), lc.position);
     as_vec3(item.get("color"), lc.color);
     const Json* v = item.get("intensity");
-    if (v && v->type == Json::Number) lc.intensity = int(v->num);
+    if (v && v->type == Json::Number) lc.intensity = json_int(v->num);
     return true;
 }
 
@@ -593,9 +614,9 @@ int parse_scene(const Json& root, SceneDesc& sc) {
     if (root.type != Json::Object) return set_error(RT_ERR_PARSE, "Root is not an object");
     if (const Json* st = root.get("settings")) {
         const Json* v;
-        if ((v = st->get("max_bounces")) && v->type == Json::Number) sc.max_depth = int(v->num);
+        if ((v = st->get("max_bounces")) && v->type == Json::Number) sc.max_depth = json_int(v->num);
         if ((v = st->get("spp")) && v->type == Json::Number) {
-            sc.spp = int(v->num);
+            sc.spp = json_int(v->num);
             if (sc.spp < 1) sc.spp = 1;
         }
         if ((v = st->get("diffuse_bounce")) && v->type == Json::Bool) sc.diffuse_bounce = v->b;
@@ -605,8 +626,8 @@ int parse_scene(const Json& root, SceneDesc& sc) {
         const Json* v;
         if ((v = cam->get("focal_length_mm")) && v->type == Json::Number) sc.focal_mm = v->num;
         if ((v = cam->get("sensor_height_mm")) && v->type == Json::Number) sc.sensor_mm = v->num;
-        if ((v = cam->get("pixel_width")) && v->type == Json::Number) sc.width = int(v->num);
-        if ((v = cam->get("pixel_height")) && v->type == Json::Number) sc.height = int(v->num);
+        if ((v = cam->get("pixel_width")) && v->type == Json::Number) sc.width = json_int(v->num);
+        if ((v = cam->get("pixel_height")) && v->type == Json::Number) sc.height = json_int(v->num);
         as_vec3(cam->get("position"), sc.cam_pos);
         as_vec3(cam->get("look_at"), sc.cam_look);
         as_vec3(cam->get("up"), sc.cam_up);
@@ -1191,6 +1212,19 @@ extern "C" int rt_ppm_read(const char* path, float* rgb_out, size_t cap_floats, 
     if (mv <= 0 || mv > 65535) return set_error(RT_ERR_PARSE, "Invalid maxval in header (must be 1..65535).");
     const int ws = in.get();
     if (ws == EOF || !is_ws(ws)) return set_error(RT_ERR_PARSE, "Expected whitespace after maxval");
+    // The samples must all be there before the size is reported (a caller sizes its buffer by
+    // it: a forged header of 99999 x 99999 on a short file is refused here, not allocated for).
+    // The reference's reader fails the same file while reading the samples (ppm_p6.cpp:340-366).
+    {
+        const std::streampos at = in.tellg();
+        in.seekg(0, std::ios::end);
+        const std::streampos end = in.tellg();
+        in.seekg(at);
+        const unsigned long long need = (unsigned long long)w * (unsigned long long)h * 3ull * (mv < 256 ? 1ull : 2ull);
+        if (at < 0 || end < at || (unsigned long long)(end - at) < need)
+            return set_error(RT_ERR_PARSE, mv < 256 ? "Failed while reading 8-bit sample byte."
+                                                    : "Failed while reading 16-bit sample bytes.");
+    }
     if (width) *width = w;
     if (height) *height = h;
     if (maxval_out) *maxval_out = mv;

@@ -8,13 +8,16 @@ CPU: the binary exists, links the in-tree library and rejects bad usage without 
 from __future__ import annotations
 
 import gzip
+import os
 import subprocess
+from pathlib import Path
 
 import pytest
 
 from conftest import GOLDEN, REPO
 
-CLI = REPO / "raytracinginonesemester_amd" / "lib" / "rt_render_cli"
+# RT_MI355X_CLI: another build of the CLI (tests/test_sanitize.py: the ASan/UBSan one)
+CLI = Path(os.environ.get("RT_MI355X_CLI", REPO / "raytracinginonesemester_amd" / "lib" / "rt_render_cli"))
 
 
 def test_cli_usage_without_arguments():

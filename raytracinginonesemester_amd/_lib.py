@@ -176,6 +176,8 @@ SIGNATURES = {
     "rt_hw1_scene_create": (I, [I, P, P, P, SZ, P]),
     "rt_hw1_scene_destroy": (None, [P]),
     "rt_render_hw1_device": (I, [P, P, Vec3, Vec3, I, P, I, P, P, P, P, P]),
+    "rt_render_hw1_deliver": (I, [P, P, Vec3, Vec3, I, I, P, P, P]),
+    "rt_hw1_wait": (I, [P, C.c_uint64]),
     "rt_hw1_kernel_times": (I, [P, P, I, P]),
     "rt_hw1_kernel_name": (C.c_char_p, [P]),
     "rt_hw1_list_info": (I, [P, P]),

@@ -554,6 +554,19 @@ class HW1Scene:
                                          ptr(jit), RT_HW1_BRUTE if brute else 0, rgb_ptr, p6_ptr, hit_idx_ptr,
                                          hit_t_ptr, stream))
 
+    def render_deliver(self, camera: Camera, light_position, light_color, spp: int, host_p6_ptr: int, stream=None,
+                       brute: bool = False) -> int:
+        """One frame's P6 body (write_p6 defaults) delivered to host memory at host_p6_ptr
+        (W*H*3 bytes, pinned) by the scene's own copy stream, overlapping the next frames'
+        kernels (rt_render_hw1_deliver); returns the frame's ticket for wait()."""
+        t = C.c_uint64()
+        check(lib().rt_render_hw1_deliver(self._h, C.byref(camera.c), _v3(light_position), _v3(light_color), int(spp),
+                                          RT_HW1_BRUTE if brute else 0, host_p6_ptr, stream, C.byref(t)))
+        return int(t.value)
+
+    def wait(self, ticket: int) -> None:
+        check(lib().rt_hw1_wait(self._h, int(ticket)))
+
     def kernel_times(self, max_frames: int = 64) -> np.ndarray:
         out = np.zeros(max_frames, np.float32)
         n = C.c_int()

@@ -2,9 +2,11 @@
 
     python -m raytracinginonesemester_amd.build
 
-* librt_mi355x.so — rt_host.cpp (g++) + the device translation units (hipcc
-  --offload-arch=gfx950): rt_device.hip (scene + render), rt_frame.hip (P6 quantisation and
-  strip un-permute on the device), rt_lbvh.hip (LBVH build on the device).
+* librt_mi355x.so — the host units rt_host.cpp and rt_records.cpp (g++) + the device translation
+  units (hipcc --offload-arch=gfx950): rt_device.hip (scene + render; its device code in the
+  rt_wave/instrument/traverse/shade/prepass.hpp sections), rt_hw1.hip (the HW1 path),
+  rt_frame.hip (P6 quantisation and strip un-permute on the device), rt_lbvh.hip (LBVH build on
+  the device), rt_renderer.hip (the multi-GPU frame renderer).  Units compile in parallel.
   Every float path is compiled with -ffp-contract=off and without fast-math; HIP's default
   correctly rounded f32 division / sqrt stay on (parity with the reference CPU build).
 * rt_render_cli   — C++ CLI over the C ABI (scene JSON in, P6 out), G/src/main.cu's role.
@@ -34,7 +36,8 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 FP = ["-ffp-contract=off", "-fno-fast-math"]
-DEVICE_UNITS = ["rt_device", "rt_frame", "rt_lbvh", "rt_renderer"]
+DEVICE_UNITS = ["rt_device", "rt_hw1", "rt_frame", "rt_lbvh", "rt_renderer"]
+HOST_UNITS = ["rt_host", "rt_records"]
 
 
 ID_TAG = b"RT_BUILD_ID:"
@@ -79,36 +82,46 @@ def _step(target: Path, deps, cmd, force: bool) -> None:
     stamp.write_text(h.hexdigest())
 
 
+def _parallel(jobs, force: bool) -> None:
+    """_step over (target, deps, cmd) jobs on a few threads (each job is its own process)."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=max(1, min(len(jobs), os.cpu_count() or 1, 8))) as ex:
+        for f in [ex.submit(_step, o, deps, cmd, force) for o, deps, cmd in jobs]:
+            f.result()
+
+
 def build(force: bool = False) -> Path:
     OUT.mkdir(parents=True, exist_ok=True)
     OBJ.mkdir(parents=True, exist_ok=True)
     bid = source_build_id()
-    hdrs = [REPO / "include" / "rt_mi355x.h", CSRC / "rt_common.hpp", CSRC / "rt_math.hpp", CSRC / "rt_ppm.hpp",
-            CSRC / "rt_hip_host.hpp"]
-    host_o = OBJ / "rt_host.o"
+    hdrs = [REPO / "include" / "rt_mi355x.h", *sorted(CSRC.glob("*.hpp"))]
+    inc = [f"-I{REPO / 'include'}", f"-I{CSRC}"]
+    jobs = []
+    host_objs = []
+    for name in HOST_UNITS:
+        o = OBJ / f"{name}.o"
+        host_objs.append(o)
+        jobs.append((o, [CSRC / f"{name}.cpp", *hdrs],
+                     [CXX, "-std=c++17", "-O2", "-fPIC", *FP, "-Wall", "-Wextra", *inc, "-c", CSRC / f"{name}.cpp", "-o", o]))
     dev_objs = []
     so = OUT / "librt_mi355x.so"
-    inc = [f"-I{REPO / 'include'}", f"-I{CSRC}"]
-    _step(host_o, [CSRC / "rt_host.cpp", *hdrs],
-          [CXX, "-std=c++17", "-O2", "-fPIC", *FP, "-Wall", "-Wextra", *inc, "-c", CSRC / "rt_host.cpp", "-o", host_o],
-          force)
     for name in DEVICE_UNITS:
         dev_o = OBJ / f"{name}.o"
         dev_objs.append(dev_o)
         # code object v5: loadable by both the image's ROCm 7.2 runtime and the ROCm 7.0 HIP
         # runtime bundled with torch (which the process uses when torch is imported first)
-        _step(dev_o, [CSRC / f"{name}.hip", *hdrs],
-              [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP, "-Wall",
-               "-mcode-object-version=5", "-Wno-unused-function", *inc, "-c", CSRC / f"{name}.hip", "-o", dev_o],
-              force)
+        jobs.append((dev_o, [CSRC / f"{name}.hip", *hdrs],
+                     [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP, "-Wall",
+                      "-mcode-object-version=5", "-Wno-unused-function", *inc, "-c", CSRC / f"{name}.hip", "-o", dev_o]))
+    _parallel(jobs, force)
     id_c = OBJ / "rt_build_id.c"
     id_c.write_text("/* generated by build.py: sha256 of csrc/ + include/ + flags */\n"
                     f"static const char tag[] __attribute__((used)) = \"{ID_TAG.decode()}{bid}\";\n"
                     "const char* rt_build_id(void) { return tag + %d; }\n" % len(ID_TAG))
     id_o = OBJ / "rt_build_id.o"
     _step(id_o, [id_c], ["gcc", "-O2", "-fPIC", "-c", id_c, "-o", id_o], force)
-    _step(so, [host_o, *dev_objs, id_o],
-          [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", host_o, *dev_objs, id_o, "-o", so, "-ldl"],
+    _step(so, [*host_objs, *dev_objs, id_o],
+          [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *host_objs, *dev_objs, id_o, "-o", so, "-ldl"],
           force or library_build_id(so) != bid)
     if library_build_id(so) != bid:
         raise RuntimeError(f"{so}: embedded build id does not match the sources")
@@ -140,28 +153,25 @@ def build_sanitized(force: bool = False) -> dict:
     """CPU-only ASan/UBSan build of the host code (see the module docstring); returns the paths."""
     ASAN.mkdir(parents=True, exist_ok=True)
     cxx, cc = LLVM_BIN / "clang++", LLVM_BIN / "clang"
-    hdrs = [REPO / "include" / "rt_mi355x.h", CSRC / "rt_common.hpp", CSRC / "rt_math.hpp", CSRC / "rt_ppm.hpp",
-            CSRC / "rt_hip_host.hpp"]
+    hdrs = [REPO / "include" / "rt_mi355x.h", *sorted(CSRC.glob("*.hpp"))]
     inc = [f"-I{REPO / 'include'}", f"-I{CSRC}"]
     objs = []
-    host_o = ASAN / "rt_host.o"
-    _step(host_o, [CSRC / "rt_host.cpp", *hdrs],
-          [cxx, "-std=c++17", "-fPIC", *FP, *SAN, *inc, "-c", CSRC / "rt_host.cpp", "-o", host_o], force)
-    objs.append(host_o)
-    # the .hip units whole (a host-only object would reference its missing device bundle), the
-    # sanitizers on the host side only (-Xarch_host: no GPU sanitizer), in parallel
-    host_san = [f for flag in SAN for f in ("-Xarch_host", flag)]
     jobs = []
+    for name in HOST_UNITS:
+        o = ASAN / f"{name}.o"
+        jobs.append((o, [CSRC / f"{name}.cpp", *hdrs],
+                     [cxx, "-std=c++17", "-fPIC", *FP, *SAN, *inc, "-c", CSRC / f"{name}.cpp", "-o", o]))
+        objs.append(o)
+    # the .hip units whole (a host-only object would reference its missing device bundle), the
+    # sanitizers on the host side only (-Xarch_host: no GPU sanitizer)
+    host_san = [f for flag in SAN for f in ("-Xarch_host", flag)]
     for name in DEVICE_UNITS:
         o = ASAN / f"{name}.o"
         jobs.append((o, [CSRC / f"{name}.hip", *hdrs],
                      [HIPCC, f"--offload-arch={ARCH}", "-O1", "-std=c++17", "-fPIC", *FP, *host_san,
                       "-mcode-object-version=5", "-Wno-unused-function", *inc, "-c", CSRC / f"{name}.hip", "-o", o]))
         objs.append(o)
-    from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(max_workers=min(4, os.cpu_count() or 1)) as ex:
-        for f in [ex.submit(_step, o, deps, cmd, force) for o, deps, cmd in jobs]:
-            f.result()
+    _parallel(jobs, force)
     id_c = ASAN / "rt_build_id.c"
     id_c.write_text("/* the sanitized CPU-only build: never the product's id */\n"
                     f"static const char tag[] __attribute__((used)) = \"asan:{source_build_id()}\";\n"

@@ -1,0 +1,906 @@
+// rt_hw1.hip — the HW1 path on gfx950 (HW1/src/render.cpp:72-116: every triangle for every
+// camera ray, the closest t >= 0 with the first index winning ties, HW1 shade
+// HW1/include/raytracer.h:21-48; ray_intersection HW1/include/ray.h:67-117), and its C ABI:
+// rt_render_hw1[_ex] (brute force or binned, synchronous), the resident rt_hw1_scene
+// (rt_render_hw1_device: the C2 configuration's binned, chunked pipeline) and its
+// pipelined host delivery (rt_render_hw1_deliver / rt_hw1_wait).  Split out of rt_device.hip in
+// round 6; it shares only the wave primitives (rt_wave.hpp) with it.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "rt_common.hpp"
+#include "rt_hip_host.hpp"
+#include "rt_math.hpp"
+#include "rt_ppm.hpp"
+
+using namespace rtd;
+
+namespace {
+
+constexpr int BLOCK = 256;  // threads per block (rt_device.hip's render blocks are the same size)
+
+#include "rt_wave.hpp"
+
+// ---- HW1 brute force (HW1/src/render.cpp:72-116) ----------------------------------------
+struct Hw1Params {
+    const float4* __restrict__ tri;   // 3 float4 per triangle: v0, e1, e2
+    const float4* __restrict__ nrm;   // 3 float4 per triangle: n0, n1, n2
+    const int4* __restrict__ rects;   // binned path: per triangle (ix_lo, iy_lo, ix_hi, iy_hi)
+    const uint32_t* __restrict__ bin_count;   // binned path: per wave tile, triangles listed
+    const uint32_t* __restrict__ bin_offset;  // exclusive prefix sum of bin_count
+    const uint32_t* __restrict__ bin_list;    // triangle indices, per tile (any order)
+    int32_t num_tris;
+    f3 center, p00, du, dv;
+    int32_t W, H, spp;
+    f3 lpos, lcol;
+    const float* __restrict__ jitter;
+    float* __restrict__ rgb;          // optional (W*H*3 floats)
+    int32_t* __restrict__ hit_idx;
+    float* __restrict__ hit_t;
+    uint8_t* __restrict__ p6;         // optional: write_p6-default samples (W*H*3 bytes)
+    uint32_t list_cap;                // binned path: entries bin_list holds; a tile whose list would
+                                      // reach past it takes the brute-force loop (exact, slower)
+    // chunked path (rt_render_hw1_device): work items of at most HW1_CHUNK list entries
+    const uint32_t* __restrict__ chunk_tile;   // per chunk: its tile
+    const uint32_t* __restrict__ chunk_first;  // per tile: its first chunk (exclusive prefix; [ntiles] = total)
+    uint32_t chunk_cap;                         // chunk_tile's entries
+    unsigned long long* __restrict__ keys;      // per (pixel, sample): min over chunks of (t bits << 32 | index)
+    uint32_t* __restrict__ zero_counts;         // resolve: counts + cursor (2 * ntiles) zeroed for the next frame
+    int32_t ntiles;
+};
+
+// HW1 shade (HW1/include/raytracer.h:21-48), material hard-coded at ray.h:111-114.
+__device__ __forceinline__ f3 shade_hw1(f3 o, f3 d, bool hit, f3 p, f3 n, f3 lpos, f3 lcol) {
+    if (!hit) {
+        const f3 ud = unit(d);
+        const float t = 0.5f * (ud.z + 1.0f);
+        return add(scale(mk(1.f, 1.f, 1.f), 1.0f - t), scale(mk(0.5f, 0.7f, 1.0f), t));
+    }
+    const f3 albedo = mk(0.8f, 0.2f, 0.2f);
+    const f3 ambient = scale(albedo, 0.1f);
+    const f3 lightDir = unit(sub(lpos, p));
+    const float diff = fmaxf(dot(n, lightDir), 0.0f);
+    const f3 diffuse = scale(mul(albedo, lcol), diff);
+    const f3 viewDir = unit(sub(o, p));
+    const f3 halfDir = unit(add(lightDir, viewDir));
+    const float spec = ref_powf(fmaxf(dot(n, halfDir), 0.0f), 64.0f);
+    f3 c = add(add(ambient, diffuse), scale(lcol, spec));
+    if (c.x > 1.0f) c.x = 1.0f;
+    if (c.y > 1.0f) c.y = 1.0f;
+    if (c.z > 1.0f) c.z = 1.0f;
+    return c;
+}
+
+// The pixel: the sample sum / float(spp) (HW1/src/render.cpp:113-115), as floats and/or as
+// write_p6-default samples (the frame epilogue fused in).
+__device__ __forceinline__ void hw1_write_pixel(const Hw1Params& P, int x, int y, f3 acc) {
+    const float fs = (float)P.spp;
+    const f3 px = mk(acc.x / fs, acc.y / fs, acc.z / fs);
+    const size_t k = ((size_t)y * P.W + x) * 3;
+    if (P.rgb) {
+        P.rgb[k] = px.x;
+        P.rgb[k + 1] = px.y;
+        P.rgb[k + 2] = px.z;
+    }
+    if (P.p6) {
+        P.p6[k] = rtp::p6_default_sample(px.x);
+        P.p6[k + 1] = rtp::p6_default_sample(px.y);
+        P.p6[k + 2] = rtp::p6_default_sample(px.z);
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void render_hw1_kernel(Hw1Params P) {
+    const int tiles_x = (P.W + 15) / 16;
+    const int tile = (int)blockIdx.x;
+    const int x = (tile % tiles_x) * 16 + (int)threadIdx.x % 16;
+    const int y = (tile / tiles_x) * 16 + (int)threadIdx.x / 16;
+    const bool valid = x < P.W && y < P.H;
+    f3 acc = mk(0.f, 0.f, 0.f);
+    for (int s = 0; s < P.spp; ++s) {
+        const float px = (float)x + P.jitter[2 * s];
+        const float py = (float)y + P.jitter[2 * s + 1];
+        const int ix = (int)px, iy = (int)py;  // get_pixel_position(int, int) truncates
+        const f3 pix = add(add(P.p00, scale(P.du, (float)ix)), scale(P.dv, (float)iy));
+        const f3 d = unit(sub(pix, P.center));  // HW1 Ray normalises (ray.h:25)
+        const f3 o = P.center;
+        float best = FLT_MAX;
+        int32_t besti = -1;
+        for (int k = 0; k < P.num_tris; ++k) {  // wave-uniform: triangle data via the scalar cache
+            const float4* T = P.tri + 3 * (size_t)k;
+            const float4 a = T[0], b = T[1], c = T[2];
+            float t, u, v;
+            if (valid && mt_hw1(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), t, u, v)) {
+                if (t < best) {  // rec.t < prev.t: the first index wins ties
+                    best = t;
+                    besti = k;
+                }
+            }
+        }
+        f3 p = mk(0.f, 0.f, 0.f), n = p;
+        const bool hit = besti >= 0;
+        if (hit) {
+            const float4* T = P.tri + 3 * (size_t)besti;
+            const float4 a = T[0], b = T[1], c = T[2];
+            float t, u, v;
+            mt_hw1(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), t, u, v);
+            p = add(o, scale(d, t));
+            const float4* N = P.nrm + 3 * (size_t)besti;
+            const float w = 1.0f - u - v;
+            n = add(add(scale(mk(N[0].x, N[0].y, N[0].z), w), scale(mk(N[1].x, N[1].y, N[1].z), u)),
+                    scale(mk(N[2].x, N[2].y, N[2].z), v));
+        }
+        acc = add(acc, shade_hw1(o, d, hit, p, n, P.lpos, P.lcol));
+        if (valid && P.hit_idx) {
+            const size_t kk = ((size_t)y * P.W + x) * (size_t)P.spp + (size_t)s;
+            P.hit_idx[kk] = besti;
+            P.hit_t[kk] = hit ? best : -1.0f;
+        }
+    }
+    if (valid) hw1_write_pixel(P, x, y, acc);
+}
+
+// ---- HW1 binned (rt_render_hw1 default; same output as render_hw1_kernel) ---------------
+// The brute-force loop's answer is the first index among the triangles ray_intersection
+// (mt_hw1) accepts with the smallest t.  Skipping triangles that provably cannot be accepted
+// for a ray, and visiting the rest in index order with the same strict `<`, gives that answer
+// bit for bit.  hw1_rect (hw1_rect_count_kernel) bounds, per triangle, the integer pixel positions (ix, iy)
+// whose camera ray mt_hw1 may accept; the render kernel gives each 16x16-pixel block the
+// triangles whose rectangle meets it, in index order.
+//
+// Why the rectangle is conservative.  With tvec = o - v0 and qvec = tvec x e1 (float, exactly
+// as mt_hw1 computes them, both ray-independent), mt_hw1's float quantities are
+//   det = d.(e2 x e1) + Ed,   U = d.(e2 x tvec) + Eu,   V = d.qvec + Ev,   tnum = e2.qvec,
+// u = U * (1/det), v = V * (1/det), t = tnum * (1/det), with |Ed|, |Eu|, |Ev| bounded by the
+// standard dot/cross rounding bounds (|d_j| <= 1).  When |tnum| is not tiny its sign s must
+// be det's (else t < 0), so acceptance needs four linear inequalities in d:
+//   s U >= 0,  s V >= 0,  s (det - U - V) >= -(4u|det| rounding of u + v and the divisions),
+//   s det >= FLT_EPSILON,
+// each relaxed by its error bound and by the rounding of unit() (d = D/|D| (1 + 3u)).  With
+// D = pixel00 + ix du + iy dv - center (exact, widened per axis by the tile-cull padding
+// for its float evaluation) and |D| in [Nmin, Nmax] over the image, every inequality becomes
+// a half-plane in (ix, iy); the rectangle is the bounding box (+1 pixel) of the padded image
+// rectangle clipped by the four half-planes.  Degenerate cases (tiny tnum, huge magnitudes,
+// an image whose directions reach 0) get the whole image.
+__device__ __forceinline__ void hw1_cross_d(const double a[3], const double b[3], double r[3]) {
+    r[0] = a[1] * b[2] - a[2] * b[1];
+    r[1] = a[2] * b[0] - a[0] * b[2];
+    r[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+__device__ int4 hw1_rect(const Hw1Params& P, int k) {
+    const int X0 = -2, X1 = P.W + 1, Y0 = -2, Y1 = P.H + 1;  // ix in [x, x+1] (truncation)
+    const int4 all = make_int4(X0, Y0, X1, Y1), none = make_int4(1, 1, 0, 0);
+    const float4 A = P.tri[3 * (size_t)k], B = P.tri[3 * (size_t)k + 1], Cq = P.tri[3 * (size_t)k + 2];
+    const f3 v0 = mk(A.x, A.y, A.z), e1 = mk(B.x, B.y, B.z), e2 = mk(Cq.x, Cq.y, Cq.z);
+    const f3 tvec = sub(P.center, v0);  // mt_hw1's own float values
+    const f3 qvec = cross(tvec, e1);
+    const float tnum = dot(e2, qvec);
+    double mag = 0.0;
+    const float mv[15] = {v0.x, v0.y, v0.z, e1.x, e1.y, e1.z, e2.x, e2.y, e2.z, tvec.x, tvec.y, tvec.z,
+                          qvec.x, qvec.y, qvec.z};
+    for (int i = 0; i < 15; ++i) mag = fmax(mag, fabs((double)mv[i]));
+    if (!(mag < 1e15) || !(fabsf(tnum) >= 1e-20f)) {
+        return all;
+    }
+    const double sg = tnum > 0.0f ? 1.0 : -1.0;
+    const double tv[3] = {tvec.x, tvec.y, tvec.z}, ea[3] = {e1.x, e1.y, e1.z}, eb[3] = {e2.x, e2.y, e2.z},
+                 qv[3] = {qvec.x, qvec.y, qvec.z};
+    double au[3], ad[3];
+    hw1_cross_d(eb, tv, au);  // U = tvec.(d x e2) = d.(e2 x tvec)
+    hw1_cross_d(eb, ea, ad);  // det = (d x e2).e1 = d.(e2 x e1)
+    const double uu = 0x1p-24, dm = 1.0001;
+    const double pb[3] = {fabs(eb[2]) + fabs(eb[1]), fabs(eb[0]) + fabs(eb[2]), fabs(eb[1]) + fabs(eb[0])};
+    double Eu = 0, Ed = 0, Ev = 0, dmax = 0;
+    for (int i = 0; i < 3; ++i) {
+        Eu += fabs(tv[i]) * pb[i];
+        Ed += fabs(ea[i]) * pb[i];
+        Ev += fabs(qv[i]);
+        dmax += fabs(ad[i]);
+    }
+    Eu *= 8 * uu * dm;
+    Ed *= 8 * uu * dm;
+    Ev *= 4 * uu * dm;
+    dmax = dmax * dm + Ed;
+    if (!(dmax < 1e10)) {  // keeps |t| = |tnum / det| >= 1e-30: a wrong-sign t stays negative
+        return all;
+    }
+    const double tiny = 1e-30;
+    double c[4][3], w[4];
+    for (int i = 0; i < 3; ++i) {
+        c[0][i] = sg * au[i];
+        c[1][i] = sg * qv[i];
+        c[2][i] = sg * (ad[i] - au[i] - qv[i]);
+        c[3][i] = sg * ad[i];
+    }
+    w[0] = -(Eu + tiny);
+    w[1] = -(Ev + tiny);
+    w[2] = -(4 * uu * dmax + Eu + Ev + Ed + tiny);
+    w[3] = (double)FLT_EPSILON - Ed;
+    // D over the image, per axis, padded as in tile_dirs
+    const double cc[3] = {P.center.x, P.center.y, P.center.z}, p0[3] = {P.p00.x, P.p00.y, P.p00.z},
+                 du[3] = {P.du.x, P.du.y, P.du.z}, dv[3] = {P.dv.x, P.dv.y, P.dv.z};
+    const double xm = fmax(fabs((double)X0), fabs((double)X1)), ym = fmax(fabs((double)Y0), fabs((double)Y1));
+    double D00[3], Dl[3], Dh[3], pad[3], scale = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        D00[a] = p0[a] - cc[a];
+        const double u0 = X0 * du[a], u1 = X1 * du[a], w0 = Y0 * dv[a], w1 = Y1 * dv[a];
+        Dl[a] = D00[a] + fmin(u0, u1) + fmin(w0, w1);
+        Dh[a] = D00[a] + fmax(u0, u1) + fmax(w0, w1);
+        pad[a] = 8.0 * 0x1p-23 * (fabs(cc[a]) + fabs(p0[a]) + xm * fabs(du[a]) + ym * fabs(dv[a]));
+        scale = fmax(scale, fmax(fabs(Dl[a]), fabs(Dh[a])));
+    }
+    double nmin2 = 0.0, nmax2 = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        pad[a] += 1e-5 * scale;
+        Dl[a] -= pad[a];
+        Dh[a] += pad[a];
+        const double near = Dl[a] > 0 ? Dl[a] : (Dh[a] < 0 ? Dh[a] : 0.0);
+        const double far = fmax(fabs(Dl[a]), fabs(Dh[a]));
+        nmin2 += near * near;
+        nmax2 += far * far;
+    }
+    const double nmin = sqrt(nmin2) * (1 - 1e-12), nmax = sqrt(nmax2) * (1 + 1e-12);
+    if (!(nmin > 0.0) || !(nmax < 1e300)) {
+        return all;
+    }
+    double px[8 + 4], py[8 + 4];
+    int n = 4;
+    px[0] = X0; py[0] = Y0;
+    px[1] = X1; py[1] = Y0;
+    px[2] = X1; py[2] = Y1;
+    px[3] = X0; py[3] = Y1;
+    for (int i = 0; i < 4 && n > 0; ++i) {
+        double cs = 0.0, cdm = 0.0, cpad = 0.0, cD00 = 0.0, al = 0.0, be = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            cs += fabs(c[i][a]);
+            cdm += fabs(c[i][a]) * fmax(fabs(Dl[a]), fabs(Dh[a]));
+            cpad += fabs(c[i][a]) * pad[a];
+            cD00 += c[i][a] * D00[a];
+            al += c[i][a] * du[a];
+            be += c[i][a] * dv[a];
+        }
+        const double w1 = w[i] - 4 * uu * dm * cs;              // unit() rounding of d
+        const double g = fmin(w1 * nmin, w1 * nmax);            // c.D >= w1 |D|
+        const double ga = g - cpad - 1e-9 * cdm - tiny - cD00;  // al ix + be iy >= ga
+        if (!(fabs(al) < 1e300 && fabs(be) < 1e300 && fabs(ga) < 1e300)) {
+            return all;
+        }
+        double qx[12], qy[12];
+        int m = 0;
+        for (int j = 0; j < n; ++j) {
+            const int jn = (j + 1) % n;
+            const double fc = al * px[j] + be * py[j] - ga, fn = al * px[jn] + be * py[jn] - ga;
+            if (fc >= 0) {
+                qx[m] = px[j];
+                qy[m] = py[j];
+                ++m;
+            }
+            if ((fc >= 0) != (fn >= 0)) {
+                const double tt = fc / (fc - fn);
+                qx[m] = px[j] + tt * (px[jn] - px[j]);
+                qy[m] = py[j] + tt * (py[jn] - py[j]);
+                ++m;
+            }
+        }
+        n = m;
+        for (int j = 0; j < n; ++j) {
+            px[j] = qx[j];
+            py[j] = qy[j];
+        }
+    }
+    if (n == 0) {
+        return none;
+    }
+    double lx = px[0], hx = px[0], ly = py[0], hy = py[0];
+    for (int j = 1; j < n; ++j) {
+        lx = fmin(lx, px[j]);
+        hx = fmax(hx, px[j]);
+        ly = fmin(ly, py[j]);
+        hy = fmax(hy, py[j]);
+    }
+    return make_int4(max(X0, (int)floor(lx) - 1), max(Y0, (int)floor(ly) - 1), min(X1, (int)ceil(hx) + 1),
+                     min(Y1, (int)ceil(hy) + 1));
+}
+
+// Binning (a tiled rasterizer's): hw1_rect_count_kernel counts, per 16x4-pixel wave tile, the
+// triangles whose rectangle meets the tile's (ix, iy) range (pixel x uses ix in {x, x+1});
+// hw1_scan_chunks_kernel turns the counts into offsets; hw1_fill_kernel writes the lists.  A list's
+// order is whatever the atomics give, so the render kernel keeps the lexicographic minimum of
+// (t, index): the smallest t, the smallest index among equal t — exactly the brute-force
+// loop's winner (it keeps the first index whose t is strictly below every earlier one), and
+// independent of the visiting order.  (A NaN t is never below or equal to anything, in
+// either form.)
+constexpr int HW1_TW = 16, HW1_TH = 4;  // wave tile: 16 x 4 pixels
+__device__ __forceinline__ bool hw1_tile_range(const Hw1Params& P, int4 r, int& tx0, int& tx1, int& ty0, int& ty1) {
+    const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW, tiles_y = (P.H + HW1_TH - 1) / HW1_TH;
+    if (r.x > r.z || r.y > r.w) return false;
+    tx0 = max(0, r.x - 1) / HW1_TW;
+    ty0 = max(0, r.y - 1) / HW1_TH;
+    tx1 = min(tiles_x - 1, r.z / HW1_TW);
+    ty1 = min(tiles_y - 1, r.w / HW1_TH);
+    return r.z >= 0 && r.w >= 0 && tx0 <= tx1 && ty0 <= ty1;
+}
+
+// The (triangle, tile) pairs of a wave's 64 triangles, 64 at a time over the wave's lanes: a
+// triangle covering many tiles no longer keeps one lane looping while the others wait (c2: 30 and
+// 25 us for the two passes with a lane per triangle).  Lane l's triangle covers cnt tiles from
+// (tx0, ty0), w per row; fn(tx, ty, triangle) runs once per pair.  Every lane of the wave calls
+// this (the shuffles read every lane).
+template <typename F>
+__device__ __forceinline__ void hw1_wave_pairs(uint32_t lane, int k, uint32_t cnt, int tx0, int ty0, int w, F&& fn) {
+    uint32_t incl = cnt;  // inclusive prefix sum over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, d);
+        if ((int)lane >= d) incl += v;
+    }
+    const uint32_t excl = incl - cnt;
+    const uint32_t total = uni((uint32_t)__shfl((int)incl, 63));
+    for (uint32_t base = 0; base < total; base += 64) {
+        const uint32_t p = base + lane;
+        // the pair's lane: the last one whose range starts at or before p (lanes without pairs
+        // start where the next lane does, so the last such lane has pairs)
+        int o = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const uint32_t e = (uint32_t)__shfl((int)excl, o + step);
+            if (e <= p) o += step;
+        }
+        const uint32_t local = p - (uint32_t)__shfl((int)excl, o);
+        const int ow = __shfl(w, o);
+        const int tx = __shfl(tx0, o) + (int)(local % (uint32_t)max(ow, 1));
+        const int ty = __shfl(ty0, o) + (int)(local / (uint32_t)max(ow, 1));
+        const int tri = __shfl(k, o);
+        if (p < total) fn(tx, ty, tri);
+    }
+}
+
+// Pass 1: each triangle's rectangle (kept for pass 2) and its count in every tile it meets.
+// (Launched with 64-thread blocks: one wave each.)
+__global__ __launch_bounds__(64) void hw1_rect_count_kernel(Hw1Params P, int4* __restrict__ rects,
+                                                            uint32_t* __restrict__ counts) {
+    const uint32_t lane = lane_id();
+    const int k = (int)(blockIdx.x * 64 + lane);
+    const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
+    int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;
+    if (k < P.num_tris) {
+        const int4 r = hw1_rect(P, k);
+        rects[k] = r;
+        if (!hw1_tile_range(P, r, tx0, tx1, ty0, ty1)) tx1 = tx0 - 1;
+    }
+    const uint32_t cnt = tx1 >= tx0 && ty1 >= ty0 ? (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1)) : 0u;
+    hw1_wave_pairs(lane, k, cnt, tx0, ty0, tx1 - tx0 + 1,
+                   [&](int tx, int ty, int) { atomicAdd(&counts[ty * tiles_x + tx], 1u); });
+}
+
+// Pass 2: the lists.  A tile whose list would reach past list_cap is not written; the render
+// kernel gives that tile the brute-force loop instead.
+__global__ __launch_bounds__(64) void hw1_fill_kernel(Hw1Params P, uint32_t* __restrict__ cursor,
+                                                      uint32_t* __restrict__ list) {
+    const uint32_t lane = lane_id();
+    const int k = (int)(blockIdx.x * 64 + lane);
+    const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
+    int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;
+    if (k < P.num_tris && !hw1_tile_range(P, P.rects[k], tx0, tx1, ty0, ty1)) tx1 = tx0 - 1;
+    const uint32_t cnt = tx1 >= tx0 && ty1 >= ty0 ? (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1)) : 0u;
+    hw1_wave_pairs(lane, k, cnt, tx0, ty0, tx1 - tx0 + 1, [&](int tx, int ty, int tri) {
+        const int t = ty * tiles_x + tx;
+        if (P.bin_offset[t + 1] <= P.list_cap) list[P.bin_offset[t] + atomicAdd(&cursor[t], 1u)] = (uint32_t)tri;
+    });
+}
+
+// The chunked pass: a tile's list is cut into work items of at most HW1_CHUNK entries (a tile
+// whose list does not fit the capacity is one item over every triangle), so a long list no
+// longer makes one wave the kernel's tail.
+constexpr uint32_t HW1_CHUNK = 64;
+
+// Exclusive prefix sum of n counts in one workgroup (n is the number of wave tiles, small);
+// offsets[n] = total.  With chunk_first: the same over the tiles' chunk counts, and every
+// chunk's tile in chunk_tile (at most chunk_cap; chunks past it are not written, the total in
+// chunk_first[n] says how many there were).
+__global__ __launch_bounds__(1024) void hw1_scan_chunks_kernel(const uint32_t* __restrict__ counts,
+                                                               uint32_t* __restrict__ offsets, int n, uint32_t list_cap,
+                                                               uint32_t* __restrict__ chunk_first,
+                                                               uint32_t* __restrict__ chunk_tile, uint32_t chunk_cap) {
+    __shared__ uint32_t part[1024], cpart[1024];
+    const int t = (int)threadIdx.x;
+    const int per = (n + 1023) / 1024;
+    const int lo = min(n, t * per), hi = min(n, lo + per);
+    uint32_t sum = 0;
+    for (int i = lo; i < hi; ++i) sum += counts[i];
+    part[t] = sum;
+    __syncthreads();
+    for (int st = 1; st < 1024; st <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t v = t >= st ? part[t - st] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    // the tiles' chunk counts need the tiles' offsets (a list past the capacity: one chunk)
+    uint32_t run = part[t] - sum, csum = 0;
+    for (int i = lo; i < hi; ++i) {
+        offsets[i] = run;
+        const uint32_t c = counts[i];
+        csum += run + c > list_cap ? 1u : (c + HW1_CHUNK - 1) / HW1_CHUNK;
+        run += c;
+    }
+    if (t == 1023) offsets[n] = part[1023];
+    cpart[t] = csum;
+    __syncthreads();
+    for (int st = 1; st < 1024; st <<= 1) {
+        const uint32_t v = t >= st ? cpart[t - st] : 0u;
+        __syncthreads();
+        cpart[t] += v;
+        __syncthreads();
+    }
+    uint32_t crun = cpart[t] - csum;
+    run = part[t] - sum;
+    for (int i = lo; i < hi; ++i) {
+        chunk_first[i] = crun;
+        const uint32_t c = counts[i];
+        const uint32_t nc = run + c > list_cap ? 1u : (c + HW1_CHUNK - 1) / HW1_CHUNK;
+        for (uint32_t k = 0; k < nc; ++k)
+            if (crun + k < chunk_cap) chunk_tile[crun + k] = (uint32_t)i;
+        crun += nc;
+        run += c;
+    }
+    if (t == 1023) chunk_first[n] = cpart[1023];
+}
+
+// One wave per chunk, grid-stride over the frame's chunks: the tile's 64 pixel lanes run mt_hw1
+// over the chunk's entries and fold each sample's winner into keys with a 64-bit atomicMin of
+// (t bits << 32 | index).  t >= 0 and never -0 (t + 0.0f), so its bits order like its value; the
+// minimum over the chunks is the lexicographic (t, index) minimum of the whole list -- the
+// brute-force loop's winner (rec.t < prev.t keeps the first index).
+__global__ __launch_bounds__(BLOCK) void render_hw1_chunks_kernel(Hw1Params P) {
+    const uint32_t total = uni(P.chunk_first[P.ntiles]);
+    const uint32_t nchunks = total < P.chunk_cap ? total : P.chunk_cap;
+    const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
+    const uint32_t lane = lane_id();
+    const uint32_t waves = gridDim.x * (BLOCK / 64);
+    for (uint32_t j = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64; j < nchunks; j += waves) {
+        const uint32_t tidx = uni(P.chunk_tile[uni(j)]);
+        const uint32_t c = j - uni(P.chunk_first[tidx]);
+        const uint32_t cnt = uni(P.bin_count[tidx]);
+        const uint32_t off = uni(P.bin_offset[tidx]);
+        const bool all = off + cnt > P.list_cap;  // the list was not written: every triangle, in order
+        const uint32_t b = all ? 0u : c * HW1_CHUNK;
+        const uint32_t e = all ? (uint32_t)P.num_tris : min(cnt, b + HW1_CHUNK);
+        const int x = (int)(tidx % tiles_x) * HW1_TW + (int)(lane % HW1_TW);
+        const int y = (int)(tidx / tiles_x) * HW1_TH + (int)(lane / HW1_TW);
+        const bool valid = x < P.W && y < P.H;
+        for (int s = 0; s < P.spp; ++s) {
+            const float pxs = (float)x + P.jitter[2 * s];
+            const float pys = (float)y + P.jitter[2 * s + 1];
+            const int ix = (int)pxs, iy = (int)pys;  // get_pixel_position(int, int) truncates
+            const f3 pix = add(add(P.p00, scale(P.du, (float)ix)), scale(P.dv, (float)iy));
+            const f3 d = unit(sub(pix, P.center));  // HW1 Ray normalises (ray.h:25)
+            const f3 o = P.center;
+            unsigned long long best = ~0ull;
+            for (uint32_t i = b; i < e; i += 4) {
+                int kk[4];
+                float4 tq[12];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    kk[q] = i + q < e ? (all ? (int)(i + q) : (int)ldc_u32(P.bin_list + off + i + q)) : -1;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4* T = P.tri + 3 * (size_t)(kk[q] < 0 ? kk[0] : kk[q]);
+                    tq[3 * q] = ldc(T);
+                    tq[3 * q + 1] = ldc(T + 1);
+                    tq[3 * q + 2] = ldc(T + 2);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 a = tq[3 * q], bq = tq[3 * q + 1], cq = tq[3 * q + 2];
+                    float t, u, v;
+                    // (t < FLT_MAX: the loop's `t < best` from best = FLT_MAX never takes FLT_MAX,
+                    // +inf or NaN)
+                    if (valid && kk[q] >= 0 &&
+                        mt_hw1(o, d, mk(a.x, a.y, a.z), mk(bq.x, bq.y, bq.z), mk(cq.x, cq.y, cq.z), t, u, v) &&
+                        t < FLT_MAX) {
+                        const unsigned long long key =
+                            (unsigned long long)__float_as_uint(t + 0.0f) << 32 | (uint32_t)kk[q];
+                        best = key < best ? key : best;
+                    }
+                }
+            }
+            if (valid && best != ~0ull) atomicMin(&P.keys[((size_t)y * P.W + x) * (size_t)P.spp + (size_t)s], best);
+        }
+    }
+}
+
+// Per pixel: each sample's winner from keys (then reset for the next frame), HW1 shade, the
+// average, AOVs; the first threads also zero the bin counters for the next frame.
+__global__ __launch_bounds__(BLOCK) void hw1_resolve_kernel(Hw1Params P) {
+    const int gid = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    if (gid < 2 * P.ntiles) P.zero_counts[gid] = 0u;
+    if (gid >= P.W * P.H) return;
+    const int x = gid % P.W, y = gid / P.W;
+    f3 acc = mk(0.f, 0.f, 0.f);
+    for (int s = 0; s < P.spp; ++s) {
+        const float pxs = (float)x + P.jitter[2 * s];
+        const float pys = (float)y + P.jitter[2 * s + 1];
+        const int ix = (int)pxs, iy = (int)pys;
+        const f3 pix = add(add(P.p00, scale(P.du, (float)ix)), scale(P.dv, (float)iy));
+        const f3 d = unit(sub(pix, P.center));
+        const f3 o = P.center;
+        const size_t kk = (size_t)gid * (size_t)P.spp + (size_t)s;
+        const unsigned long long key = P.keys[kk];
+        P.keys[kk] = ~0ull;
+        const bool hit = key != ~0ull;
+        const int32_t besti = hit ? (int32_t)(uint32_t)key : -1;
+        f3 p = mk(0.f, 0.f, 0.f), n = p;
+        float best = FLT_MAX;
+        if (hit) {  // the accepting test's own t, u, v
+            const float4* T = P.tri + 3 * (size_t)besti;
+            const float4 a = T[0], b = T[1], cq = T[2];
+            float t, u, v;
+            mt_hw1(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(cq.x, cq.y, cq.z), t, u, v);
+            best = t;
+            p = add(o, scale(d, t));
+            const float4* N = P.nrm + 3 * (size_t)besti;
+            const float wgt = 1.0f - u - v;
+            n = add(add(scale(mk(N[0].x, N[0].y, N[0].z), wgt), scale(mk(N[1].x, N[1].y, N[1].z), u)),
+                    scale(mk(N[2].x, N[2].y, N[2].z), v));
+        }
+        acc = add(acc, shade_hw1(o, d, hit, p, n, P.lpos, P.lcol));
+        if (P.hit_idx) {
+            P.hit_idx[kk] = besti;
+            P.hit_t[kk] = hit ? best : -1.0f;
+        }
+    }
+    hw1_write_pixel(P, x, y, acc);
+}
+
+}  // namespace
+
+using rt::set_error;
+using rt::hip_msg;
+using rt::DevBuf;
+using rt::check_device;
+using rt::DeviceGuard;
+
+extern "C" int rt_render_hw1(int device, const rt_vec3* pos, const rt_vec3* nrm, const uint32_t* idx, size_t P,
+                             const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp, const float* jitter,
+                             float* rgb_host, int32_t* hit_idx_host, float* hit_t_host) {
+    return rt_render_hw1_ex(device, pos, nrm, idx, P, cam, lpos, lcol, spp, jitter, 0, rgb_host, hit_idx_host,
+                            hit_t_host, nullptr);
+}
+
+// ---- HW1 resident scene (the C2 configuration's device path) ---------------------------
+// The mesh packed once (v0, e1, e2 as ray_intersection computes them, the three normals per
+// triangle), the binning buffers kept across frames.  A frame is four launches on the caller's
+// stream (counts zeroed, rect + count, scan, fill, render) and no host synchronisation: the
+// bin list's capacity is checked on the device (a tile whose list would not fit takes the
+// brute-force loop), and the host grows it from the latest finished frame's total.
+struct rt_hw1_scene {
+    int device = 0;
+    size_t P = 0;
+    DevBuf tri, nrm, rects, bins, list, jitter;
+    DevBuf chunks;             // chunk_first (ntiles + 1) | chunk_tile (chunk_cap)
+    DevBuf keys;               // per (pixel, sample): the chunked pass's winners, kept at ~0 between frames
+    int bins_tiles = -1;       // tiles the bins buffer is laid out for
+    size_t keys_n = 0;         // samples the keys buffer holds
+    uint32_t list_cap = 0, chunk_cap = 0;
+    int jitter_spp = -1;
+    std::vector<float> jitter_host;
+    static constexpr int kRing = 64;
+    hipEvent_t e0[kRing] = {}, e1[kRing] = {};
+    uint32_t* total_host = nullptr;  // pinned: the list total of frame f at [f % kRing]
+    uint64_t frames = 0;
+    hipStream_t last_stream = nullptr;
+    const char* last_kernel = "";
+    // rt_render_hw1_deliver: frames rendered into a ring of kDeliver device P6 bodies, each body
+    // copied to the caller's host buffer on the copy stream while the next frames render
+    static constexpr int kDeliver = 3;
+    DevBuf dp6[kDeliver];
+    hipStream_t copy = nullptr;
+    hipEvent_t rdone[kRing] = {}, cdone[kRing] = {};  // per ticket: rendered, copied
+    uint64_t tickets = 0;
+    ~rt_hw1_scene() {
+        for (int i = 0; i < kRing; ++i) {
+            if (e0[i]) (void)hipEventSynchronize(e1[i]);
+            if (e0[i]) (void)hipEventDestroy(e0[i]);
+            if (e1[i]) (void)hipEventDestroy(e1[i]);
+            if (cdone[i]) (void)hipEventSynchronize(cdone[i]);
+            if (rdone[i]) (void)hipEventDestroy(rdone[i]);
+            if (cdone[i]) (void)hipEventDestroy(cdone[i]);
+        }
+        if (copy) (void)hipStreamDestroy(copy);
+        if (total_host) (void)hipHostFree(total_host);
+    }
+};
+
+extern "C" int rt_hw1_scene_create(int device, const rt_vec3* pos, const rt_vec3* nrm, const uint32_t* idx, size_t P,
+                                   rt_hw1_scene** out) {
+    if (!out) return set_error(RT_ERR_ARG, "rt_hw1_scene_create: null out");
+    *out = nullptr;
+    if (!pos || !nrm || !idx || P == 0)
+        return set_error(RT_ERR_ARG, "rt_hw1_scene_create: bad argument (HW1 requires per-vertex normals)");
+    if (P > 0x7FFFFFFFull) return set_error(RT_ERR_UNSUPPORTED, "too many triangles");
+    int rc = check_device(device);
+    if (rc != RT_OK) return rc;
+    DeviceGuard g(device);
+    std::vector<float4> ht(3 * P), hn(3 * P);
+    for (size_t k = 0; k < P; ++k) {
+        const rt_vec3 a = pos[idx[3 * k]], b = pos[idx[3 * k + 1]], c = pos[idx[3 * k + 2]];
+        // e1 = v1 - v0, e2 = v2 - v0 exactly as ray_intersection computes them (HW1/include/ray.h:71-72)
+        ht[3 * k] = make_float4(a.x, a.y, a.z, 0.f);
+        ht[3 * k + 1] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, 0.f);
+        ht[3 * k + 2] = make_float4(c.x - a.x, c.y - a.y, c.z - a.z, 0.f);
+        for (int j = 0; j < 3; ++j) {
+            const rt_vec3 n = nrm[idx[3 * k + j]];
+            hn[3 * k + j] = make_float4(n.x, n.y, n.z, 0.f);
+        }
+    }
+    std::unique_ptr<rt_hw1_scene> s(new (std::nothrow) rt_hw1_scene());
+    if (!s) return set_error(RT_ERR_NOMEM, "out of memory");
+    s->device = device;
+    s->P = P;
+    if ((rc = s->tri.upload(ht.data(), ht.size() * sizeof(float4))) != RT_OK) return rc;
+    if ((rc = s->nrm.upload(hn.data(), hn.size() * sizeof(float4))) != RT_OK) return rc;
+    if ((rc = s->rects.alloc(P * sizeof(int4))) != RT_OK) return rc;
+    // a first capacity: a few tiles per triangle (grown from the frames' totals)
+    s->list_cap = uint32_t(std::min<size_t>(std::max<size_t>(4 * P, size_t(1) << 16), 0x7FFFFFFFull));
+    if ((rc = s->list.alloc(size_t(s->list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->total_host), rt_hw1_scene::kRing * sizeof(uint32_t),
+                          hipHostMallocDefault));
+    for (int i = 0; i < rt_hw1_scene::kRing; ++i) {
+        s->total_host[i] = 0;
+        HIP_TRY(hipEventCreate(&s->e0[i]));
+        HIP_TRY(hipEventCreate(&s->e1[i]));
+    }
+    *out = s.release();
+    return RT_OK;
+}
+
+extern "C" void rt_hw1_scene_destroy(rt_hw1_scene* s) {
+    if (!s) return;
+    DeviceGuard g(s->device);
+    delete s;
+}
+
+extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp,
+                                    const float* jitter, int flags, float* rgb_dev, uint8_t* p6_dev,
+                                    int32_t* hit_idx_dev, float* hit_t_dev, void* stream) {
+    if (!s || !cam || spp < 1) return set_error(RT_ERR_ARG, "rt_render_hw1_device: bad argument");
+    if ((hit_idx_dev == nullptr) != (hit_t_dev == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
+    const int W = cam->pixel_width, H = cam->pixel_height;
+    if (W < 1 || H < 1) return set_error(RT_ERR_ARG, "camera has no pixels");
+    DeviceGuard g(s->device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int rc;
+    // jitter_samples(spp, 42u) offsets in [0,1) (HW1/include/antialias.h:12-27), or the caller's
+    std::vector<float> tab(2 * size_t(spp));
+    if (jitter) std::memcpy(tab.data(), jitter, tab.size() * sizeof(float));
+    else if ((rc = rt_jittered_samples(spp, 42u, 0, tab.data())) != RT_OK) return rc;
+    if (s->jitter_spp != spp || s->jitter_host != tab) {
+        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->e1[(s->frames - 1) % rt_hw1_scene::kRing]));
+        if ((rc = s->jitter.upload(tab.data(), tab.size() * sizeof(float))) != RT_OK) return rc;
+        s->jitter_spp = spp;
+        s->jitter_host = tab;
+    }
+    const bool brute = (flags & RT_HW1_BRUTE) != 0;
+    const int ntiles = ((W + HW1_TW - 1) / HW1_TW) * ((H + HW1_TH - 1) / HW1_TH);
+    // the latest finished frame's list total (frames are scanned back to front, non-blocking)
+    for (uint64_t b = 1; b <= std::min<uint64_t>(s->frames, 4); ++b) {
+        const int sl = int((s->frames - b) % rt_hw1_scene::kRing);
+        if (hipEventQuery(s->e1[sl]) != hipSuccess) continue;
+        const uint32_t tot = s->total_host[sl];
+        if (tot > s->list_cap) {  // grow (the old list may still be read by frames in flight)
+            HIP_TRY(hipEventSynchronize(s->e1[(s->frames - 1) % rt_hw1_scene::kRing]));
+            s->list_cap = uint32_t(std::min<uint64_t>(uint64_t(tot) + tot / 4 + 1024, 0x7FFFFFFFull));
+            if ((rc = s->list.alloc(size_t(s->list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
+            s->bins_tiles = -1;  // the chunk table follows the list's capacity
+        }
+        break;
+    }
+    (void)hipGetLastError();  // a not-ready query is not an error of this call
+    const size_t nsamples = size_t(W) * size_t(H) * size_t(spp);
+    if (!brute && (s->bins_tiles != ntiles || s->keys_n != nsamples)) {
+        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->e1[(s->frames - 1) % rt_hw1_scene::kRing]));
+        // counts | cursor | offsets (ntiles + 1): counts and cursor zeroed here, then by every
+        // frame's resolve pass for the next
+        if ((rc = s->bins.alloc(size_t(3 * ntiles + 1) * sizeof(uint32_t))) != RT_OK) return rc;
+        HIP_TRY(hipMemset(s->bins.p, 0, size_t(2 * ntiles) * sizeof(uint32_t)));
+        // chunks: at most one per HW1_CHUNK listed entries plus one per tile
+        s->chunk_cap = uint32_t(std::min<uint64_t>(uint64_t(s->list_cap) / HW1_CHUNK + uint64_t(ntiles) + 1, 0x7FFFFFFFull));
+        if ((rc = s->chunks.alloc((size_t(ntiles) + 1 + s->chunk_cap) * sizeof(uint32_t))) != RT_OK) return rc;
+        if ((rc = s->keys.alloc(nsamples * sizeof(unsigned long long))) != RT_OK) return rc;
+        HIP_TRY(hipMemset(s->keys.p, 0xFF, nsamples * sizeof(unsigned long long)));
+        s->bins_tiles = ntiles;
+        s->keys_n = nsamples;
+    }
+    Hw1Params hp;
+    hp.tri = static_cast<const float4*>(s->tri.p);
+    hp.nrm = static_cast<const float4*>(s->nrm.p);
+    hp.num_tris = int32_t(s->P);
+    hp.center = f3{cam->center.x, cam->center.y, cam->center.z};
+    hp.p00 = f3{cam->pixel00_loc.x, cam->pixel00_loc.y, cam->pixel00_loc.z};
+    hp.du = f3{cam->pixel_delta_u.x, cam->pixel_delta_u.y, cam->pixel_delta_u.z};
+    hp.dv = f3{cam->pixel_delta_v.x, cam->pixel_delta_v.y, cam->pixel_delta_v.z};
+    hp.W = W;
+    hp.H = H;
+    hp.spp = spp;
+    hp.lpos = f3{lpos.x, lpos.y, lpos.z};
+    hp.lcol = f3{lcol.x, lcol.y, lcol.z};
+    hp.jitter = static_cast<const float*>(s->jitter.p);
+    hp.rgb = rgb_dev;
+    hp.hit_idx = hit_idx_dev;
+    hp.hit_t = hit_t_dev;
+    hp.p6 = p6_dev;
+    hp.rects = static_cast<const int4*>(s->rects.p);
+    hp.bin_count = hp.bin_offset = hp.bin_list = nullptr;
+    hp.list_cap = s->list_cap;
+    hp.chunk_first = hp.chunk_tile = nullptr;
+    hp.chunk_cap = s->chunk_cap;
+    hp.keys = static_cast<unsigned long long*>(s->keys.p);
+    hp.zero_counts = static_cast<uint32_t*>(s->bins.p);
+    hp.ntiles = ntiles;
+    const int sl = int(s->frames % rt_hw1_scene::kRing);
+    // the scene's buffers are shared by its frames: a frame on another stream waits for the last
+    if (s->frames > 0 && st != s->last_stream)
+        HIP_TRY(hipStreamWaitEvent(st, s->e1[(s->frames - 1) % rt_hw1_scene::kRing], 0));
+    s->last_stream = st;
+    HIP_TRY(hipEventRecord(s->e0[sl], st));
+    const int blocks = ((W + 15) / 16) * ((H + 15) / 16);
+    if (brute) {
+        hipLaunchKernelGGL(render_hw1_kernel, dim3(blocks), dim3(BLOCK), 0, st, hp);
+        s->last_kernel = "render_hw1_kernel";
+    } else {
+        // one wave per 64 triangles (a block each): the per-triangle passes spread over every CU
+        // (256-thread blocks kept c2's 19,858 triangles on 78 CUs: 30 + 25 us)
+        const dim3 tgrid(unsigned((s->P + 63) / 64));
+        uint32_t* counts = static_cast<uint32_t*>(s->bins.p);  // zeroed by the previous frame's resolve
+        uint32_t* cursor = counts + ntiles;
+        uint32_t* offsets = cursor + ntiles;  // ntiles + 1 entries
+        uint32_t* cfirst = static_cast<uint32_t*>(s->chunks.p);
+        uint32_t* ctile = cfirst + ntiles + 1;
+        hipLaunchKernelGGL(hw1_rect_count_kernel, tgrid, dim3(64), 0, st, hp, static_cast<int4*>(s->rects.p), counts);
+        hipLaunchKernelGGL(hw1_scan_chunks_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, ntiles, s->list_cap,
+                           cfirst, ctile, s->chunk_cap);
+        hp.bin_count = counts;
+        hp.bin_offset = offsets;
+        hp.bin_list = static_cast<const uint32_t*>(s->list.p);
+        hp.chunk_first = cfirst;
+        hp.chunk_tile = ctile;
+        hipLaunchKernelGGL(hw1_fill_kernel, tgrid, dim3(64), 0, st, hp, cursor, static_cast<uint32_t*>(s->list.p));
+        // chunks grid-stride over a grid of every CU's worth of waves (the count is on the device)
+        hipLaunchKernelGGL(render_hw1_chunks_kernel, dim3(1024), dim3(BLOCK), 0, st, hp);
+        const int rgrid = (std::max(W * H, 2 * ntiles) + BLOCK - 1) / BLOCK;
+        hipLaunchKernelGGL(hw1_resolve_kernel, dim3(rgrid), dim3(BLOCK), 0, st, hp);
+        s->last_kernel = "render_hw1_chunks_kernel";
+        HIP_TRY(hipGetLastError());
+        // this frame's total, for the capacity of the next ones
+        HIP_TRY(hipMemcpyAsync(s->total_host + sl, offsets + ntiles, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(s->e1[sl], st));
+    s->frames++;
+    return RT_OK;
+}
+
+// A frame delivered to host memory (C2's bench step, as rt_renderer delivers G/ frames): the
+// frame's P6 body is rendered into ring slot k % kDeliver (after that slot's previous copy), and
+// copied on the scene's copy stream once the frame's kernels are done, so the copy of frame k
+// overlaps the kernels of frame k+1 instead of following them on one stream (VERDICT r05 item 8:
+// 0.129 ms per step against 0.096 of kernels when the caller copied on the render stream).
+extern "C" int rt_render_hw1_deliver(rt_hw1_scene* s, const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp,
+                                     int flags, uint8_t* host_p6, void* stream, uint64_t* ticket) {
+    if (!s || !cam || !host_p6 || !ticket || spp < 1) return set_error(RT_ERR_ARG, "rt_render_hw1_deliver: bad argument");
+    const int W = cam->pixel_width, H = cam->pixel_height;
+    if (W < 1 || H < 1) return set_error(RT_ERR_ARG, "camera has no pixels");
+    DeviceGuard g(s->device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (!s->copy) {
+        HIP_TRY(hipStreamCreateWithFlags(&s->copy, hipStreamNonBlocking));
+        for (int i = 0; i < rt_hw1_scene::kRing; ++i) {
+            HIP_TRY(hipEventCreateWithFlags(&s->rdone[i], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s->cdone[i], hipEventDisableTiming));
+        }
+    }
+    const uint64_t k = s->tickets;
+    const int slot = int(k % rt_hw1_scene::kDeliver), ring = int(k % rt_hw1_scene::kRing);
+    const size_t bytes = size_t(W) * size_t(H) * 3;
+    // ticket k - kRing used these events: it must be complete before they are recorded again
+    if (k >= uint64_t(rt_hw1_scene::kRing)) HIP_TRY(hipEventSynchronize(s->cdone[ring]));
+    if (s->dp6[slot].n < bytes) {
+        if (k >= uint64_t(rt_hw1_scene::kDeliver))  // the slot's previous frame may still be copied
+            HIP_TRY(hipEventSynchronize(s->cdone[(k - rt_hw1_scene::kDeliver) % rt_hw1_scene::kRing]));
+        int rc = s->dp6[slot].alloc(bytes);
+        if (rc != RT_OK) return rc;
+    } else if (k >= uint64_t(rt_hw1_scene::kDeliver)) {
+        HIP_TRY(hipStreamWaitEvent(st, s->cdone[(k - rt_hw1_scene::kDeliver) % rt_hw1_scene::kRing], 0));
+    }
+    int rc = rt_render_hw1_device(s, cam, lpos, lcol, spp, nullptr, flags, nullptr,
+                                  static_cast<uint8_t*>(s->dp6[slot].p), nullptr, nullptr, stream);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipEventRecord(s->rdone[ring], st));
+    HIP_TRY(hipStreamWaitEvent(s->copy, s->rdone[ring], 0));
+    HIP_TRY(hipMemcpyAsync(host_p6, s->dp6[slot].p, bytes, hipMemcpyDeviceToHost, s->copy));
+    HIP_TRY(hipEventRecord(s->cdone[ring], s->copy));
+    *ticket = k;
+    s->tickets++;
+    return RT_OK;
+}
+
+// Wait until frame `ticket` of rt_render_hw1_deliver is in its host buffer (one of the last
+// 64 delivered frames).
+extern "C" int rt_hw1_wait(rt_hw1_scene* s, uint64_t ticket) {
+    if (!s) return set_error(RT_ERR_ARG, "rt_hw1_wait: null scene");
+    if (ticket >= s->tickets || ticket + rt_hw1_scene::kRing < s->tickets)
+        return set_error(RT_ERR_ARG, "rt_hw1_wait: not one of the last 64 delivered frames");
+    DeviceGuard g(s->device);
+    HIP_TRY(hipEventSynchronize(s->cdone[ticket % rt_hw1_scene::kRing]));
+    return RT_OK;
+}
+
+extern "C" int rt_hw1_kernel_times(const rt_hw1_scene* s, float* ms_out, int max, int* n_out) {
+    if (!s || !ms_out || !n_out || max < 0) return set_error(RT_ERR_ARG, "rt_hw1_kernel_times: bad argument");
+    DeviceGuard g(s->device);
+    const int n = int(std::min<uint64_t>({uint64_t(max), s->frames, uint64_t(rt_hw1_scene::kRing)}));
+    for (int i = 0; i < n; ++i) {
+        const int sl = int((s->frames - uint64_t(n - i)) % rt_hw1_scene::kRing);
+        HIP_TRY(hipEventSynchronize(s->e1[sl]));
+        HIP_TRY(hipEventElapsedTime(&ms_out[i], s->e0[sl], s->e1[sl]));
+    }
+    *n_out = n;
+    return RT_OK;
+}
+
+extern "C" const char* rt_hw1_kernel_name(const rt_hw1_scene* s) { return s ? s->last_kernel : ""; }
+
+extern "C" int rt_hw1_list_info(const rt_hw1_scene* s, int64_t info[2]) {
+    if (!s || !info) return set_error(RT_ERR_ARG, "rt_hw1_list_info: null argument");
+    DeviceGuard g(s->device);
+    info[0] = s->list_cap;
+    info[1] = 0;
+    if (s->frames > 0) {
+        const int sl = int((s->frames - 1) % rt_hw1_scene::kRing);
+        HIP_TRY(hipEventSynchronize(s->e1[sl]));
+        info[1] = s->total_host[sl];
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_render_hw1_ex(int device, const rt_vec3* pos, const rt_vec3* nrm, const uint32_t* idx, size_t P,
+                                const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp, const float* jitter,
+                                int flags, float* rgb_host, int32_t* hit_idx_host, float* hit_t_host,
+                                float* kernel_ms) {
+    if (!pos || !nrm || !idx || !cam || !rgb_host || spp < 1 || P == 0)
+        return set_error(RT_ERR_ARG, "rt_render_hw1: bad argument (HW1 requires per-vertex normals)");
+    if ((hit_idx_host == nullptr) != (hit_t_host == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
+    rt_hw1_scene* sp = nullptr;
+    int rc = rt_hw1_scene_create(device, pos, nrm, idx, P, &sp);
+    if (rc != RT_OK) return rc;
+    std::unique_ptr<rt_hw1_scene, void (*)(rt_hw1_scene*)> s(sp, rt_hw1_scene_destroy);
+    DeviceGuard g(device);
+    const int W = cam->pixel_width, H = cam->pixel_height;
+    const size_t npx = size_t(std::max(W, 0)) * size_t(std::max(H, 0));
+    DevBuf drgb, dhi, dht;
+    if ((rc = drgb.alloc(npx * 3 * sizeof(float))) != RT_OK) return rc;
+    if (hit_idx_host) {
+        if ((rc = dhi.alloc(npx * size_t(spp) * sizeof(int32_t))) != RT_OK) return rc;
+        if ((rc = dht.alloc(npx * size_t(spp) * sizeof(float))) != RT_OK) return rc;
+    }
+    rc = rt_render_hw1_device(sp, cam, lpos, lcol, spp, jitter, flags, static_cast<float*>(drgb.p), nullptr,
+                              static_cast<int32_t*>(dhi.p), static_cast<float*>(dht.p), nullptr);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    if (kernel_ms) {
+        int n = 0;
+        if ((rc = rt_hw1_kernel_times(sp, kernel_ms, 1, &n)) != RT_OK) return rc;
+    }
+    HIP_TRY(hipMemcpy(rgb_host, drgb.p, npx * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    if (hit_idx_host) {
+        HIP_TRY(hipMemcpy(hit_idx_host, dhi.p, npx * size_t(spp) * sizeof(int32_t), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(hit_t_host, dht.p, npx * size_t(spp) * sizeof(float), hipMemcpyDeviceToHost));
+    }
+    return RT_OK;
+}

@@ -11,7 +11,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/build/variants/$NAME
 SRC=${SRC:-$ROOT/raytracinginonesemester_amd/csrc/rt_device.hip}
 mkdir -p "$OUT"
-if [ ! -f "$ROOT/build/obj/rt_host.o" ]; then
+if [ ! -f "$ROOT/build/obj/rt_host.o" ] || [ ! -f "$ROOT/build/obj/rt_hw1.o" ]; then
   python3 -c "import sys; sys.path.insert(0, '$ROOT'); from raytracinginonesemester_amd import build; build.build()" > /dev/null
 fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall \
@@ -23,7 +23,7 @@ VID=$( (cat "$SRC"; printf '%s\0' "$@") | sha256sum | cut -c1-64)
 printf 'static const char tag[] __attribute__((used)) = "variant:%s:%s";\nconst char* rt_build_id(void) { return tag; }\n' \
     "$NAME" "$VID" > "$OUT/rt_build_id.c"
 gcc -O2 -fPIC -c "$OUT/rt_build_id.c" -o "$OUT/rt_build_id.o"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$ROOT/build/obj/rt_host.o" "$OUT/rt_device.o" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$ROOT/build/obj/rt_host.o" "$ROOT/build/obj/rt_records.o" "$OUT/rt_device.o" "$ROOT/build/obj/rt_hw1.o" \
     "$ROOT/build/obj/rt_frame.o" "$ROOT/build/obj/rt_lbvh.o" "$ROOT/build/obj/rt_renderer.o" "$OUT/rt_build_id.o" \
     -o "$OUT/librt_mi355x.so"
 rm -f "$OUT/rt_device.o" "$OUT/rt_build_id.o"  # only the library travels to the GPU box

@@ -55,6 +55,40 @@ def test_resident_hw1_frames_match_reference(name, cfg):
         sc.close()
 
 
+@pytest.mark.parametrize("name,cfg", [("c1_full", "c1"), ("c2_full", "c2")])
+def test_delivered_hw1_frames_match_reference(name, cfg):
+    """rt_render_hw1_deliver (the C1/C2 bench step): frames pipelined 3 deep into pinned host
+    buffers, each copied on the scene's copy stream while the next renders; every delivered body
+    is the reference's P6 file, including frames whose device ring slot and host buffer were
+    reused, and a stale ticket is refused."""
+    c = configs.HW1_CONFIGS[cfg]
+    meta = golden_meta(name)
+    W, H = meta["width"], meta["height"]
+    mesh = rt.MeshHW1(configs.MESHES / c["mesh"])
+    cam = rt.Camera(c["position"], c["look_at"], c["up"], c["focal_mm"], c["sensor_mm"], W, H, hw1=True)
+    want = gzip.open(GOLDEN / "scenes" / name / "image.ppm.gz").read()
+    sc = rt.HW1Scene(mesh.positions, mesh.normals, mesh.indices)
+    host = [torch.zeros(W * H * 3, dtype=torch.uint8, pin_memory=True) for _ in range(3)]
+    st = torch.cuda.Stream()
+    try:
+        pend = []
+        for k in range(12):
+            if len(pend) >= 2:
+                t, b = pend.pop(0)
+                sc.wait(t)
+                assert rt.p6_header(W, H) + host[b].numpy().tobytes() == want, (k, t)
+                host[b].zero_()
+            pend.append((sc.render_deliver(cam, c["light_pos"], c["light_color"], c["spp"], host[k % 3].data_ptr(),
+                                           stream=st.cuda_stream), k % 3))
+        for t, b in pend:
+            sc.wait(t)
+            assert rt.p6_header(W, H) + host[b].numpy().tobytes() == want, t
+        with pytest.raises(rt.RTError):
+            sc.wait(10**6)
+    finally:
+        sc.close()
+
+
 def _big_triangles(n=12, seed=3):
     """n large overlapping triangles in front of the camera: each covers most of a 1080p image,
     so their bin lists (~n x 32k tile entries) outgrow the first capacity (65536 entries)."""

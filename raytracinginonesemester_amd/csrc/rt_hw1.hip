@@ -402,11 +402,14 @@ constexpr uint32_t HW1_CHUNK = 64;
 // Exclusive prefix sum of n counts in one workgroup (n is the number of wave tiles, small);
 // offsets[n] = total.  With chunk_first: the same over the tiles' chunk counts, and every
 // chunk's tile in chunk_tile (at most chunk_cap; chunks past it are not written, the total in
-// chunk_first[n] says how many there were).
+// chunk_first[n] says how many there were).  total_out (host memory, may be null): the list
+// total, stored from here for the host's capacity check (a 4-byte copy on the frame's stream
+// after the kernels held every frame for its own latency).
 __global__ __launch_bounds__(1024) void hw1_scan_chunks_kernel(const uint32_t* __restrict__ counts,
                                                                uint32_t* __restrict__ offsets, int n, uint32_t list_cap,
                                                                uint32_t* __restrict__ chunk_first,
-                                                               uint32_t* __restrict__ chunk_tile, uint32_t chunk_cap) {
+                                                               uint32_t* __restrict__ chunk_tile, uint32_t chunk_cap,
+                                                               uint32_t* total_out) {
     __shared__ uint32_t part[1024], cpart[1024];
     const int t = (int)threadIdx.x;
     const int per = (n + 1023) / 1024;
@@ -429,7 +432,10 @@ __global__ __launch_bounds__(1024) void hw1_scan_chunks_kernel(const uint32_t* _
         csum += run + c > list_cap ? 1u : (c + HW1_CHUNK - 1) / HW1_CHUNK;
         run += c;
     }
-    if (t == 1023) offsets[n] = part[1023];
+    if (t == 1023) {
+        offsets[n] = part[1023];
+        if (total_out) __hip_atomic_store(total_out, part[1023], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     cpart[t] = csum;
     __syncthreads();
     for (int st = 1; st < 1024; st <<= 1) {
@@ -650,7 +656,7 @@ extern "C" int rt_hw1_scene_create(int device, const rt_vec3* pos, const rt_vec3
     s->list_cap = uint32_t(std::min<size_t>(std::max<size_t>(4 * P, size_t(1) << 16), 0x7FFFFFFFull));
     if ((rc = s->list.alloc(size_t(s->list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->total_host), rt_hw1_scene::kRing * sizeof(uint32_t),
-                          hipHostMallocDefault));
+                          hipHostMallocCoherent));
     for (int i = 0; i < rt_hw1_scene::kRing; ++i) {
         s->total_host[i] = 0;
         HIP_TRY(hipEventCreate(&s->e0[i]));
@@ -764,7 +770,7 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
         uint32_t* ctile = cfirst + ntiles + 1;
         hipLaunchKernelGGL(hw1_rect_count_kernel, tgrid, dim3(64), 0, st, hp, static_cast<int4*>(s->rects.p), counts);
         hipLaunchKernelGGL(hw1_scan_chunks_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, ntiles, s->list_cap,
-                           cfirst, ctile, s->chunk_cap);
+                           cfirst, ctile, s->chunk_cap, s->total_host + sl);
         hp.bin_count = counts;
         hp.bin_offset = offsets;
         hp.bin_list = static_cast<const uint32_t*>(s->list.p);
@@ -777,8 +783,6 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
         hipLaunchKernelGGL(hw1_resolve_kernel, dim3(rgrid), dim3(BLOCK), 0, st, hp);
         s->last_kernel = "render_hw1_chunks_kernel";
         HIP_TRY(hipGetLastError());
-        // this frame's total, for the capacity of the next ones
-        HIP_TRY(hipMemcpyAsync(s->total_host + sl, offsets + ntiles, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(s->e1[sl], st));

@@ -373,33 +373,11 @@ __device__ __forceinline__ void traverse_frustum(const SceneView& sc, const RayP
 }
 
 // traverse_frustum's DFS over the records (LOOSE: the wave has a loose axis).
-// Split families (round 6; -DRT_NO_SPLIT_FAMILY for the single family, A/B): a wave on a
-// silhouette holds lanes that have hit the surface and lanes that pass beside it.  One family of
-// every live lane then carries tmax = FLT_MAX (the lanes without a hit) over the whole direction
-// cone, so the DFS walks everything behind the surface for the lanes that hit it.  Two families
-// instead: the "open" lanes (no hit yet; bestT = FLT_MAX) with their own directions U0 and tmax
-// FLT_MAX, and the "hit" lanes with the directions U of every live lane (a superset) and tmax_w =
-// the largest bestT among them.  An entry passes when either family's test passes.  Exact for
-// the single family's reason: each live lane is in a family whose directions contain its own and
-// whose tmax is at least its bestT (bestT only decreases; a lane moves from open to hit, never
-// back; U0 is made from the open lanes of some earlier pop, a superset of the open lanes now).
-// U0 is remade when the open lanes have halved since it was made (6 wave reductions).  Waves
-// whose lanes are all open or all hit test one family, as before.
-#ifndef RT_NO_SPLIT_FAMILY
-constexpr bool kSplitFamily = true;
-#else
-constexpr bool kSplitFamily = false;
-#endif
 template <bool PK, bool XL, bool QR, bool LOOSE>
 __device__ __forceinline__ void frustum_loop(const SceneView& sc, const RayPre& r, bool live, HitState& hs,
                                              const float* o, const v2f* U) {
     const float kW = 1.0f / 524288.0f;  // 2^-19
-    // kSplitFamily: the largest bestT of the hit lanes (the hit family's tmax); else of every
-    // live lane (FLT_MAX while one has no hit)
     float tmax_w = FLT_MAX;
-    v2f U0[3] = {U[0], U[1], U[2]};  // the open family's directions
-    bool has_open = true, has_hit = false;
-    int open_n = __popcll(ballot(live));
     uint32_t ref = sc.root_ref;
     uint32_t st_ref = 0, st_hi = 0;  // lane k holds entry k, st_hi entries 64 + k (FRUSTUM_STACK)
     int sp = 0;
@@ -444,19 +422,7 @@ __device__ __forceinline__ void frustum_loop(const SceneView& sc, const RayPre& 
                         hs.bestT = t;
                         hs.slot = (int32_t)slot;
                     }
-                    if constexpr (kSplitFamily) {
-                        const bool hit_l = live && hs.slot >= 0;
-                        tmax_w = wave_reduce_f<true>(hit_l ? hs.bestT : 0.0f);
-                        has_hit = true;
-                        const int n = __popcll(ballot(live && !hit_l));
-                        has_open = n != 0;
-                        if (has_open && 2 * n <= open_n) {
-                            open_n = n;
-                            (void)family_dirs(sc, r, live && !hit_l, o, U0);
-                        }
-                    } else {
-                        tmax_w = wave_reduce_f<true>(live ? hs.bestT : 0.0f);
-                    }
+                    tmax_w = wave_reduce_f<true>(live ? hs.bestT : 0.0f);
                 }
             }
         } else {
@@ -486,32 +452,26 @@ __device__ __forceinline__ void frustum_loop(const SceneView& sc, const RayPre& 
                 bb[2] = B[2];
                 rk = reinterpret_cast<const uint32_t*>(W)[kref];
             }
-            // the family test of this lane's entry for directions Uf and tmax tm
-            auto fam = [&](const v2f* Uf, float tm) -> bool {
-                float nr[3], fr[3];
+            float nr[3], fr[3];
 #pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    const v2f db = bb[a] - (v2f){o[a], o[a]};
-                    const v2f p = (v2f){db.x, db.x} * Uf[a], q = (v2f){db.y, db.y} * Uf[a];
-                    nr[a] = fminf(fminf(p.x, p.y), fminf(q.x, q.y));
-                    fr[a] = fmaxf(fmaxf(p.x, p.y), fmaxf(q.x, q.y));
-                    if constexpr (LOOSE) {  // Uf[a] = (ihp, iln) on a loose axis
-                        if (Uf[a].x > 0.0f && Uf[a].y < 0.0f) {
-                            nr[a] = fmaxf(p.x, q.y);
-                            fr[a] = INFINITY;
-                        }
+            for (int a = 0; a < 3; ++a) {
+                const v2f db = bb[a] - (v2f){o[a], o[a]};
+                const v2f p = (v2f){db.x, db.x} * U[a], q = (v2f){db.y, db.y} * U[a];
+                nr[a] = fminf(fminf(p.x, p.y), fminf(q.x, q.y));
+                fr[a] = fmaxf(fmaxf(p.x, p.y), fmaxf(q.x, q.y));
+                if constexpr (LOOSE) {  // U[a] = (ihp, iln) on a loose axis
+                    if (U[a].x > 0.0f && U[a].y < 0.0f) {
+                        nr[a] = fmaxf(p.x, q.y);
+                        fr[a] = INFINITY;
                     }
                 }
-                float Lc = fmaxf(fmaxf(nr[0], nr[1]), nr[2]);
-                float Hc = fminf(fminf(fr[0], fr[1]), fr[2]);
-                Lc = __builtin_fmaf(fabsf(Lc), -kW, Lc);
-                Hc = __builtin_fmaf(fabsf(Hc), kW, Hc);
-                return fmaxf(Lc, kRayTMin) <= fminf(Hc, tm);
-            };
-            bool pass;
-            if (!kSplitFamily || !(has_open && has_hit)) pass = fam(kSplitFamily && has_hit ? U : U0, tmax_w);
-            else pass = fam(U0, FLT_MAX) || fam(U, tmax_w);
-            const uint32_t m = (uint32_t)ballot(rk != NO_REF && pass) & ent_mask;
+            }
+            float Lc = fmaxf(fmaxf(nr[0], nr[1]), nr[2]);
+            float Hc = fminf(fminf(fr[0], fr[1]), fr[2]);
+            Lc = __builtin_fmaf(fabsf(Lc), -kW, Lc);
+            Hc = __builtin_fmaf(fabsf(Hc), kW, Hc);
+            const uint32_t m =
+                (uint32_t)ballot(rk != NO_REF && fmaxf(Lc, kRayTMin) <= fminf(Hc, tmax_w)) & ent_mask;
             if (m != 0) {
                 RT_STAT(4, 1);
                 // push the passing entries in record order, hold the last (the reference pops it next)

@@ -723,8 +723,11 @@ def hw1_main(a):
     # rt_render_hw1_deliver: each frame's P6 body copied to pinned host memory on the scene's copy
     # stream while the next frame renders (the copy on the render stream serialised with the
     # frames: 0.129 ms per step against 0.096 of kernels); 3 host frames, every
-    # frame waited for before its buffer is reused and at the end
-    depth = 3
+    # frame waited for before its buffer is reused and at the end.  6 host frames: the host waits
+    # for the copy of the frame 5 back, long done, so its wake-up is off the GPU's path (with 3,
+    # the next frame's kernels were submitted only after the host woke from frame k-2's copy:
+    # ~16 us idle between frames, profiles/r06/exp/c2_deliver_trace_summary.json)
+    depth = 6
     host = [torch.empty(W * H * 3, dtype=torch.uint8, pin_memory=True) for _ in range(depth)]
     nxt = {"k": 0}
 

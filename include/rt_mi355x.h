@@ -425,11 +425,11 @@ void rt_hw1_scene_destroy(rt_hw1_scene* s);
 int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_vec3 light_position, rt_vec3 light_color,
                          int spp, const float* jitter, int flags, float* rgb_dev, uint8_t* p6_dev,
                          int32_t* hit_idx_dev, float* hit_t_dev, void* hip_stream);
-/* rt_render_hw1_device into one of the scene's 3 device P6 bodies, then that body copied to
+/* rt_render_hw1_device into one of the scene's 4 device P6 bodies, then that body copied to
  * host_p6 (W*H*3 bytes; pinned memory for an asynchronous copy) on the scene's own copy stream
  * once the frame's kernels are done, so the copy overlaps the next frames' kernels; *ticket
  * numbers the frame.  host_p6 must stay valid until rt_hw1_wait(ticket) returns; a frame reuses
- * the device body of the frame 3 before it (its stream waits for that copy). */
+ * the device body of the frame 4 before it (its stream waits for that copy if still running). */
 int rt_render_hw1_deliver(rt_hw1_scene* s, const rt_camera* cam, rt_vec3 light_position, rt_vec3 light_color,
                           int spp, int flags, uint8_t* host_p6, void* hip_stream, uint64_t* ticket);
 int rt_hw1_wait(rt_hw1_scene* s, uint64_t ticket);

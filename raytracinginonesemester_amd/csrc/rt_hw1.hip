@@ -6,6 +6,7 @@
 // pipelined host delivery (rt_render_hw1_deliver / rt_hw1_wait).  Split out of rt_device.hip in
 // round 6; it shares only the wave primitives (rt_wave.hpp) with it.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cstdint>
@@ -598,22 +599,30 @@ struct rt_hw1_scene {
     std::vector<float> jitter_host;
     static constexpr int kRing = 64;
     hipEvent_t e0[kRing] = {}, e1[kRing] = {};
+    hipEvent_t f1[kRing] = {};  // the frame's end, no timestamp (ordering and completion queries)
+    // e0 / e1 (the kernels' start and end timestamps) are recorded for every direct frame but for
+    // one delivered frame in RT_TUNE_KERNEL_TIMING_EVERY: a timing event between two kernels holds
+    // the next one's dispatch until the previous has completed and the timestamp is written
+    // (DESIGN.md §4.13); f1 marks every frame's end without a timestamp
+    bool timed[kRing] = {};
+    bool in_deliver = false;  // rt_render_hw1_deliver is calling rt_render_hw1_device
     uint32_t* total_host = nullptr;  // pinned: the list total of frame f at [f % kRing]
     uint64_t frames = 0;
     hipStream_t last_stream = nullptr;
     const char* last_kernel = "";
     // rt_render_hw1_deliver: frames rendered into a ring of kDeliver device P6 bodies, each body
     // copied to the caller's host buffer on the copy stream while the next frames render
-    static constexpr int kDeliver = 3;
+    static constexpr int kDeliver = 4;
     DevBuf dp6[kDeliver];
     hipStream_t copy = nullptr;
     hipEvent_t rdone[kRing] = {}, cdone[kRing] = {};  // per ticket: rendered, copied
     uint64_t tickets = 0;
     ~rt_hw1_scene() {
         for (int i = 0; i < kRing; ++i) {
-            if (e0[i]) (void)hipEventSynchronize(e1[i]);
+            if (f1[i]) (void)hipEventSynchronize(f1[i]);
             if (e0[i]) (void)hipEventDestroy(e0[i]);
             if (e1[i]) (void)hipEventDestroy(e1[i]);
+            if (f1[i]) (void)hipEventDestroy(f1[i]);
             if (cdone[i]) (void)hipEventSynchronize(cdone[i]);
             if (rdone[i]) (void)hipEventDestroy(rdone[i]);
             if (cdone[i]) (void)hipEventDestroy(cdone[i]);
@@ -661,6 +670,7 @@ extern "C" int rt_hw1_scene_create(int device, const rt_vec3* pos, const rt_vec3
         s->total_host[i] = 0;
         HIP_TRY(hipEventCreate(&s->e0[i]));
         HIP_TRY(hipEventCreate(&s->e1[i]));
+        HIP_TRY(hipEventCreateWithFlags(&s->f1[i], hipEventDisableTiming));
     }
     *out = s.release();
     return RT_OK;
@@ -687,7 +697,7 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
     if (jitter) std::memcpy(tab.data(), jitter, tab.size() * sizeof(float));
     else if ((rc = rt_jittered_samples(spp, 42u, 0, tab.data())) != RT_OK) return rc;
     if (s->jitter_spp != spp || s->jitter_host != tab) {
-        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->e1[(s->frames - 1) % rt_hw1_scene::kRing]));
+        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->f1[(s->frames - 1) % rt_hw1_scene::kRing]));
         if ((rc = s->jitter.upload(tab.data(), tab.size() * sizeof(float))) != RT_OK) return rc;
         s->jitter_spp = spp;
         s->jitter_host = tab;
@@ -697,10 +707,10 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
     // the latest finished frame's list total (frames are scanned back to front, non-blocking)
     for (uint64_t b = 1; b <= std::min<uint64_t>(s->frames, 4); ++b) {
         const int sl = int((s->frames - b) % rt_hw1_scene::kRing);
-        if (hipEventQuery(s->e1[sl]) != hipSuccess) continue;
+        if (hipEventQuery(s->f1[sl]) != hipSuccess) continue;
         const uint32_t tot = s->total_host[sl];
         if (tot > s->list_cap) {  // grow (the old list may still be read by frames in flight)
-            HIP_TRY(hipEventSynchronize(s->e1[(s->frames - 1) % rt_hw1_scene::kRing]));
+            HIP_TRY(hipEventSynchronize(s->f1[(s->frames - 1) % rt_hw1_scene::kRing]));
             s->list_cap = uint32_t(std::min<uint64_t>(uint64_t(tot) + tot / 4 + 1024, 0x7FFFFFFFull));
             if ((rc = s->list.alloc(size_t(s->list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
             s->bins_tiles = -1;  // the chunk table follows the list's capacity
@@ -710,7 +720,7 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
     (void)hipGetLastError();  // a not-ready query is not an error of this call
     const size_t nsamples = size_t(W) * size_t(H) * size_t(spp);
     if (!brute && (s->bins_tiles != ntiles || s->keys_n != nsamples)) {
-        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->e1[(s->frames - 1) % rt_hw1_scene::kRing]));
+        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->f1[(s->frames - 1) % rt_hw1_scene::kRing]));
         // counts | cursor | offsets (ntiles + 1): counts and cursor zeroed here, then by every
         // frame's resolve pass for the next
         if ((rc = s->bins.alloc(size_t(3 * ntiles + 1) * sizeof(uint32_t))) != RT_OK) return rc;
@@ -752,12 +762,16 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
     const int sl = int(s->frames % rt_hw1_scene::kRing);
     // the scene's buffers are shared by its frames: a frame on another stream waits for the last
     if (s->frames > 0 && st != s->last_stream)
-        HIP_TRY(hipStreamWaitEvent(st, s->e1[(s->frames - 1) % rt_hw1_scene::kRing], 0));
+        HIP_TRY(hipStreamWaitEvent(st, s->f1[(s->frames - 1) % rt_hw1_scene::kRing], 0));
     s->last_stream = st;
-    HIP_TRY(hipEventRecord(s->e0[sl], st));
+    const uint64_t every = uint64_t(std::clamp(rt::tuning(RT_TUNE_KERNEL_TIMING_EVERY, 4.0), 1.0, 256.0));
+    s->timed[sl] = !s->in_deliver || s->frames % every == 0;
+    // the timestamps are taken by the first and last dispatches themselves (hipExtLaunchKernel
+    // start / stop events), not by event packets between them
+    hipEvent_t t0 = s->timed[sl] ? s->e0[sl] : nullptr, t1 = s->timed[sl] ? s->e1[sl] : nullptr;
     const int blocks = ((W + 15) / 16) * ((H + 15) / 16);
     if (brute) {
-        hipLaunchKernelGGL(render_hw1_kernel, dim3(blocks), dim3(BLOCK), 0, st, hp);
+        hipExtLaunchKernelGGL(render_hw1_kernel, dim3(blocks), dim3(BLOCK), 0, st, t0, t1, 0, hp);
         s->last_kernel = "render_hw1_kernel";
     } else {
         // one wave per 64 triangles (a block each): the per-triangle passes spread over every CU
@@ -768,7 +782,8 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
         uint32_t* offsets = cursor + ntiles;  // ntiles + 1 entries
         uint32_t* cfirst = static_cast<uint32_t*>(s->chunks.p);
         uint32_t* ctile = cfirst + ntiles + 1;
-        hipLaunchKernelGGL(hw1_rect_count_kernel, tgrid, dim3(64), 0, st, hp, static_cast<int4*>(s->rects.p), counts);
+        hipExtLaunchKernelGGL(hw1_rect_count_kernel, tgrid, dim3(64), 0, st, t0, nullptr, 0, hp,
+                              static_cast<int4*>(s->rects.p), counts);
         hipLaunchKernelGGL(hw1_scan_chunks_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, ntiles, s->list_cap,
                            cfirst, ctile, s->chunk_cap, s->total_host + sl);
         hp.bin_count = counts;
@@ -780,12 +795,12 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
         // chunks grid-stride over a grid of every CU's worth of waves (the count is on the device)
         hipLaunchKernelGGL(render_hw1_chunks_kernel, dim3(1024), dim3(BLOCK), 0, st, hp);
         const int rgrid = (std::max(W * H, 2 * ntiles) + BLOCK - 1) / BLOCK;
-        hipLaunchKernelGGL(hw1_resolve_kernel, dim3(rgrid), dim3(BLOCK), 0, st, hp);
+        hipExtLaunchKernelGGL(hw1_resolve_kernel, dim3(rgrid), dim3(BLOCK), 0, st, nullptr, t1, 0, hp);
         s->last_kernel = "render_hw1_chunks_kernel";
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(s->e1[sl], st));
+    HIP_TRY(hipEventRecord(s->f1[sl], st));
     s->frames++;
     return RT_OK;
 }
@@ -820,10 +835,18 @@ extern "C" int rt_render_hw1_deliver(rt_hw1_scene* s, const rt_camera* cam, rt_v
         int rc = s->dp6[slot].alloc(bytes);
         if (rc != RT_OK) return rc;
     } else if (k >= uint64_t(rt_hw1_scene::kDeliver)) {
-        HIP_TRY(hipStreamWaitEvent(st, s->cdone[(k - rt_hw1_scene::kDeliver) % rt_hw1_scene::kRing], 0));
+        // the slot's previous copy: a wait on the render stream only while it is still running
+        // (a cross-stream wait holds the next frame's first kernel even when already satisfied)
+        hipEvent_t prev = s->cdone[(k - rt_hw1_scene::kDeliver) % rt_hw1_scene::kRing];
+        if (hipEventQuery(prev) != hipSuccess) {
+            (void)hipGetLastError();  // not ready is not an error of this call
+            HIP_TRY(hipStreamWaitEvent(st, prev, 0));
+        }
     }
+    s->in_deliver = true;
     int rc = rt_render_hw1_device(s, cam, lpos, lcol, spp, nullptr, flags, nullptr,
                                   static_cast<uint8_t*>(s->dp6[slot].p), nullptr, nullptr, stream);
+    s->in_deliver = false;
     if (rc != RT_OK) return rc;
     HIP_TRY(hipEventRecord(s->rdone[ring], st));
     HIP_TRY(hipStreamWaitEvent(s->copy, s->rdone[ring], 0));
@@ -848,9 +871,16 @@ extern "C" int rt_hw1_wait(rt_hw1_scene* s, uint64_t ticket) {
 extern "C" int rt_hw1_kernel_times(const rt_hw1_scene* s, float* ms_out, int max, int* n_out) {
     if (!s || !ms_out || !n_out || max < 0) return set_error(RT_ERR_ARG, "rt_hw1_kernel_times: bad argument");
     DeviceGuard g(s->device);
-    const int n = int(std::min<uint64_t>({uint64_t(max), s->frames, uint64_t(rt_hw1_scene::kRing)}));
+    // the latest timed frames (all direct frames; delivered ones are sampled), oldest first
+    std::vector<int> slots;
+    const uint64_t have = std::min<uint64_t>(s->frames, uint64_t(rt_hw1_scene::kRing));
+    for (uint64_t b = 1; b <= have && int(slots.size()) < max; ++b) {
+        const int sl = int((s->frames - b) % rt_hw1_scene::kRing);
+        if (s->timed[sl]) slots.push_back(sl);
+    }
+    const int n = int(slots.size());
     for (int i = 0; i < n; ++i) {
-        const int sl = int((s->frames - uint64_t(n - i)) % rt_hw1_scene::kRing);
+        const int sl = slots[size_t(n - 1 - i)];
         HIP_TRY(hipEventSynchronize(s->e1[sl]));
         HIP_TRY(hipEventElapsedTime(&ms_out[i], s->e0[sl], s->e1[sl]));
     }
@@ -867,7 +897,7 @@ extern "C" int rt_hw1_list_info(const rt_hw1_scene* s, int64_t info[2]) {
     info[1] = 0;
     if (s->frames > 0) {
         const int sl = int((s->frames - 1) % rt_hw1_scene::kRing);
-        HIP_TRY(hipEventSynchronize(s->e1[sl]));
+        HIP_TRY(hipEventSynchronize(s->f1[sl]));
         info[1] = s->total_host[sl];
     }
     return RT_OK;

@@ -597,9 +597,13 @@ struct rt_hw1_scene {
     uint32_t list_cap = 0, chunk_cap = 0;
     int jitter_spp = -1;
     std::vector<float> jitter_host;
+    bool jitter_default = false;  // jitter_host is jittered_samples(jitter_spp, 42)
     static constexpr int kRing = 64;
     hipEvent_t e0[kRing] = {}, e1[kRing] = {};
-    hipEvent_t f1[kRing] = {};  // the frame's end, no timestamp (ordering and completion queries)
+    hipEvent_t f1[kRing] = {};  // the frame's end, no timestamp
+    // the frame's end event: e1 on timed frames, f1 otherwise; set by the frame's last dispatch
+    // itself (its stop event), so no marker packet sits between two frames' kernels
+    hipEvent_t end_of(int sl) const { return timed[sl] ? e1[sl] : f1[sl]; }
     // e0 / e1 (the kernels' start and end timestamps) are recorded for every direct frame but for
     // one delivered frame in RT_TUNE_KERNEL_TIMING_EVERY: a timing event between two kernels holds
     // the next one's dispatch until the previous has completed and the timestamp is written
@@ -615,16 +619,15 @@ struct rt_hw1_scene {
     static constexpr int kDeliver = 4;
     DevBuf dp6[kDeliver];
     hipStream_t copy = nullptr;
-    hipEvent_t rdone[kRing] = {}, cdone[kRing] = {};  // per ticket: rendered, copied
+    hipEvent_t cdone[kRing] = {};  // per ticket: copied
     uint64_t tickets = 0;
     ~rt_hw1_scene() {
         for (int i = 0; i < kRing; ++i) {
-            if (f1[i]) (void)hipEventSynchronize(f1[i]);
+            if (f1[i]) (void)hipEventSynchronize(end_of(i));
             if (e0[i]) (void)hipEventDestroy(e0[i]);
             if (e1[i]) (void)hipEventDestroy(e1[i]);
             if (f1[i]) (void)hipEventDestroy(f1[i]);
             if (cdone[i]) (void)hipEventSynchronize(cdone[i]);
-            if (rdone[i]) (void)hipEventDestroy(rdone[i]);
             if (cdone[i]) (void)hipEventDestroy(cdone[i]);
         }
         if (copy) (void)hipStreamDestroy(copy);
@@ -693,24 +696,30 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
     hipStream_t st = static_cast<hipStream_t>(stream);
     int rc;
     // jitter_samples(spp, 42u) offsets in [0,1) (HW1/include/antialias.h:12-27), or the caller's
-    std::vector<float> tab(2 * size_t(spp));
-    if (jitter) std::memcpy(tab.data(), jitter, tab.size() * sizeof(float));
-    else if ((rc = rt_jittered_samples(spp, 42u, 0, tab.data())) != RT_OK) return rc;
-    if (s->jitter_spp != spp || s->jitter_host != tab) {
-        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->f1[(s->frames - 1) % rt_hw1_scene::kRing]));
+    // (the default table of the scene's current spp is already uploaded: nothing to make)
+    const bool have_default = !jitter && s->jitter_default && s->jitter_spp == spp;
+    std::vector<float> tab;
+    if (!have_default) {
+        tab.resize(2 * size_t(spp));
+        if (jitter) std::memcpy(tab.data(), jitter, tab.size() * sizeof(float));
+        else if ((rc = rt_jittered_samples(spp, 42u, 0, tab.data())) != RT_OK) return rc;
+    }
+    if (!have_default && (s->jitter_spp != spp || s->jitter_host != tab)) {
+        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->end_of(int((s->frames - 1) % rt_hw1_scene::kRing))));
         if ((rc = s->jitter.upload(tab.data(), tab.size() * sizeof(float))) != RT_OK) return rc;
         s->jitter_spp = spp;
         s->jitter_host = tab;
     }
+    if (!have_default) s->jitter_default = jitter == nullptr;
     const bool brute = (flags & RT_HW1_BRUTE) != 0;
     const int ntiles = ((W + HW1_TW - 1) / HW1_TW) * ((H + HW1_TH - 1) / HW1_TH);
     // the latest finished frame's list total (frames are scanned back to front, non-blocking)
     for (uint64_t b = 1; b <= std::min<uint64_t>(s->frames, 4); ++b) {
         const int sl = int((s->frames - b) % rt_hw1_scene::kRing);
-        if (hipEventQuery(s->f1[sl]) != hipSuccess) continue;
+        if (hipEventQuery(s->end_of(sl)) != hipSuccess) continue;
         const uint32_t tot = s->total_host[sl];
         if (tot > s->list_cap) {  // grow (the old list may still be read by frames in flight)
-            HIP_TRY(hipEventSynchronize(s->f1[(s->frames - 1) % rt_hw1_scene::kRing]));
+            HIP_TRY(hipEventSynchronize(s->end_of(int((s->frames - 1) % rt_hw1_scene::kRing))));
             s->list_cap = uint32_t(std::min<uint64_t>(uint64_t(tot) + tot / 4 + 1024, 0x7FFFFFFFull));
             if ((rc = s->list.alloc(size_t(s->list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
             s->bins_tiles = -1;  // the chunk table follows the list's capacity
@@ -720,7 +729,7 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
     (void)hipGetLastError();  // a not-ready query is not an error of this call
     const size_t nsamples = size_t(W) * size_t(H) * size_t(spp);
     if (!brute && (s->bins_tiles != ntiles || s->keys_n != nsamples)) {
-        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->f1[(s->frames - 1) % rt_hw1_scene::kRing]));
+        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->end_of(int((s->frames - 1) % rt_hw1_scene::kRing))));
         // counts | cursor | offsets (ntiles + 1): counts and cursor zeroed here, then by every
         // frame's resolve pass for the next
         if ((rc = s->bins.alloc(size_t(3 * ntiles + 1) * sizeof(uint32_t))) != RT_OK) return rc;
@@ -762,13 +771,13 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
     const int sl = int(s->frames % rt_hw1_scene::kRing);
     // the scene's buffers are shared by its frames: a frame on another stream waits for the last
     if (s->frames > 0 && st != s->last_stream)
-        HIP_TRY(hipStreamWaitEvent(st, s->f1[(s->frames - 1) % rt_hw1_scene::kRing], 0));
+        HIP_TRY(hipStreamWaitEvent(st, s->end_of(int((s->frames - 1) % rt_hw1_scene::kRing)), 0));
     s->last_stream = st;
     const uint64_t every = uint64_t(std::clamp(rt::tuning(RT_TUNE_KERNEL_TIMING_EVERY, 4.0), 1.0, 256.0));
     s->timed[sl] = !s->in_deliver || s->frames % every == 0;
     // the timestamps are taken by the first and last dispatches themselves (hipExtLaunchKernel
     // start / stop events), not by event packets between them
-    hipEvent_t t0 = s->timed[sl] ? s->e0[sl] : nullptr, t1 = s->timed[sl] ? s->e1[sl] : nullptr;
+    hipEvent_t t0 = s->timed[sl] ? s->e0[sl] : nullptr, t1 = s->end_of(sl);
     const int blocks = ((W + 15) / 16) * ((H + 15) / 16);
     if (brute) {
         hipExtLaunchKernelGGL(render_hw1_kernel, dim3(blocks), dim3(BLOCK), 0, st, t0, t1, 0, hp);
@@ -800,7 +809,6 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(s->f1[sl], st));
     s->frames++;
     return RT_OK;
 }
@@ -820,7 +828,6 @@ extern "C" int rt_render_hw1_deliver(rt_hw1_scene* s, const rt_camera* cam, rt_v
     if (!s->copy) {
         HIP_TRY(hipStreamCreateWithFlags(&s->copy, hipStreamNonBlocking));
         for (int i = 0; i < rt_hw1_scene::kRing; ++i) {
-            HIP_TRY(hipEventCreateWithFlags(&s->rdone[i], hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&s->cdone[i], hipEventDisableTiming));
         }
     }
@@ -848,8 +855,9 @@ extern "C" int rt_render_hw1_deliver(rt_hw1_scene* s, const rt_camera* cam, rt_v
                                   static_cast<uint8_t*>(s->dp6[slot].p), nullptr, nullptr, stream);
     s->in_deliver = false;
     if (rc != RT_OK) return rc;
-    HIP_TRY(hipEventRecord(s->rdone[ring], st));
-    HIP_TRY(hipStreamWaitEvent(s->copy, s->rdone[ring], 0));
+    // the copy waits for the frame's end event, set by its last kernel's dispatch (a marker
+    // packet here held the next frame's first kernel: ~16 us between frames)
+    HIP_TRY(hipStreamWaitEvent(s->copy, s->end_of(int((s->frames - 1) % rt_hw1_scene::kRing)), 0));
     HIP_TRY(hipMemcpyAsync(host_p6, s->dp6[slot].p, bytes, hipMemcpyDeviceToHost, s->copy));
     HIP_TRY(hipEventRecord(s->cdone[ring], s->copy));
     *ticket = k;
@@ -897,7 +905,7 @@ extern "C" int rt_hw1_list_info(const rt_hw1_scene* s, int64_t info[2]) {
     info[1] = 0;
     if (s->frames > 0) {
         const int sl = int((s->frames - 1) % rt_hw1_scene::kRing);
-        HIP_TRY(hipEventSynchronize(s->f1[sl]));
+        HIP_TRY(hipEventSynchronize(s->end_of(sl)));
         info[1] = s->total_host[sl];
     }
     return RT_OK;

@@ -425,11 +425,14 @@ void rt_hw1_scene_destroy(rt_hw1_scene* s);
 int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_vec3 light_position, rt_vec3 light_color,
                          int spp, const float* jitter, int flags, float* rgb_dev, uint8_t* p6_dev,
                          int32_t* hit_idx_dev, float* hit_t_dev, void* hip_stream);
-/* rt_render_hw1_device into one of the scene's 4 device P6 bodies, then that body copied to
- * host_p6 (W*H*3 bytes; pinned memory for an asynchronous copy) on the scene's own copy stream
- * once the frame's kernels are done, so the copy overlaps the next frames' kernels; *ticket
- * numbers the frame.  host_p6 must stay valid until rt_hw1_wait(ticket) returns; a frame reuses
- * the device body of the frame 4 before it (its stream waits for that copy if still running). */
+/* One frame as rt_render_hw1_device renders it, into one of the scene's 8 device P6 bodies, then
+ * that body copied to host_p6 (W*H*3 bytes, pinned) once the frame's kernels are done — by a DMA
+ * (SDMA) engine, queued from a copier thread, or with RT_TUNE_COPY_ENGINE 0 by the HIP runtime
+ * on the scene's copy stream — so the copy overlaps the next frames' kernels; *ticket numbers the
+ * frame.  Frames alternate over the scene's lanes (binning buffers and a stream each,
+ * RT_TUNE_HW1_LANES), after the work queued on hip_stream so far.  host_p6 must stay valid until
+ * rt_hw1_wait(ticket) returns; a frame reuses the device body of the frame 8 before it (after
+ * that frame's copy). */
 int rt_render_hw1_deliver(rt_hw1_scene* s, const rt_camera* cam, rt_vec3 light_position, rt_vec3 light_color,
                           int spp, int flags, uint8_t* host_p6, void* hip_stream, uint64_t* ticket);
 int rt_hw1_wait(rt_hw1_scene* s, uint64_t ticket);
@@ -558,7 +561,11 @@ typedef enum {
     RT_TUNE_CUT_SUB = 20,        /* sub-boxes per box of the tile-culling cut, tested for the tiles whose rays
                                     may reach that box (16; a power of two <= 64; < 2: one level);
                                     at scene creation */
-    RT_TUNE_COUNT = 21
+    RT_TUNE_HW1_LANES = 21,      /* rt_render_hw1_deliver: frames alternate over this many lanes (binning
+                                    buffers + a stream each, 1..8; default 2): a lane
+                                    overlaps the others only on a hardware queue of its own (HIP:
+                                    GPU_MAX_HW_QUEUES per process, 4 by default) */
+    RT_TUNE_COUNT = 22
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */
 int rt_tuning_set(int id, double value);

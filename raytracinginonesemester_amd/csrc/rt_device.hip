@@ -718,6 +718,7 @@ struct rt_scene {
         for (hipStream_t& r : rstream) HIP_TRY(hipStreamCreateWithFlags(&r, hipStreamNonBlocking));
         if (int rc = fault.alloc(sizeof(uint32_t)); rc != RT_OK) return rc;
         HIP_TRY(hipMemset(fault.p, 0, sizeof(uint32_t)));
+        HIP_TRY(hipDeviceSynchronize());  // (the frames run on non-blocking streams)
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&drain), sizeof(uint32_t), hipHostMallocCoherent));
         *drain = 0;
         for (int i = 0; i < kRing; ++i) {
@@ -1199,7 +1200,10 @@ extern "C" int rt_scene_faults(rt_scene* s, uint32_t* flags, int clear) {
     DeviceGuard g(s->device);
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(flags, s->fault.p, sizeof(uint32_t), hipMemcpyDeviceToHost));
-    if (clear) HIP_TRY(hipMemset(s->fault.p, 0, sizeof(uint32_t)));
+    if (clear) {
+        HIP_TRY(hipMemset(s->fault.p, 0, sizeof(uint32_t)));
+        HIP_TRY(hipDeviceSynchronize());  // before any later frame on a non-blocking stream
+    }
     return RT_OK;
 }
 extern "C" size_t rt_scene_device_bytes(const rt_scene* s) { return s ? s->bytes : 0; }
@@ -2044,6 +2048,7 @@ extern "C" int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts
     // (rt_scene_faults still sees what this frame raised)
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemset(s->fault.p, 0, sizeof(uint32_t)));
+    HIP_TRY(hipDeviceSynchronize());  // (the frame runs on the scene's non-blocking streams)
     rc = rt_render_device(s, cam, o, static_cast<float*>(rgb.p), static_cast<int32_t*>(hi.p),
                           static_cast<float*>(ht.p), nullptr);
     if (rc != RT_OK) return rc;
@@ -2086,6 +2091,7 @@ extern "C" int rt_count_rays_ex(rt_scene* s, const rt_camera* cam, const rt_rend
     if ((rc = cnt.alloc(4 * sizeof(unsigned long long))) != RT_OK) return rc;
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemset(cnt.p, 0, 4 * sizeof(unsigned long long)));
+    HIP_TRY(hipDeviceSynchronize());
     rt_render_opts lo = *o;
     lo.kernel = RT_KERNEL_LANE;  // deep trees take the DEEP kernels, which count too
     t_ray_count = static_cast<unsigned long long*>(cnt.p);

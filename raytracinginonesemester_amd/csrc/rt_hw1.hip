@@ -18,6 +18,7 @@
 #include "rt_hip_host.hpp"
 #include "rt_math.hpp"
 #include "rt_ppm.hpp"
+#include "rt_dma.hpp"
 
 using namespace rtd;
 
@@ -582,19 +583,33 @@ extern "C" int rt_render_hw1(int device, const rt_vec3* pos, const rt_vec3* nrm,
 
 // ---- HW1 resident scene (the C2 configuration's device path) ---------------------------
 // The mesh packed once (v0, e1, e2 as ray_intersection computes them, the three normals per
-// triangle), the binning buffers kept across frames.  A frame is four launches on the caller's
-// stream (counts zeroed, rect + count, scan, fill, render) and no host synchronisation: the
-// bin list's capacity is checked on the device (a tile whose list would not fit takes the
-// brute-force loop), and the host grows it from the latest finished frame's total.
+// triangle), the binning buffers kept across frames.  A frame is five launches (rect + count,
+// scan, fill, render, resolve) and no host synchronisation: the bin list's capacity is checked
+// on the device (a tile whose list would not fit takes the brute-force loop), and the host grows
+// it from the latest finished frame's total.
 struct rt_hw1_scene {
     int device = 0;
     size_t P = 0;
-    DevBuf tri, nrm, rects, bins, list, jitter;
-    DevBuf chunks;             // chunk_first (ntiles + 1) | chunk_tile (chunk_cap)
-    DevBuf keys;               // per (pixel, sample): the chunked pass's winners, kept at ~0 between frames
-    int bins_tiles = -1;       // tiles the bins buffer is laid out for
-    size_t keys_n = 0;         // samples the keys buffer holds
-    uint32_t list_cap = 0, chunk_cap = 0;
+    DevBuf tri, nrm, jitter;
+    // A lane: one frame's binning state.  Direct frames (rt_render_hw1_device) use lane 0 on the
+    // caller's stream; delivered frames alternate over the kLanes lanes, each on a stream of its
+    // own, so one frame's latency-bound passes (rect + count, the one-workgroup scan and fill:
+    // ~60 of the frame's ~97 us with a fraction of the CUs busy) run beside the other frame's
+    // render kernel.  Every frame still runs all five passes over its own buffers.
+    struct Lane {
+        DevBuf rects, bins, list;
+        DevBuf chunks;             // chunk_first (ntiles + 1) | chunk_tile (chunk_cap)
+        DevBuf keys;               // per (pixel, sample): the chunked pass's winners, kept at ~0 between frames
+        int bins_tiles = -1;       // tiles the bins buffer is laid out for
+        size_t keys_n = 0;         // samples the keys buffer holds
+        uint32_t list_cap = 0, chunk_cap = 0;
+        hipStream_t own = nullptr;          // delivered frames' stream (made on first use)
+        hipStream_t last_stream = nullptr;  // the stream of the lane's latest frame
+        uint64_t last_frame = 0;
+        bool used = false;
+    };
+    static constexpr int kLanes = 8;
+    Lane lane[kLanes];
     int jitter_spp = -1;
     std::vector<float> jitter_host;
     bool jitter_default = false;  // jitter_host is jittered_samples(jitter_spp, 42)
@@ -604,32 +619,75 @@ struct rt_hw1_scene {
     // the frame's end event: e1 on timed frames, f1 otherwise; set by the frame's last dispatch
     // itself (its stop event), so no marker packet sits between two frames' kernels
     hipEvent_t end_of(int sl) const { return timed[sl] ? e1[sl] : f1[sl]; }
+    hipEvent_t frame_end(uint64_t f) const { return end_of(int(f % kRing)); }
     // e0 / e1 (the kernels' start and end timestamps) are recorded for every direct frame but for
     // one delivered frame in RT_TUNE_KERNEL_TIMING_EVERY: a timing event between two kernels holds
     // the next one's dispatch until the previous has completed and the timestamp is written
     // (DESIGN.md §4.13); f1 marks every frame's end without a timestamp
     bool timed[kRing] = {};
-    bool in_deliver = false;  // rt_render_hw1_deliver is calling rt_render_hw1_device
+    int lane_of[kRing] = {};  // the lane of frame f at [f % kRing]
+    bool in_deliver = false;  // rt_render_hw1_deliver is calling render_frame
     uint32_t* total_host = nullptr;  // pinned: the list total of frame f at [f % kRing]
     uint64_t frames = 0;
-    hipStream_t last_stream = nullptr;
     const char* last_kernel = "";
     // rt_render_hw1_deliver: frames rendered into a ring of kDeliver device P6 bodies, each body
     // copied to the caller's host buffer on the copy stream while the next frames render
-    static constexpr int kDeliver = 4;
+    static constexpr int kDeliver = 8;
     DevBuf dp6[kDeliver];
+    // the copies: SDMA (copy_mode 1: a copier thread queues each body on a DMA engine once its
+    // frame's end event has fired; dma_done[ticket % kRing] drops to 0 when it has landed), or
+    // the HIP runtime's on the copy stream (copy_mode 0: blit kernels on the CUs beside the next
+    // frame's; cdone[ticket % kRing] fires when it has landed); -1 until the first delivery
+    int copy_mode = -1;
+    std::unique_ptr<rt_dma::DmaCopier> dma;
+    hsa_signal_t dma_done[kRing] = {};
+    bool dma_pending[kRing] = {};
     hipStream_t copy = nullptr;
     hipEvent_t cdone[kRing] = {};  // per ticket: copied
+    hipEvent_t caller = nullptr;   // the caller's stream's pending work, for a lane to wait on
     uint64_t tickets = 0;
+    // ticket t's body is in host memory
+    int wait_copy(uint64_t t) {
+        const int r = int(t % kRing);
+        if (copy_mode == 1) {
+            if (dma_pending[r]) {
+                (void)rt_dma::hsa().signal_wait(dma_done[r], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+                dma_pending[r] = false;
+            }
+            std::string msg;
+            const int rc = dma->error(&msg);
+            return rc == RT_OK ? RT_OK : set_error(rc, msg);
+        }
+        if (copy_mode == 0) HIP_TRY(hipEventSynchronize(cdone[r]));
+        return RT_OK;
+    }
+    // every frame of lane L is done (a lane's frames are ordered: one stream, or a wait)
+    hipError_t sync_lane(const Lane& L) const { return L.used ? hipEventSynchronize(frame_end(L.last_frame)) : hipSuccess; }
+    hipError_t sync_all() const {
+        for (const Lane& L : lane) {
+            const hipError_t e = sync_lane(L);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
     ~rt_hw1_scene() {
+        (void)sync_all();
+        for (int i = 0; i < kRing; ++i)  // SDMA copies still reading the bodies
+            if (dma_pending[i])
+                (void)rt_dma::hsa().signal_wait(dma_done[i], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+        dma.reset();  // (the copier thread queries the frames' events)
+        for (int i = 0; i < kRing; ++i)
+            if (dma_done[i].handle) (void)rt_dma::hsa().signal_destroy(dma_done[i]);
         for (int i = 0; i < kRing; ++i) {
-            if (f1[i]) (void)hipEventSynchronize(end_of(i));
             if (e0[i]) (void)hipEventDestroy(e0[i]);
             if (e1[i]) (void)hipEventDestroy(e1[i]);
             if (f1[i]) (void)hipEventDestroy(f1[i]);
             if (cdone[i]) (void)hipEventSynchronize(cdone[i]);
             if (cdone[i]) (void)hipEventDestroy(cdone[i]);
         }
+        if (caller) (void)hipEventDestroy(caller);
+        for (Lane& L : lane)
+            if (L.own) (void)hipStreamDestroy(L.own);
         if (copy) (void)hipStreamDestroy(copy);
         if (total_host) (void)hipHostFree(total_host);
     }
@@ -663,10 +721,12 @@ extern "C" int rt_hw1_scene_create(int device, const rt_vec3* pos, const rt_vec3
     s->P = P;
     if ((rc = s->tri.upload(ht.data(), ht.size() * sizeof(float4))) != RT_OK) return rc;
     if ((rc = s->nrm.upload(hn.data(), hn.size() * sizeof(float4))) != RT_OK) return rc;
-    if ((rc = s->rects.alloc(P * sizeof(int4))) != RT_OK) return rc;
-    // a first capacity: a few tiles per triangle (grown from the frames' totals)
-    s->list_cap = uint32_t(std::min<size_t>(std::max<size_t>(4 * P, size_t(1) << 16), 0x7FFFFFFFull));
-    if ((rc = s->list.alloc(size_t(s->list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
+    for (rt_hw1_scene::Lane& L : s->lane) {
+        if ((rc = L.rects.alloc(P * sizeof(int4))) != RT_OK) return rc;
+        // a first capacity: a few tiles per triangle (grown from the frames' totals)
+        L.list_cap = uint32_t(std::min<size_t>(std::max<size_t>(4 * P, size_t(1) << 16), 0x7FFFFFFFull));
+        if ((rc = L.list.alloc(size_t(L.list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
+    }
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->total_host), rt_hw1_scene::kRing * sizeof(uint32_t),
                           hipHostMallocCoherent));
     for (int i = 0; i < rt_hw1_scene::kRing; ++i) {
@@ -685,15 +745,13 @@ extern "C" void rt_hw1_scene_destroy(rt_hw1_scene* s) {
     delete s;
 }
 
-extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp,
-                                    const float* jitter, int flags, float* rgb_dev, uint8_t* p6_dev,
-                                    int32_t* hit_idx_dev, float* hit_t_dev, void* stream) {
-    if (!s || !cam || spp < 1) return set_error(RT_ERR_ARG, "rt_render_hw1_device: bad argument");
-    if ((hit_idx_dev == nullptr) != (hit_t_dev == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
+// One frame on lane li, on stream st (rt_render_hw1_device: lane 0, the caller's stream;
+// rt_render_hw1_deliver: the lanes in turn, each on its own stream).
+static int render_frame(rt_hw1_scene* s, int li, const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp,
+                        const float* jitter, int flags, float* rgb_dev, uint8_t* p6_dev, int32_t* hit_idx_dev,
+                        float* hit_t_dev, hipStream_t st) {
     const int W = cam->pixel_width, H = cam->pixel_height;
-    if (W < 1 || H < 1) return set_error(RT_ERR_ARG, "camera has no pixels");
-    DeviceGuard g(s->device);
-    hipStream_t st = static_cast<hipStream_t>(stream);
+    rt_hw1_scene::Lane& L = s->lane[li];
     int rc;
     // jitter_samples(spp, 42u) offsets in [0,1) (HW1/include/antialias.h:12-27), or the caller's
     // (the default table of the scene's current spp is already uploaded: nothing to make)
@@ -705,7 +763,7 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
         else if ((rc = rt_jittered_samples(spp, 42u, 0, tab.data())) != RT_OK) return rc;
     }
     if (!have_default && (s->jitter_spp != spp || s->jitter_host != tab)) {
-        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->end_of(int((s->frames - 1) % rt_hw1_scene::kRing))));
+        HIP_TRY(s->sync_all());  // every lane's frames read the table
         if ((rc = s->jitter.upload(tab.data(), tab.size() * sizeof(float))) != RT_OK) return rc;
         s->jitter_spp = spp;
         s->jitter_host = tab;
@@ -718,29 +776,31 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
         const int sl = int((s->frames - b) % rt_hw1_scene::kRing);
         if (hipEventQuery(s->end_of(sl)) != hipSuccess) continue;
         const uint32_t tot = s->total_host[sl];
-        if (tot > s->list_cap) {  // grow (the old list may still be read by frames in flight)
-            HIP_TRY(hipEventSynchronize(s->end_of(int((s->frames - 1) % rt_hw1_scene::kRing))));
-            s->list_cap = uint32_t(std::min<uint64_t>(uint64_t(tot) + tot / 4 + 1024, 0x7FFFFFFFull));
-            if ((rc = s->list.alloc(size_t(s->list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
-            s->bins_tiles = -1;  // the chunk table follows the list's capacity
+        if (tot > L.list_cap) {  // grow (the old list may still be read by the lane's frames in flight)
+            HIP_TRY(s->sync_lane(L));
+            L.list_cap = uint32_t(std::min<uint64_t>(uint64_t(tot) + tot / 4 + 1024, 0x7FFFFFFFull));
+            if ((rc = L.list.alloc(size_t(L.list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
+            L.bins_tiles = -1;  // the chunk table follows the list's capacity
         }
         break;
     }
     (void)hipGetLastError();  // a not-ready query is not an error of this call
     const size_t nsamples = size_t(W) * size_t(H) * size_t(spp);
-    if (!brute && (s->bins_tiles != ntiles || s->keys_n != nsamples)) {
-        if (s->frames > 0) HIP_TRY(hipEventSynchronize(s->end_of(int((s->frames - 1) % rt_hw1_scene::kRing))));
+    if (!brute && (L.bins_tiles != ntiles || L.keys_n != nsamples)) {
+        HIP_TRY(s->sync_lane(L));
         // counts | cursor | offsets (ntiles + 1): counts and cursor zeroed here, then by every
-        // frame's resolve pass for the next
-        if ((rc = s->bins.alloc(size_t(3 * ntiles + 1) * sizeof(uint32_t))) != RT_OK) return rc;
-        HIP_TRY(hipMemset(s->bins.p, 0, size_t(2 * ntiles) * sizeof(uint32_t)));
+        // frame's resolve pass for the lane's next
+        if ((rc = L.bins.alloc(size_t(3 * ntiles + 1) * sizeof(uint32_t))) != RT_OK) return rc;
+        // (on the frame's stream: a null-stream memset is not ordered before a non-blocking
+        // stream's kernels)
+        HIP_TRY(hipMemsetAsync(L.bins.p, 0, size_t(2 * ntiles) * sizeof(uint32_t), st));
         // chunks: at most one per HW1_CHUNK listed entries plus one per tile
-        s->chunk_cap = uint32_t(std::min<uint64_t>(uint64_t(s->list_cap) / HW1_CHUNK + uint64_t(ntiles) + 1, 0x7FFFFFFFull));
-        if ((rc = s->chunks.alloc((size_t(ntiles) + 1 + s->chunk_cap) * sizeof(uint32_t))) != RT_OK) return rc;
-        if ((rc = s->keys.alloc(nsamples * sizeof(unsigned long long))) != RT_OK) return rc;
-        HIP_TRY(hipMemset(s->keys.p, 0xFF, nsamples * sizeof(unsigned long long)));
-        s->bins_tiles = ntiles;
-        s->keys_n = nsamples;
+        L.chunk_cap = uint32_t(std::min<uint64_t>(uint64_t(L.list_cap) / HW1_CHUNK + uint64_t(ntiles) + 1, 0x7FFFFFFFull));
+        if ((rc = L.chunks.alloc((size_t(ntiles) + 1 + L.chunk_cap) * sizeof(uint32_t))) != RT_OK) return rc;
+        if ((rc = L.keys.alloc(nsamples * sizeof(unsigned long long))) != RT_OK) return rc;
+        HIP_TRY(hipMemsetAsync(L.keys.p, 0xFF, nsamples * sizeof(unsigned long long), st));
+        L.bins_tiles = ntiles;
+        L.keys_n = nsamples;
     }
     Hw1Params hp;
     hp.tri = static_cast<const float4*>(s->tri.p);
@@ -760,21 +820,20 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
     hp.hit_idx = hit_idx_dev;
     hp.hit_t = hit_t_dev;
     hp.p6 = p6_dev;
-    hp.rects = static_cast<const int4*>(s->rects.p);
+    hp.rects = static_cast<const int4*>(L.rects.p);
     hp.bin_count = hp.bin_offset = hp.bin_list = nullptr;
-    hp.list_cap = s->list_cap;
+    hp.list_cap = L.list_cap;
     hp.chunk_first = hp.chunk_tile = nullptr;
-    hp.chunk_cap = s->chunk_cap;
-    hp.keys = static_cast<unsigned long long*>(s->keys.p);
-    hp.zero_counts = static_cast<uint32_t*>(s->bins.p);
+    hp.chunk_cap = L.chunk_cap;
+    hp.keys = static_cast<unsigned long long*>(L.keys.p);
+    hp.zero_counts = static_cast<uint32_t*>(L.bins.p);
     hp.ntiles = ntiles;
     const int sl = int(s->frames % rt_hw1_scene::kRing);
-    // the scene's buffers are shared by its frames: a frame on another stream waits for the last
-    if (s->frames > 0 && st != s->last_stream)
-        HIP_TRY(hipStreamWaitEvent(st, s->end_of(int((s->frames - 1) % rt_hw1_scene::kRing)), 0));
-    s->last_stream = st;
+    // the lane's buffers are shared by its frames: a frame on another stream waits for the last
+    if (L.used && st != L.last_stream) HIP_TRY(hipStreamWaitEvent(st, s->frame_end(L.last_frame), 0));
     const uint64_t every = uint64_t(std::clamp(rt::tuning(RT_TUNE_KERNEL_TIMING_EVERY, 4.0), 1.0, 256.0));
     s->timed[sl] = !s->in_deliver || s->frames % every == 0;
+    s->lane_of[sl] = li;
     // the timestamps are taken by the first and last dispatches themselves (hipExtLaunchKernel
     // start / stop events), not by event packets between them
     hipEvent_t t0 = s->timed[sl] ? s->e0[sl] : nullptr, t1 = s->end_of(sl);
@@ -786,31 +845,44 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
         // one wave per 64 triangles (a block each): the per-triangle passes spread over every CU
         // (256-thread blocks kept c2's 19,858 triangles on 78 CUs: 30 + 25 us)
         const dim3 tgrid(unsigned((s->P + 63) / 64));
-        uint32_t* counts = static_cast<uint32_t*>(s->bins.p);  // zeroed by the previous frame's resolve
+        uint32_t* counts = static_cast<uint32_t*>(L.bins.p);  // zeroed by the lane's previous resolve
         uint32_t* cursor = counts + ntiles;
         uint32_t* offsets = cursor + ntiles;  // ntiles + 1 entries
-        uint32_t* cfirst = static_cast<uint32_t*>(s->chunks.p);
+        uint32_t* cfirst = static_cast<uint32_t*>(L.chunks.p);
         uint32_t* ctile = cfirst + ntiles + 1;
         hipExtLaunchKernelGGL(hw1_rect_count_kernel, tgrid, dim3(64), 0, st, t0, nullptr, 0, hp,
-                              static_cast<int4*>(s->rects.p), counts);
-        hipLaunchKernelGGL(hw1_scan_chunks_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, ntiles, s->list_cap,
-                           cfirst, ctile, s->chunk_cap, s->total_host + sl);
+                              static_cast<int4*>(L.rects.p), counts);
+        hipLaunchKernelGGL(hw1_scan_chunks_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, ntiles, L.list_cap,
+                           cfirst, ctile, L.chunk_cap, s->total_host + sl);
         hp.bin_count = counts;
         hp.bin_offset = offsets;
-        hp.bin_list = static_cast<const uint32_t*>(s->list.p);
+        hp.bin_list = static_cast<const uint32_t*>(L.list.p);
         hp.chunk_first = cfirst;
         hp.chunk_tile = ctile;
-        hipLaunchKernelGGL(hw1_fill_kernel, tgrid, dim3(64), 0, st, hp, cursor, static_cast<uint32_t*>(s->list.p));
+        hipLaunchKernelGGL(hw1_fill_kernel, tgrid, dim3(64), 0, st, hp, cursor, static_cast<uint32_t*>(L.list.p));
         // chunks grid-stride over a grid of every CU's worth of waves (the count is on the device)
         hipLaunchKernelGGL(render_hw1_chunks_kernel, dim3(1024), dim3(BLOCK), 0, st, hp);
         const int rgrid = (std::max(W * H, 2 * ntiles) + BLOCK - 1) / BLOCK;
         hipExtLaunchKernelGGL(hw1_resolve_kernel, dim3(rgrid), dim3(BLOCK), 0, st, nullptr, t1, 0, hp);
         s->last_kernel = "render_hw1_chunks_kernel";
-        HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipGetLastError());
+    L.used = true;
+    L.last_stream = st;
+    L.last_frame = s->frames;
     s->frames++;
     return RT_OK;
+}
+
+extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp,
+                                    const float* jitter, int flags, float* rgb_dev, uint8_t* p6_dev,
+                                    int32_t* hit_idx_dev, float* hit_t_dev, void* stream) {
+    if (!s || !cam || spp < 1) return set_error(RT_ERR_ARG, "rt_render_hw1_device: bad argument");
+    if ((hit_idx_dev == nullptr) != (hit_t_dev == nullptr)) return set_error(RT_ERR_ARG, "hit_idx and hit_t go together");
+    if (cam->pixel_width < 1 || cam->pixel_height < 1) return set_error(RT_ERR_ARG, "camera has no pixels");
+    DeviceGuard g(s->device);
+    return render_frame(s, 0, cam, lpos, lcol, spp, jitter, flags, rgb_dev, p6_dev, hit_idx_dev, hit_t_dev,
+                        static_cast<hipStream_t>(stream));
 }
 
 // A frame delivered to host memory (C2's bench step, as rt_renderer delivers G/ frames): the
@@ -818,6 +890,8 @@ extern "C" int rt_render_hw1_device(rt_hw1_scene* s, const rt_camera* cam, rt_ve
 // copied on the scene's copy stream once the frame's kernels are done, so the copy of frame k
 // overlaps the kernels of frame k+1 instead of following them on one stream (VERDICT r05 item 8:
 // 0.129 ms per step against 0.096 of kernels when the caller copied on the render stream).
+// Frames alternate over the scene's lanes (RT_TUNE_HW1_LANES), each lane's frames in order on its
+// own stream after the work already queued on the caller's stream.
 extern "C" int rt_render_hw1_deliver(rt_hw1_scene* s, const rt_camera* cam, rt_vec3 lpos, rt_vec3 lcol, int spp,
                                      int flags, uint8_t* host_p6, void* stream, uint64_t* ticket) {
     if (!s || !cam || !host_p6 || !ticket || spp < 1) return set_error(RT_ERR_ARG, "rt_render_hw1_deliver: bad argument");
@@ -825,41 +899,80 @@ extern "C" int rt_render_hw1_deliver(rt_hw1_scene* s, const rt_camera* cam, rt_v
     if (W < 1 || H < 1) return set_error(RT_ERR_ARG, "camera has no pixels");
     DeviceGuard g(s->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (!s->copy) {
-        HIP_TRY(hipStreamCreateWithFlags(&s->copy, hipStreamNonBlocking));
-        for (int i = 0; i < rt_hw1_scene::kRing; ++i) {
-            HIP_TRY(hipEventCreateWithFlags(&s->cdone[i], hipEventDisableTiming));
+    int rc;
+    if (s->copy_mode < 0) {
+        // RT_TUNE_COPY_ENGINE: -1 (default) SDMA when the HSA runtime offers it, 0 the runtime's
+        // copies, 1 SDMA or fail
+        const int want = int(rt::tuning(RT_TUNE_COPY_ENGINE, -1.0));
+        hsa_agent_t ga{0}, ca{0};
+        if (want != 0 && rt_dma::hsa_agents(s->device, &ga, &ca)) {
+            for (hsa_signal_t& d : s->dma_done)
+                if (rt_dma::hsa().signal_create(0, 0, nullptr, &d) != HSA_STATUS_SUCCESS)
+                    return set_error(RT_ERR_HIP, "hsa_signal_create failed");
+            s->dma = std::make_unique<rt_dma::DmaCopier>(ga, ca);
+            s->copy_mode = 1;
+        } else if (want == 1) {
+            return set_error(RT_ERR_UNSUPPORTED, "SDMA delivery unavailable: " + rt_dma::hsa().err);
+        } else {
+            HIP_TRY(hipStreamCreateWithFlags(&s->copy, hipStreamNonBlocking));
+            for (int i = 0; i < rt_hw1_scene::kRing; ++i)
+                HIP_TRY(hipEventCreateWithFlags(&s->cdone[i], hipEventDisableTiming));
+            s->copy_mode = 0;
         }
     }
     const uint64_t k = s->tickets;
     const int slot = int(k % rt_hw1_scene::kDeliver), ring = int(k % rt_hw1_scene::kRing);
+    // (a lane's frames overlap the others' only on a hardware queue of its own: HIP gives a process
+    // GPU_MAX_HW_QUEUES of them, 4 by default and shared with the caller's streams.  c2: 2 lanes
+    // 0.058 ms per frame with 4 queues, 3 lanes 0.073 (two lanes on one queue); with 8 queues
+    // 3 lanes 0.046, 4 lanes 0.042)
+    const int nl = int(std::clamp(rt::tuning(RT_TUNE_HW1_LANES, 2.0), 1.0, double(rt_hw1_scene::kLanes)));
+    const int li = int(k % uint64_t(nl));
+    rt_hw1_scene::Lane& L = s->lane[li];
+    if (!L.own) HIP_TRY(hipStreamCreateWithFlags(&L.own, hipStreamNonBlocking));
+    if (!s->caller) HIP_TRY(hipEventCreateWithFlags(&s->caller, hipEventDisableTiming));
+    // work queued on the caller's stream comes first (a wait only while some is pending)
+    if (hipStreamQuery(st) != hipSuccess) {
+        (void)hipGetLastError();
+        HIP_TRY(hipEventRecord(s->caller, st));
+        HIP_TRY(hipStreamWaitEvent(L.own, s->caller, 0));
+    }
     const size_t bytes = size_t(W) * size_t(H) * 3;
-    // ticket k - kRing used these events: it must be complete before they are recorded again
-    if (k >= uint64_t(rt_hw1_scene::kRing)) HIP_TRY(hipEventSynchronize(s->cdone[ring]));
+    // ticket k - kRing used this ring entry: its copy must have landed before it is reused
+    if (k >= uint64_t(rt_hw1_scene::kRing) && (rc = s->wait_copy(k - rt_hw1_scene::kRing)) != RT_OK) return rc;
+    const bool prev = k >= uint64_t(rt_hw1_scene::kDeliver);  // the body's previous frame
     if (s->dp6[slot].n < bytes) {
-        if (k >= uint64_t(rt_hw1_scene::kDeliver))  // the slot's previous frame may still be copied
-            HIP_TRY(hipEventSynchronize(s->cdone[(k - rt_hw1_scene::kDeliver) % rt_hw1_scene::kRing]));
-        int rc = s->dp6[slot].alloc(bytes);
-        if (rc != RT_OK) return rc;
-    } else if (k >= uint64_t(rt_hw1_scene::kDeliver)) {
-        // the slot's previous copy: a wait on the render stream only while it is still running
+        if (prev && (rc = s->wait_copy(k - rt_hw1_scene::kDeliver)) != RT_OK) return rc;
+        if ((rc = s->dp6[slot].alloc(bytes)) != RT_OK) return rc;
+    } else if (prev && s->copy_mode == 1) {
+        // the body's previous copy has landed (kDeliver frames back: normally long done)
+        if ((rc = s->wait_copy(k - rt_hw1_scene::kDeliver)) != RT_OK) return rc;
+    } else if (prev) {
+        // the slot's previous copy: a wait on the lane's stream only while it is still running
         // (a cross-stream wait holds the next frame's first kernel even when already satisfied)
-        hipEvent_t prev = s->cdone[(k - rt_hw1_scene::kDeliver) % rt_hw1_scene::kRing];
-        if (hipEventQuery(prev) != hipSuccess) {
+        hipEvent_t pe = s->cdone[(k - rt_hw1_scene::kDeliver) % rt_hw1_scene::kRing];
+        if (hipEventQuery(pe) != hipSuccess) {
             (void)hipGetLastError();  // not ready is not an error of this call
-            HIP_TRY(hipStreamWaitEvent(st, prev, 0));
+            HIP_TRY(hipStreamWaitEvent(L.own, pe, 0));
         }
     }
     s->in_deliver = true;
-    int rc = rt_render_hw1_device(s, cam, lpos, lcol, spp, nullptr, flags, nullptr,
-                                  static_cast<uint8_t*>(s->dp6[slot].p), nullptr, nullptr, stream);
+    rc = render_frame(s, li, cam, lpos, lcol, spp, nullptr, flags, nullptr, static_cast<uint8_t*>(s->dp6[slot].p),
+                      nullptr, nullptr, L.own);
     s->in_deliver = false;
     if (rc != RT_OK) return rc;
     // the copy waits for the frame's end event, set by its last kernel's dispatch (a marker
     // packet here held the next frame's first kernel: ~16 us between frames)
-    HIP_TRY(hipStreamWaitEvent(s->copy, s->end_of(int((s->frames - 1) % rt_hw1_scene::kRing)), 0));
-    HIP_TRY(hipMemcpyAsync(host_p6, s->dp6[slot].p, bytes, hipMemcpyDeviceToHost, s->copy));
-    HIP_TRY(hipEventRecord(s->cdone[ring], s->copy));
+    hipEvent_t end = s->frame_end(s->frames - 1);
+    if (s->copy_mode == 1) {
+        rt_dma::hsa().signal_store(s->dma_done[ring], 1);
+        s->dma_pending[ring] = true;
+        s->dma->push({end, host_p6, s->dp6[slot].p, bytes, s->dma_done[ring]});
+    } else {
+        HIP_TRY(hipStreamWaitEvent(s->copy, end, 0));
+        HIP_TRY(hipMemcpyAsync(host_p6, s->dp6[slot].p, bytes, hipMemcpyDeviceToHost, s->copy));
+        HIP_TRY(hipEventRecord(s->cdone[ring], s->copy));
+    }
     *ticket = k;
     s->tickets++;
     return RT_OK;
@@ -872,8 +985,7 @@ extern "C" int rt_hw1_wait(rt_hw1_scene* s, uint64_t ticket) {
     if (ticket >= s->tickets || ticket + rt_hw1_scene::kRing < s->tickets)
         return set_error(RT_ERR_ARG, "rt_hw1_wait: not one of the last 64 delivered frames");
     DeviceGuard g(s->device);
-    HIP_TRY(hipEventSynchronize(s->cdone[ticket % rt_hw1_scene::kRing]));
-    return RT_OK;
+    return s->wait_copy(ticket);
 }
 
 extern "C" int rt_hw1_kernel_times(const rt_hw1_scene* s, float* ms_out, int max, int* n_out) {
@@ -901,10 +1013,11 @@ extern "C" const char* rt_hw1_kernel_name(const rt_hw1_scene* s) { return s ? s-
 extern "C" int rt_hw1_list_info(const rt_hw1_scene* s, int64_t info[2]) {
     if (!s || !info) return set_error(RT_ERR_ARG, "rt_hw1_list_info: null argument");
     DeviceGuard g(s->device);
-    info[0] = s->list_cap;
+    info[0] = s->lane[0].list_cap;
     info[1] = 0;
     if (s->frames > 0) {
         const int sl = int((s->frames - 1) % rt_hw1_scene::kRing);
+        info[0] = s->lane[s->lane_of[sl]].list_cap;
         HIP_TRY(hipEventSynchronize(s->end_of(sl)));
         info[1] = s->total_host[sl];
     }

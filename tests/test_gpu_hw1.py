@@ -55,12 +55,16 @@ def test_resident_hw1_frames_match_reference(name, cfg):
         sc.close()
 
 
-@pytest.mark.parametrize("name,cfg", [("c1_full", "c1"), ("c2_full", "c2")])
-def test_delivered_hw1_frames_match_reference(name, cfg):
-    """rt_render_hw1_deliver (the C1/C2 bench step): frames pipelined 3 deep into pinned host
-    buffers, each copied on the scene's copy stream while the next renders; every delivered body
-    is the reference's P6 file, including frames whose device ring slot and host buffer were
-    reused, and a stale ticket is refused."""
+@pytest.mark.parametrize("name,cfg,lanes,engine", [("c1_full", "c1", 2, -1), ("c2_full", "c2", 2, -1),
+                                                   ("c2_full", "c2", 1, -1), ("c2_full", "c2", 2, 0),
+                                                   ("c2_full", "c2", 1, 0)])
+def test_delivered_hw1_frames_match_reference(name, cfg, lanes, engine, tune):
+    """rt_render_hw1_deliver (the C1/C2 bench step): frames pipelined into pinned host buffers,
+    alternating over the scene's lanes (RT_TUNE_HW1_LANES) and each copied by a DMA engine or on
+    the scene's copy stream (RT_TUNE_COPY_ENGINE) while the next render; every delivered body is
+    the reference's P6 file, including frames whose device body (8 frames back) and host buffer
+    were reused, and a stale ticket is refused."""
+    tune(hw1_lanes=lanes, copy_engine=engine)
     c = configs.HW1_CONFIGS[cfg]
     meta = golden_meta(name)
     W, H = meta["width"], meta["height"]
@@ -72,7 +76,7 @@ def test_delivered_hw1_frames_match_reference(name, cfg):
     st = torch.cuda.Stream()
     try:
         pend = []
-        for k in range(12):
+        for k in range(20):
             if len(pend) >= 2:
                 t, b = pend.pop(0)
                 sc.wait(t)
@@ -127,5 +131,34 @@ def test_bin_list_capacity_fallback_is_exact():
             for x, y in zip(got, ref):
                 assert np.array_equal(x.view(np.uint8), y.view(np.uint8))
         assert (ref[2] >= 0).mean() > 0.3
+    finally:
+        sc.close()
+
+
+def test_delivered_frames_grow_each_lane_list_and_mix_with_direct_frames(tune):
+    """Delivered frames over two lanes whose lists outgrow the first capacity (each lane grows its
+    own list from a finished frame's total, the overflowing tiles of the frames before take the
+    brute-force loop), interleaved with direct frames on the caller's stream (lane 0 shared by
+    both streams): every P6 body equals the brute-force kernel's."""
+    tune(hw1_lanes=2)
+    pos, nrm, idx = _big_triangles()
+    c = {"light_pos": (-3.0, 0.0, 1.0), "light_color": (1.0, 0.0, 1.0)}
+    W, H = 1920, 1080
+    cam = rt.Camera((0.0, 0.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, 24.0, W, H, hw1=True)
+    sc = rt.HW1Scene(pos, nrm, idx)
+    host = [torch.zeros(W * H * 3, dtype=torch.uint8, pin_memory=True) for _ in range(4)]
+    st = torch.cuda.Stream()
+    try:
+        want = _frame(sc, cam, c, 1, brute=True)[1].tobytes()
+        cap0 = sc.list_info()[0]
+        for rnd in range(3):
+            tickets = [sc.render_deliver(cam, c["light_pos"], c["light_color"], 1, host[k].data_ptr(),
+                                         stream=st.cuda_stream) for k in range(4)]
+            for k, t in enumerate(tickets):
+                sc.wait(t)
+                assert host[k].numpy().tobytes() == want, (rnd, k)
+                host[k].zero_()
+            assert _frame(sc, cam, c, 1)[1].tobytes() == want, rnd  # a direct frame (lane 0)
+        assert sc.list_info()[0] > cap0  # the lists grew
     finally:
         sc.close()

@@ -45,6 +45,26 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
+HW1_CONFIG_NAMES = ("c1", "c2")  # configs.HW1_CONFIGS (checked in main; the package loads HIP, so later)
+
+
+def _argv_value(argv, flag):
+    for i, x in enumerate(argv):
+        if x == flag and i + 1 < len(argv):
+            return argv[i + 1]
+        if x.startswith(flag + "="):
+            return x.split("=", 1)[1]
+    return None
+
+
+# The HW1 delivery's frames alternate over lanes, and a lane overlaps the others only on a hardware
+# queue of its own (rt_render_hw1_deliver, RT_TUNE_HW1_LANES): HIP gives a process
+# GPU_MAX_HW_QUEUES of them (4 by default); 8 hold the 4 lanes hw1_main runs.  HIP reads it at its
+# initialisation, so it is set here, before torch loads the runtime (--hw-queues).
+HW1_HW_QUEUES, HW1_LANES = 8, 4
+if _argv_value(sys.argv[1:], "--config") in HW1_CONFIG_NAMES:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(int(_argv_value(sys.argv[1:], "--hw-queues") or HW1_HW_QUEUES))
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402  (import before librt_mi355x: one HIP runtime in the process)
 import torch.distributed as dist  # noqa: E402
@@ -96,6 +116,9 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="--comm torch only. gloo: CPU-staged gather (lets N ranks share one GPU)")
     ap.add_argument("--gather-payload", default="p6", choices=["p6", "f32"], help="--comm torch only")
+    ap.add_argument("--hw-queues", type=int, default=HW1_HW_QUEUES,
+                    help="c1 / c2: GPU_MAX_HW_QUEUES for this process (a delivery lane per 2; set before HIP "
+                         "initialises)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
@@ -714,6 +737,10 @@ def hw1_main(a):
         raise SystemExit("bench: the HW1 configurations run on one GPU (replicas only)")
     c = configs.HW1_CONFIGS[a.config]
     W, H, spp = c["width"], c["height"], c["spp"]
+    queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    if not any(kv.startswith("hw1_lanes=") for kv in a.tune):  # a lane per 2 hardware queues, 2..4
+        rt.set_tuning("hw1_lanes", min(max(queues // 2, 2), HW1_LANES))
+    lanes = int(rt.get_tuning("hw1_lanes"))
     mesh = rt.MeshHW1(configs.MESHES / c["mesh"])
     cam = rt.Camera(c["position"], c["look_at"], c["up"], c["focal_mm"], c["sensor_mm"], W, H, hw1=True)
     dev = torch.device("cuda", 0)
@@ -730,14 +757,16 @@ def hw1_main(a):
     # ~16 us idle between frames, profiles/r06/exp/c2_deliver_trace_summary.json)
     depth = 6
     host = [torch.empty(W * H * 3, dtype=torch.uint8, pin_memory=True) for _ in range(depth)]
-    nxt = {"k": 0, "submit_s": 0.0}
+    nxt = {"k": 0, "submit_s": 0.0, "wait_s": 0.0}
 
     def frames(n):
         pend = []
         for _ in range(n):
             k = nxt["k"]
             if len(pend) >= depth - 1:
+                tw = time.perf_counter()
                 sc.wait(pend.pop(0))
+                nxt["wait_s"] += time.perf_counter() - tw
             ts = time.perf_counter()
             pend.append(sc.render_deliver(cam, c["light_pos"], c["light_color"], spp, host[k % depth].data_ptr(),
                                           stream=st.cuda_stream))
@@ -752,7 +781,7 @@ def hw1_main(a):
     frames(a.warmup)
     st.synchronize()
     t0 = time.perf_counter()
-    nxt["submit_s"] = 0.0
+    nxt["submit_s"] = nxt["wait_s"] = 0.0
     frames(a.steps)
     st.synchronize()
     elapsed = time.perf_counter() - t0
@@ -772,25 +801,31 @@ def hw1_main(a):
                        "step_delivers": "the frame's P6 samples in host memory (pinned), copied by a DMA engine "
                                          "while the next frames render (rt_render_hw1_deliver), every frame "
                                          "waited for",
-                       "pipeline": "frames alternate over 2 lanes (binning buffers + a stream each, "
-                                   "RT_TUNE_HW1_LANES): one frame's latency-bound binning passes run beside "
-                                   "the other's render kernel; every frame runs all five passes",
+                       "pipeline": f"frames alternate over {lanes} lanes (binning buffers + a stream each, "
+                                   f"RT_TUNE_HW1_LANES; GPU_MAX_HW_QUEUES={queues}): one frame's latency-bound "
+                                   "binning passes run beside the others' render kernels; every frame runs all "
+                                   "four passes",
+                       "lanes": lanes, "hw_queues": queues,
                        "kernels": "hw1_rect_count_kernel + hw1_scan_chunks_kernel + hw1_fill_kernel + "
-                                  "render_hw1_chunks_kernel + hw1_resolve_kernel (rt_render_hw1_device)"}}
+                                  "render_hw1_chunks_kernel (the resolve fused in; rt_render_hw1_device)"}}
     if a.tune:
         line["config"]["tuning"] = dict(kv.partition("=")[::2] for kv in a.tune)
     instance = sc.kernel_name()
     tr = load_traffic(Path(a.traffic_file), a.config, instance)
     roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": instance,
-            "kernel_ms": round(kernel_ms, 4), "note": "kernel_ms: the frame's five launches, HIP events around them"}
-    hw1_kernels = ("hw1_rect_count_kernel", "hw1_scan_chunks_kernel", "hw1_fill_kernel", "render_hw1_chunks_kernel", "hw1_resolve_kernel")
+            "kernel_ms": round(kernel_ms, 4),
+            "note": "kernel_ms: one frame's four launches, HIP events around them (its latency: the lanes' frames "
+                    "overlap); achieved_per_step: the same bytes per ms_per_step"}
+    hw1_kernels = ("hw1_rect_count_kernel", "hw1_scan_chunks_kernel", "hw1_fill_kernel", "render_hw1_chunks_kernel")
     per = (tr or {}).get("per_kernel") or {}
     if tr and all(k in per for k in hw1_kernels):
-        # the frame's five launches (the live kernel_ms spans them): their measured bytes summed
+        # the frame's four launches (the live kernel_ms spans them): their measured bytes summed
         frame_bytes = sum(per[k]["bytes_per_launch"] for k in hw1_kernels)
         ach = frame_bytes / (kernel_ms / 1e3) / 1e9
+        step_ach = frame_bytes / (elapsed / a.steps) / 1e9  # frames overlap over the lanes
+        roof.update(achieved_per_step=round(step_ach, 2), frac_per_step=round(step_ach / HBM_PEAK_GBS, 5))
         roof.update(traffic=frame_bytes, achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
-                    achieved_from=f"measured HBM bytes of the frame's five kernels (rocprofv3 --pmc, "
+                    achieved_from=f"measured HBM bytes of the frame's four kernels (rocprofv3 --pmc, "
                                   f"{tr.get('source', '?')}) / live kernel_ms",
                     per_kernel={k: per[k] for k in hw1_kernels})
         for k in ("issue", "binding"):
@@ -801,7 +836,9 @@ def hw1_main(a):
                     achieved_from=f"no PMC traffic profiled for {instance} on {a.config} (profiles/traffic.json)")
     line["roofline"] = roof
     line["timing"] = {"kernel_ms": round(kernel_ms, 4), "kernel_ms_min": round(float(kms.min()), 4),
-                      "host_submit_ms_per_frame": round(submit_ms, 4)}
+                      "host_submit_ms_per_frame": round(submit_ms, 4),
+                      # host time blocked in rt_hw1_wait per frame: ~0 when the host is what limits the rate
+                      "host_wait_ms_per_frame": round(nxt["wait_s"] / a.steps * 1e3, 4)}
     if not a.no_parity:
         gdir = REPO / "tests" / "golden" / "scenes" / HW1_GOLDEN[a.config]
         want = gzip.open(gdir / "image.ppm.gz").read()
@@ -823,6 +860,7 @@ def main():
     for kv in a.tune:
         k, _, v = kv.partition("=")
         rt.set_tuning(k, float(v))
+    assert set(HW1_CONFIG_NAMES) == set(configs.HW1_CONFIGS), "HW1_CONFIG_NAMES out of date"
     if a.config in configs.HW1_CONFIGS:
         return hw1_main(a)
     ctx = Ctx(a)

@@ -565,7 +565,12 @@ typedef enum {
                                     buffers + a stream each, 1..8; default 2): a lane
                                     overlaps the others only on a hardware queue of its own (HIP:
                                     GPU_MAX_HW_QUEUES per process, 4 by default) */
-    RT_TUNE_COUNT = 22
+    RT_TUNE_HW1_COPY_WAIT = 22,  /* rt_render_hw1_deliver's SDMA copier thread: 1 (default) waits for a frame with
+                                    hipEventSynchronize, 0 polls hipEventQuery; at the scene's first delivery */
+    RT_TUNE_HW1_FUSE = 23,       /* the HW1 scene's frames: bit 0 the scan fused into the count pass (its last
+                                    block, up to 5,120 tiles), bit 1 the resolve fused into the render pass
+                                    (each tile's last item); default 2 */
+    RT_TUNE_COUNT = 24
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */
 int rt_tuning_set(int id, double value);

@@ -148,7 +148,12 @@ class DmaCopier {
         size_t bytes;
         hsa_signal_t done;
     };
-    DmaCopier(hsa_agent_t gpu, hsa_agent_t cpu) : gpu_(gpu), cpu_(cpu) { th_ = std::thread([this] { loop(); }); }
+    // block: wait for a job's event with hipEventSynchronize (one runtime call per job) instead of
+    // polling it with hipEventQuery (each poll takes the runtime's locks the submitting thread
+    // needs for its launches; polling reacts sooner)
+    DmaCopier(hsa_agent_t gpu, hsa_agent_t cpu, bool block = false) : gpu_(gpu), cpu_(cpu), block_(block) {
+        th_ = std::thread([this] { loop(); });
+    }
     ~DmaCopier() {
         {
             std::lock_guard<std::mutex> lk(m_);
@@ -183,9 +188,13 @@ class DmaCopier {
                 q_.pop_front();
             }
             hipError_t e;
-            for (uint32_t i = 0; (e = hipEventQuery(j.ready)) == hipErrorNotReady; ++i) {
-                if (i < 4096) _mm_pause();
-                else std::this_thread::yield();
+            if (block_) {
+                e = hipEventSynchronize(j.ready);
+            } else {
+                for (uint32_t i = 0; (e = hipEventQuery(j.ready)) == hipErrorNotReady; ++i) {
+                    if (i < 4096) _mm_pause();
+                    else std::this_thread::yield();
+                }
             }
             const Hsa& H = hsa();
             hsa_status_t hs = HSA_STATUS_SUCCESS;
@@ -202,6 +211,7 @@ class DmaCopier {
         }
     }
     hsa_agent_t gpu_, cpu_;
+    bool block_ = false;
     std::thread th_;
     std::mutex m_;
     std::condition_variable cv_;

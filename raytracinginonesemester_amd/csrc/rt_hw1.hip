@@ -52,8 +52,22 @@ struct Hw1Params {
     const uint32_t* __restrict__ chunk_first;  // per tile: its first chunk (exclusive prefix; [ntiles] = total)
     uint32_t chunk_cap;                         // chunk_tile's entries
     unsigned long long* __restrict__ keys;      // per (pixel, sample): min over chunks of (t bits << 32 | index)
-    uint32_t* __restrict__ zero_counts;         // resolve: counts + cursor (2 * ntiles) zeroed for the next frame
+    uint32_t* zero_counts;  // counts | cursor | done (3 * ntiles): each tile's resolving item zeroes its own
+                            // entries for the lane's next frame (after every item of the tile read them)
     int32_t ntiles;
+};
+
+// The scan's outputs (hw1_scan_chunks_kernel's arguments, for the scan fused into the count pass).
+struct Hw1Scan {
+    uint32_t* offsets;       // ntiles + 1
+    int32_t n;               // tiles
+    uint32_t list_cap;
+    uint32_t* chunk_first;   // ntiles + 1
+    uint32_t* chunk_tile;    // chunk_cap
+    uint32_t chunk_cap;
+    unsigned long long* total_out;  // host: tag << 32 | list total
+    uint32_t tag;
+    uint32_t* arrive;        // blocks done counting (zeroed again by the last)
 };
 
 // HW1 shade (HW1/include/raytracer.h:21-48), material hard-coded at ray.h:111-114.
@@ -362,24 +376,6 @@ __device__ __forceinline__ void hw1_wave_pairs(uint32_t lane, int k, uint32_t cn
     }
 }
 
-// Pass 1: each triangle's rectangle (kept for pass 2) and its count in every tile it meets.
-// (Launched with 64-thread blocks: one wave each.)
-__global__ __launch_bounds__(64) void hw1_rect_count_kernel(Hw1Params P, int4* __restrict__ rects,
-                                                            uint32_t* __restrict__ counts) {
-    const uint32_t lane = lane_id();
-    const int k = (int)(blockIdx.x * 64 + lane);
-    const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
-    int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;
-    if (k < P.num_tris) {
-        const int4 r = hw1_rect(P, k);
-        rects[k] = r;
-        if (!hw1_tile_range(P, r, tx0, tx1, ty0, ty1)) tx1 = tx0 - 1;
-    }
-    const uint32_t cnt = tx1 >= tx0 && ty1 >= ty0 ? (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1)) : 0u;
-    hw1_wave_pairs(lane, k, cnt, tx0, ty0, tx1 - tx0 + 1,
-                   [&](int tx, int ty, int) { atomicAdd(&counts[ty * tiles_x + tx], 1u); });
-}
-
 // Pass 2: the lists.  A tile whose list would reach past list_cap is not written; the render
 // kernel gives that tile the brute-force loop instead.
 __global__ __launch_bounds__(64) void hw1_fill_kernel(Hw1Params P, uint32_t* __restrict__ cursor,
@@ -401,94 +397,263 @@ __global__ __launch_bounds__(64) void hw1_fill_kernel(Hw1Params P, uint32_t* __r
 // longer makes one wave the kernel's tail.
 constexpr uint32_t HW1_CHUNK = 64;
 
-// Exclusive prefix sum of n counts in one workgroup (n is the number of wave tiles, small);
-// offsets[n] = total.  With chunk_first: the same over the tiles' chunk counts, and every
-// chunk's tile in chunk_tile (at most chunk_cap; chunks past it are not written, the total in
-// chunk_first[n] says how many there were).  total_out (host memory, may be null): the list
-// total, stored from here for the host's capacity check (a 4-byte copy on the frame's stream
-// after the kernels held every frame for its own latency).
+// A tile's work items: one per HW1_CHUNK listed entries, or one brute-force item for a list that
+// does not fit the capacity; one item with no triangles for an empty tile (no triangle's
+// rectangle meets it: every sample misses, and the item resolves the tile).
+__device__ __forceinline__ uint32_t hw1_tile_chunks(uint32_t off, uint32_t c, uint32_t list_cap) {
+    return c == 0 ? 1u : (off + c > list_cap ? 1u : (c + HW1_CHUNK - 1) / HW1_CHUNK);
+}
+
+// Inclusive sum of v over a 1024-thread block: a shuffle scan per wave, then the 16 wave totals
+// through LDS (two barriers; wsum is free again on return).
+__device__ __forceinline__ uint32_t hw1_block_scan(uint32_t v, uint32_t* wsum) {
+    const int t = (int)threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_up((int)v, d);
+        if (lane >= d) v += u;
+    }
+    if (lane == 63) wsum[w] = v;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int i = 0; i < w; ++i) base += wsum[i];
+    __syncthreads();
+    return v + base;
+}
+
+// Inclusive sum of v over the wave's lanes.
+__device__ __forceinline__ uint32_t hw1_wave_incl(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_up((int)v, d);
+        if ((int)lane >= d) v += u;
+    }
+    return v;
+}
+
+// Exclusive prefix sum of n counts in one workgroup (n is the number of wave tiles); offsets[n] =
+// total.  With chunk_first: the same over the tiles' chunk counts, and every chunk's tile in
+// chunk_tile (at most chunk_cap; chunks past it are not written, the total in chunk_first[n] says
+// how many there were).  total_out (host memory, may be null): the list total, stored from here
+// with the frame's tag in the high half for the host's capacity check (a 4-byte copy on the
+// frame's stream after the kernels held every frame for its own latency; the tag tells the host
+// the total is this frame's without asking the runtime).  Each thread takes PER consecutive tiles, kept in registers (PER 0:
+// any number, re-read).
+template <int PER>
 __global__ __launch_bounds__(1024) void hw1_scan_chunks_kernel(const uint32_t* __restrict__ counts,
                                                                uint32_t* __restrict__ offsets, int n, uint32_t list_cap,
                                                                uint32_t* __restrict__ chunk_first,
                                                                uint32_t* __restrict__ chunk_tile, uint32_t chunk_cap,
-                                                               uint32_t* total_out) {
-    __shared__ uint32_t part[1024], cpart[1024];
+                                                               unsigned long long* total_out, uint32_t tag) {
+    __shared__ uint32_t wsum[16];
     const int t = (int)threadIdx.x;
-    const int per = (n + 1023) / 1024;
+    const int per = PER > 0 ? PER : (n + 1023) / 1024;
     const int lo = min(n, t * per), hi = min(n, lo + per);
+    uint32_t c[PER > 0 ? PER : 1];
     uint32_t sum = 0;
-    for (int i = lo; i < hi; ++i) sum += counts[i];
-    part[t] = sum;
-    __syncthreads();
-    for (int st = 1; st < 1024; st <<= 1) {  // Hillis-Steele inclusive scan
-        const uint32_t v = t >= st ? part[t - st] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
+    if constexpr (PER > 0) {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {  // the loads first, all in flight together
+            c[j] = lo + j < hi ? counts[lo + j] : 0u;
+            sum += c[j];
+        }
+    } else {
+        for (int i = lo; i < hi; ++i) sum += counts[i];
     }
+    auto cnt = [&](int j) {
+        if constexpr (PER > 0) return c[j];
+        else return counts[lo + j];
+    };
+    const int m = PER > 0 ? PER : per;
+    const uint32_t incl = hw1_block_scan(sum, wsum);
     // the tiles' chunk counts need the tiles' offsets (a list past the capacity: one chunk)
-    uint32_t run = part[t] - sum, csum = 0;
-    for (int i = lo; i < hi; ++i) {
-        offsets[i] = run;
-        const uint32_t c = counts[i];
-        csum += run + c > list_cap ? 1u : (c + HW1_CHUNK - 1) / HW1_CHUNK;
-        run += c;
+    uint32_t run = incl - sum, csum = 0;
+#pragma unroll 32
+    for (int j = 0; j < m; ++j) {
+        if (lo + j < hi) {
+            const uint32_t cj = cnt(j);
+            offsets[lo + j] = run;
+            csum += hw1_tile_chunks(run, cj, list_cap);
+            run += cj;
+        }
     }
     if (t == 1023) {
-        offsets[n] = part[1023];
-        if (total_out) __hip_atomic_store(total_out, part[1023], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        offsets[n] = incl;
+        if (total_out)
+            __hip_atomic_store(total_out, (unsigned long long)tag << 32 | incl, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    cpart[t] = csum;
-    __syncthreads();
-    for (int st = 1; st < 1024; st <<= 1) {
-        const uint32_t v = t >= st ? cpart[t - st] : 0u;
-        __syncthreads();
-        cpart[t] += v;
-        __syncthreads();
+    const uint32_t cincl = hw1_block_scan(csum, wsum);
+    uint32_t crun = cincl - csum;
+    run = incl - sum;
+#pragma unroll 32
+    for (int j = 0; j < m; ++j) {
+        if (lo + j < hi) {
+            const uint32_t cj = cnt(j);
+            chunk_first[lo + j] = crun;
+            const uint32_t nc = hw1_tile_chunks(run, cj, list_cap);
+            for (uint32_t k = 0; k < nc; ++k)
+                if (crun + k < chunk_cap) chunk_tile[crun + k] = (uint32_t)(lo + j);
+            crun += nc;
+            run += cj;
+        }
     }
-    uint32_t crun = cpart[t] - csum;
-    run = part[t] - sum;
-    for (int i = lo; i < hi; ++i) {
-        chunk_first[i] = crun;
-        const uint32_t c = counts[i];
-        const uint32_t nc = run + c > list_cap ? 1u : (c + HW1_CHUNK - 1) / HW1_CHUNK;
-        for (uint32_t k = 0; k < nc; ++k)
-            if (crun + k < chunk_cap) chunk_tile[crun + k] = (uint32_t)i;
-        crun += nc;
-        run += c;
-    }
-    if (t == 1023) chunk_first[n] = cpart[1023];
+    if (t == 1023) chunk_first[n] = cincl;
 }
 
-// One wave per chunk, grid-stride over the frame's chunks: the tile's 64 pixel lanes run mt_hw1
-// over the chunk's entries and fold each sample's winner into keys with a 64-bit atomicMin of
+// The list offsets and work items of n tiles, by one wave (the fused form of
+// hw1_scan_chunks_kernel, for n <= 64 * PER): lane l takes PER consecutive tiles, loaded together.
+template <int PER>
+__device__ __forceinline__ void hw1_wave_scan_tiles(const uint32_t* counts, const Hw1Scan& S, uint32_t lane) {
+    const int lo = min(S.n, (int)lane * PER), hi = min(S.n, lo + PER);
+    uint32_t c[PER];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {  // (the other blocks' counts: atomics, read at the coherence point)
+        c[j] = lo + j < hi ? __hip_atomic_load(&counts[lo + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        sum += c[j];
+    }
+    const uint32_t incl = hw1_wave_incl(sum, lane);
+    uint32_t run = incl - sum, csum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        if (lo + j < hi) {
+            S.offsets[lo + j] = run;
+            csum += hw1_tile_chunks(run, c[j], S.list_cap);
+            run += c[j];
+        }
+    }
+    if (lane == 63) {
+        S.offsets[S.n] = incl;
+        if (S.total_out)
+            __hip_atomic_store(S.total_out, (unsigned long long)S.tag << 32 | incl, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    const uint32_t cincl = hw1_wave_incl(csum, lane);
+    uint32_t crun = cincl - csum;
+    run = incl - sum;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        if (lo + j < hi) {
+            S.chunk_first[lo + j] = crun;
+            const uint32_t nc = hw1_tile_chunks(run, c[j], S.list_cap);
+            for (uint32_t k = 0; k < nc; ++k)
+                if (crun + k < S.chunk_cap) S.chunk_tile[crun + k] = (uint32_t)(lo + j);
+            crun += nc;
+            run += c[j];
+        }
+    }
+    if (lane == 63) S.chunk_first[S.n] = cincl;
+}
+
+// Pass 1: each triangle's rectangle (kept for pass 2) and its count in every tile it meets.
+// (Launched with 64-thread blocks: one wave each.)  SCAN_PER > 0: the scan fused in -- the last
+// block to finish counting (an arrival counter after a release fence) scans the counts
+// (hw1_wave_scan_tiles), so the frame has no kernel boundary and no launch between the passes.
+template <int SCAN_PER>
+__global__ __launch_bounds__(64) void hw1_rect_count_kernel(Hw1Params P, int4* __restrict__ rects,
+                                                            uint32_t* __restrict__ counts, Hw1Scan S) {
+    const uint32_t lane = lane_id();
+    const int k = (int)(blockIdx.x * 64 + lane);
+    const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
+    int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;
+    if (k < P.num_tris) {
+        const int4 r = hw1_rect(P, k);
+        rects[k] = r;
+        if (!hw1_tile_range(P, r, tx0, tx1, ty0, ty1)) tx1 = tx0 - 1;
+    }
+    const uint32_t cnt = tx1 >= tx0 && ty1 >= ty0 ? (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1)) : 0u;
+    hw1_wave_pairs(lane, k, cnt, tx0, ty0, tx1 - tx0 + 1,
+                   [&](int tx, int ty, int) { atomicAdd(&counts[ty * tiles_x + tx], 1u); });
+    if constexpr (SCAN_PER > 0) {
+        // the hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms: 4-byte agent
+        // atomics both sides): every block's count atomics have completed (vmcnt) before its
+        // arrival add, and the block whose add came last reads the counts with sc1 loads only
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t prev = 0;
+        if (lane == 0) prev = atomicAdd(S.arrive, 1u);
+        if (uni((uint32_t)__shfl((int)prev, 0)) + 1 != gridDim.x) return;
+        if (lane == 0) *S.arrive = 0u;  // for the lane's next frame
+        hw1_wave_scan_tiles<SCAN_PER>(counts, S, lane);
+    }
+}
+
+// One sample of pixel (x, y) from its winner key (~0: no hit): the accepting test's own t, u, v
+// (mt_hw1 again), HW1 shade (HW1/include/raytracer.h:21-48), the AOVs.
+__device__ __forceinline__ f3 hw1_resolve_sample(const Hw1Params& P, int x, int y, int s, unsigned long long key,
+                                                 f3 o, f3 d) {
+    const bool hit = key != ~0ull;
+    const int32_t besti = hit ? (int32_t)(uint32_t)key : -1;
+    f3 p = mk(0.f, 0.f, 0.f), n = p;
+    float best = FLT_MAX;
+    if (hit) {
+        const float4* T = P.tri + 3 * (size_t)besti;
+        const float4 a = T[0], b = T[1], cq = T[2];
+        float t, u, v;
+        mt_hw1(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(cq.x, cq.y, cq.z), t, u, v);
+        best = t;
+        p = add(o, scale(d, t));
+        const float4* N = P.nrm + 3 * (size_t)besti;
+        const float wgt = 1.0f - u - v;
+        n = add(add(scale(mk(N[0].x, N[0].y, N[0].z), wgt), scale(mk(N[1].x, N[1].y, N[1].z), u)),
+                scale(mk(N[2].x, N[2].y, N[2].z), v));
+    }
+    if (P.hit_idx) {
+        const size_t kk = ((size_t)y * P.W + x) * (size_t)P.spp + (size_t)s;
+        P.hit_idx[kk] = besti;
+        P.hit_t[kk] = hit ? best : -1.0f;
+    }
+    return shade_hw1(o, d, hit, p, n, P.lpos, P.lcol);
+}
+
+// The camera ray of sample s of pixel (x, y) (HW1/src/render.cpp:95-104: the jittered position
+// truncated by get_pixel_position(int, int), the direction normalised as HW1's Ray does, ray.h:25).
+__device__ __forceinline__ f3 hw1_dir(const Hw1Params& P, int x, int y, int s) {
+    const float pxs = (float)x + P.jitter[2 * s];
+    const float pys = (float)y + P.jitter[2 * s + 1];
+    const int ix = (int)pxs, iy = (int)pys;
+    const f3 pix = add(add(P.p00, scale(P.du, (float)ix)), scale(P.dv, (float)iy));
+    return unit(sub(pix, P.center));
+}
+
+// One wave per work item, grid-stride over the frame's items: the tile's 64 pixel lanes run mt_hw1
+// over the item's chunk of the tile's list and keep each sample's winner as the key
 // (t bits << 32 | index).  t >= 0 and never -0 (t + 0.0f), so its bits order like its value; the
-// minimum over the chunks is the lexicographic (t, index) minimum of the whole list -- the
-// brute-force loop's winner (rec.t < prev.t keeps the first index).
+// minimum over a tile's chunks is the lexicographic (t, index) minimum of its whole list -- the
+// brute-force loop's winner (rec.t < prev.t keeps the first index).  The frame's resolve is fused
+// in: a tile of one item (its whole list, an empty list, or the brute-force item of a list past
+// the capacity) shades its samples from the keys in registers; a tile of several items folds its
+// keys into `keys` with a 64-bit atomicMin and counts its finished items, and the item finishing
+// last reads the keys back (agent-scope atomic loads, after every item's atomics completed),
+// shades, and resets them.  The tile's counters are left zeroed for the lane's next frame.
+// (FUSED false: every item folds its keys with atomicMin and hw1_resolve_kernel resolves.)
+template <bool FUSED>
 __global__ __launch_bounds__(BLOCK) void render_hw1_chunks_kernel(Hw1Params P) {
     const uint32_t total = uni(P.chunk_first[P.ntiles]);
-    const uint32_t nchunks = total < P.chunk_cap ? total : P.chunk_cap;
+    const uint32_t nitems = total < P.chunk_cap ? total : P.chunk_cap;
     const int tiles_x = (P.W + HW1_TW - 1) / HW1_TW;
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (BLOCK / 64);
-    for (uint32_t j = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64; j < nchunks; j += waves) {
+    uint32_t* const cursor = P.zero_counts + P.ntiles;
+    uint32_t* const done = P.zero_counts + 2 * P.ntiles;
+    for (uint32_t j = blockIdx.x * (BLOCK / 64) + threadIdx.x / 64; j < nitems; j += waves) {
         const uint32_t tidx = uni(P.chunk_tile[uni(j)]);
-        const uint32_t c = j - uni(P.chunk_first[tidx]);
+        const uint32_t first = uni(P.chunk_first[tidx]);
+        const uint32_t items = uni(P.chunk_first[tidx + 1]) - first;
+        const uint32_t c = j - first;
         const uint32_t cnt = uni(P.bin_count[tidx]);
         const uint32_t off = uni(P.bin_offset[tidx]);
-        const bool all = off + cnt > P.list_cap;  // the list was not written: every triangle, in order
+        const bool all = cnt > 0 && off + cnt > P.list_cap;  // the list was not written: every triangle, in order
         const uint32_t b = all ? 0u : c * HW1_CHUNK;
         const uint32_t e = all ? (uint32_t)P.num_tris : min(cnt, b + HW1_CHUNK);
         const int x = (int)(tidx % tiles_x) * HW1_TW + (int)(lane % HW1_TW);
         const int y = (int)(tidx / tiles_x) * HW1_TH + (int)(lane / HW1_TW);
         const bool valid = x < P.W && y < P.H;
+        const bool single = FUSED && items == 1;
+        const f3 o = P.center;
+        f3 acc = mk(0.f, 0.f, 0.f);
         for (int s = 0; s < P.spp; ++s) {
-            const float pxs = (float)x + P.jitter[2 * s];
-            const float pys = (float)y + P.jitter[2 * s + 1];
-            const int ix = (int)pxs, iy = (int)pys;  // get_pixel_position(int, int) truncates
-            const f3 pix = add(add(P.p00, scale(P.du, (float)ix)), scale(P.dv, (float)iy));
-            const f3 d = unit(sub(pix, P.center));  // HW1 Ray normalises (ray.h:25)
-            const f3 o = P.center;
+            const f3 d = hw1_dir(P, x, y, s);
             unsigned long long best = ~0ull;
             for (uint32_t i = b; i < e; i += 4) {
                 int kk[4];
@@ -518,13 +683,44 @@ __global__ __launch_bounds__(BLOCK) void render_hw1_chunks_kernel(Hw1Params P) {
                     }
                 }
             }
-            if (valid && best != ~0ull) atomicMin(&P.keys[((size_t)y * P.W + x) * (size_t)P.spp + (size_t)s], best);
+            if (single) {
+                if (valid) acc = add(acc, hw1_resolve_sample(P, x, y, s, best, o, d));
+            } else if (valid && best != ~0ull) {
+                atomicMin(&P.keys[((size_t)y * P.W + x) * (size_t)P.spp + (size_t)s], best);
+            }
+        }
+        bool resolve = single;
+        if (FUSED && !single) {
+            // the hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms: 8-byte
+            // agent atomics both sides; no fences): this wave's key atomics have completed (vmcnt)
+            // before its count, and the wave whose count came last reads the keys with sc1 loads
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint32_t prev = 0;
+            if (lane == 0) prev = atomicAdd(&done[tidx], 1u);
+            resolve = uni((uint32_t)__shfl((int)prev, 0)) + 1 == items;
+            if (resolve) {
+                for (int s = 0; s < P.spp && valid; ++s) {
+                    unsigned long long* kp = &P.keys[((size_t)y * P.W + x) * (size_t)P.spp + (size_t)s];
+                    const unsigned long long key = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    *kp = ~0ull;
+                    acc = add(acc, hw1_resolve_sample(P, x, y, s, key, o, hw1_dir(P, x, y, s)));
+                }
+            }
+        }
+        if (resolve) {
+            if (valid) hw1_write_pixel(P, x, y, acc);
+            if (lane == 0) {  // (every item of the tile has read its count)
+                P.zero_counts[tidx] = 0u;
+                cursor[tidx] = 0u;
+                done[tidx] = 0u;
+            }
         }
     }
 }
 
-// Per pixel: each sample's winner from keys (then reset for the next frame), HW1 shade, the
-// average, AOVs; the first threads also zero the bin counters for the next frame.
+// The unfused resolve: per pixel, each sample's winner from keys (then reset for the next
+// frame), HW1 shade, the average, AOVs; the first threads also zero the tiles' counts and cursors
+// for the lane's next frame.
 __global__ __launch_bounds__(BLOCK) void hw1_resolve_kernel(Hw1Params P) {
     const int gid = (int)(blockIdx.x * BLOCK + threadIdx.x);
     if (gid < 2 * P.ntiles) P.zero_counts[gid] = 0u;
@@ -532,36 +728,10 @@ __global__ __launch_bounds__(BLOCK) void hw1_resolve_kernel(Hw1Params P) {
     const int x = gid % P.W, y = gid / P.W;
     f3 acc = mk(0.f, 0.f, 0.f);
     for (int s = 0; s < P.spp; ++s) {
-        const float pxs = (float)x + P.jitter[2 * s];
-        const float pys = (float)y + P.jitter[2 * s + 1];
-        const int ix = (int)pxs, iy = (int)pys;
-        const f3 pix = add(add(P.p00, scale(P.du, (float)ix)), scale(P.dv, (float)iy));
-        const f3 d = unit(sub(pix, P.center));
-        const f3 o = P.center;
         const size_t kk = (size_t)gid * (size_t)P.spp + (size_t)s;
         const unsigned long long key = P.keys[kk];
         P.keys[kk] = ~0ull;
-        const bool hit = key != ~0ull;
-        const int32_t besti = hit ? (int32_t)(uint32_t)key : -1;
-        f3 p = mk(0.f, 0.f, 0.f), n = p;
-        float best = FLT_MAX;
-        if (hit) {  // the accepting test's own t, u, v
-            const float4* T = P.tri + 3 * (size_t)besti;
-            const float4 a = T[0], b = T[1], cq = T[2];
-            float t, u, v;
-            mt_hw1(o, d, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(cq.x, cq.y, cq.z), t, u, v);
-            best = t;
-            p = add(o, scale(d, t));
-            const float4* N = P.nrm + 3 * (size_t)besti;
-            const float wgt = 1.0f - u - v;
-            n = add(add(scale(mk(N[0].x, N[0].y, N[0].z), wgt), scale(mk(N[1].x, N[1].y, N[1].z), u)),
-                    scale(mk(N[2].x, N[2].y, N[2].z), v));
-        }
-        acc = add(acc, shade_hw1(o, d, hit, p, n, P.lpos, P.lcol));
-        if (P.hit_idx) {
-            P.hit_idx[kk] = besti;
-            P.hit_t[kk] = hit ? best : -1.0f;
-        }
+        acc = add(acc, hw1_resolve_sample(P, x, y, s, key, P.center, hw1_dir(P, x, y, s)));
     }
     hw1_write_pixel(P, x, y, acc);
 }
@@ -627,7 +797,7 @@ struct rt_hw1_scene {
     bool timed[kRing] = {};
     int lane_of[kRing] = {};  // the lane of frame f at [f % kRing]
     bool in_deliver = false;  // rt_render_hw1_deliver is calling render_frame
-    uint32_t* total_host = nullptr;  // pinned: the list total of frame f at [f % kRing]
+    unsigned long long* total_host = nullptr;  // pinned: frame f's tag (f mod 2^32) << 32 | its list total, at [f % kRing]
     uint64_t frames = 0;
     const char* last_kernel = "";
     // rt_render_hw1_deliver: frames rendered into a ring of kDeliver device P6 bodies, each body
@@ -727,10 +897,10 @@ extern "C" int rt_hw1_scene_create(int device, const rt_vec3* pos, const rt_vec3
         L.list_cap = uint32_t(std::min<size_t>(std::max<size_t>(4 * P, size_t(1) << 16), 0x7FFFFFFFull));
         if ((rc = L.list.alloc(size_t(L.list_cap) * sizeof(uint32_t))) != RT_OK) return rc;
     }
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->total_host), rt_hw1_scene::kRing * sizeof(uint32_t),
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->total_host), rt_hw1_scene::kRing * sizeof(unsigned long long),
                           hipHostMallocCoherent));
     for (int i = 0; i < rt_hw1_scene::kRing; ++i) {
-        s->total_host[i] = 0;
+        s->total_host[i] = ~0ull;  // (no frame's tag)
         HIP_TRY(hipEventCreate(&s->e0[i]));
         HIP_TRY(hipEventCreate(&s->e1[i]));
         HIP_TRY(hipEventCreateWithFlags(&s->f1[i], hipEventDisableTiming));
@@ -771,11 +941,13 @@ static int render_frame(rt_hw1_scene* s, int li, const rt_camera* cam, rt_vec3 l
     if (!have_default) s->jitter_default = jitter == nullptr;
     const bool brute = (flags & RT_HW1_BRUTE) != 0;
     const int ntiles = ((W + HW1_TW - 1) / HW1_TW) * ((H + HW1_TH - 1) / HW1_TH);
-    // the latest finished frame's list total (frames are scanned back to front, non-blocking)
-    for (uint64_t b = 1; b <= std::min<uint64_t>(s->frames, 4); ++b) {
-        const int sl = int((s->frames - b) % rt_hw1_scene::kRing);
-        if (hipEventQuery(s->end_of(sl)) != hipSuccess) continue;
-        const uint32_t tot = s->total_host[sl];
+    // the list total of the latest frame whose scan has run (each total carries its frame's tag:
+    // read from pinned memory, no runtime call)
+    for (uint64_t b = 1; b <= std::min<uint64_t>(s->frames, uint64_t(rt_hw1_scene::kRing) / 2); ++b) {
+        const uint64_t f = s->frames - b;
+        const unsigned long long v = __atomic_load_n(&s->total_host[f % rt_hw1_scene::kRing], __ATOMIC_ACQUIRE);
+        if (uint32_t(v >> 32) != uint32_t(f)) continue;
+        const uint32_t tot = uint32_t(v);
         if (tot > L.list_cap) {  // grow (the old list may still be read by the lane's frames in flight)
             HIP_TRY(s->sync_lane(L));
             L.list_cap = uint32_t(std::min<uint64_t>(uint64_t(tot) + tot / 4 + 1024, 0x7FFFFFFFull));
@@ -784,16 +956,16 @@ static int render_frame(rt_hw1_scene* s, int li, const rt_camera* cam, rt_vec3 l
         }
         break;
     }
-    (void)hipGetLastError();  // a not-ready query is not an error of this call
     const size_t nsamples = size_t(W) * size_t(H) * size_t(spp);
     if (!brute && (L.bins_tiles != ntiles || L.keys_n != nsamples)) {
         HIP_TRY(s->sync_lane(L));
-        // counts | cursor | offsets (ntiles + 1): counts and cursor zeroed here, then by every
-        // frame's resolve pass for the lane's next
-        if ((rc = L.bins.alloc(size_t(3 * ntiles + 1) * sizeof(uint32_t))) != RT_OK) return rc;
+        // counts | cursor | done (finished items) | arrive | offsets (ntiles + 1): the first four
+        // zeroed here, then by every frame's passes (each tile's resolving item, the count pass's
+        // last block) for the lane's next
+        if ((rc = L.bins.alloc(size_t(4 * ntiles + 2) * sizeof(uint32_t))) != RT_OK) return rc;
         // (on the frame's stream: a null-stream memset is not ordered before a non-blocking
         // stream's kernels)
-        HIP_TRY(hipMemsetAsync(L.bins.p, 0, size_t(2 * ntiles) * sizeof(uint32_t), st));
+        HIP_TRY(hipMemsetAsync(L.bins.p, 0, size_t(3 * ntiles + 1) * sizeof(uint32_t), st));
         // chunks: at most one per HW1_CHUNK listed entries plus one per tile
         L.chunk_cap = uint32_t(std::min<uint64_t>(uint64_t(L.list_cap) / HW1_CHUNK + uint64_t(ntiles) + 1, 0x7FFFFFFFull));
         if ((rc = L.chunks.alloc((size_t(ntiles) + 1 + L.chunk_cap) * sizeof(uint32_t))) != RT_OK) return rc;
@@ -839,31 +1011,55 @@ static int render_frame(rt_hw1_scene* s, int li, const rt_camera* cam, rt_vec3 l
     hipEvent_t t0 = s->timed[sl] ? s->e0[sl] : nullptr, t1 = s->end_of(sl);
     const int blocks = ((W + 15) / 16) * ((H + 15) / 16);
     if (brute) {
+        __atomic_store_n(&s->total_host[sl], (unsigned long long)uint32_t(s->frames) << 32, __ATOMIC_RELEASE);  // (no list)
         hipExtLaunchKernelGGL(render_hw1_kernel, dim3(blocks), dim3(BLOCK), 0, st, t0, t1, 0, hp);
         s->last_kernel = "render_hw1_kernel";
     } else {
         // one wave per 64 triangles (a block each): the per-triangle passes spread over every CU
         // (256-thread blocks kept c2's 19,858 triangles on 78 CUs: 30 + 25 us)
         const dim3 tgrid(unsigned((s->P + 63) / 64));
-        uint32_t* counts = static_cast<uint32_t*>(L.bins.p);  // zeroed by the lane's previous resolve
+        uint32_t* counts = static_cast<uint32_t*>(L.bins.p);  // zeroed by the lane's previous frame
         uint32_t* cursor = counts + ntiles;
-        uint32_t* offsets = cursor + ntiles;  // ntiles + 1 entries
-        uint32_t* cfirst = static_cast<uint32_t*>(L.chunks.p);
-        uint32_t* ctile = cfirst + ntiles + 1;
-        hipExtLaunchKernelGGL(hw1_rect_count_kernel, tgrid, dim3(64), 0, st, t0, nullptr, 0, hp,
-                              static_cast<int4*>(L.rects.p), counts);
-        hipLaunchKernelGGL(hw1_scan_chunks_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, ntiles, L.list_cap,
-                           cfirst, ctile, L.chunk_cap, s->total_host + sl);
+        Hw1Scan sc;
+        sc.arrive = cursor + 2 * ntiles;  // (after done)
+        sc.offsets = sc.arrive + 1;       // ntiles + 1 entries
+        sc.n = ntiles;
+        sc.list_cap = L.list_cap;
+        sc.chunk_first = static_cast<uint32_t*>(L.chunks.p);
+        sc.chunk_tile = sc.chunk_first + ntiles + 1;
+        sc.chunk_cap = L.chunk_cap;
+        sc.total_out = s->total_host + sl;
+        sc.tag = uint32_t(s->frames);
+        // the scan fused into the count pass up to 64 x 80 tiles (c2: 4800), else its own
+        // 1024-thread kernel (PER tiles per thread in registers: 8 up to 8192 tiles, 32 up to
+        // 1080p's 32400); the first launch carries the start event only on timed frames
+        const int fuse = int(rt::tuning(RT_TUNE_HW1_FUSE, 2.0));
+        const bool fused = (fuse & 1) && ntiles <= 64 * 80;
+        auto count = fused ? hw1_rect_count_kernel<80> : hw1_rect_count_kernel<0>;
+        int4* rects = static_cast<int4*>(L.rects.p);
+        if (t0) hipExtLaunchKernelGGL(count, tgrid, dim3(64), 0, st, t0, nullptr, 0, hp, rects, counts, sc);
+        else hipLaunchKernelGGL(count, tgrid, dim3(64), 0, st, hp, rects, counts, sc);
+        if (!fused) {
+            auto scan = ntiles <= 8 * 1024 ? hw1_scan_chunks_kernel<8>
+                        : ntiles <= 32 * 1024 ? hw1_scan_chunks_kernel<32> : hw1_scan_chunks_kernel<0>;
+            hipLaunchKernelGGL(scan, dim3(1), dim3(1024), 0, st, counts, sc.offsets, ntiles, L.list_cap,
+                               sc.chunk_first, sc.chunk_tile, L.chunk_cap, sc.total_out, sc.tag);
+        }
         hp.bin_count = counts;
-        hp.bin_offset = offsets;
+        hp.bin_offset = sc.offsets;
         hp.bin_list = static_cast<const uint32_t*>(L.list.p);
-        hp.chunk_first = cfirst;
-        hp.chunk_tile = ctile;
+        hp.chunk_first = sc.chunk_first;
+        hp.chunk_tile = sc.chunk_tile;
         hipLaunchKernelGGL(hw1_fill_kernel, tgrid, dim3(64), 0, st, hp, cursor, static_cast<uint32_t*>(L.list.p));
-        // chunks grid-stride over a grid of every CU's worth of waves (the count is on the device)
-        hipLaunchKernelGGL(render_hw1_chunks_kernel, dim3(1024), dim3(BLOCK), 0, st, hp);
-        const int rgrid = (std::max(W * H, 2 * ntiles) + BLOCK - 1) / BLOCK;
-        hipExtLaunchKernelGGL(hw1_resolve_kernel, dim3(rgrid), dim3(BLOCK), 0, st, nullptr, t1, 0, hp);
+        // items grid-stride over a grid of every CU's worth of waves (the count is on the device);
+        // the resolve fused in, or its own pass
+        if (fuse & 2) {
+            hipExtLaunchKernelGGL(render_hw1_chunks_kernel<true>, dim3(1024), dim3(BLOCK), 0, st, nullptr, t1, 0, hp);
+        } else {
+            hipLaunchKernelGGL(render_hw1_chunks_kernel<false>, dim3(1024), dim3(BLOCK), 0, st, hp);
+            const int rgrid = (std::max(W * H, 2 * ntiles) + BLOCK - 1) / BLOCK;
+            hipExtLaunchKernelGGL(hw1_resolve_kernel, dim3(rgrid), dim3(BLOCK), 0, st, nullptr, t1, 0, hp);
+        }
         s->last_kernel = "render_hw1_chunks_kernel";
     }
     HIP_TRY(hipGetLastError());
@@ -909,7 +1105,7 @@ extern "C" int rt_render_hw1_deliver(rt_hw1_scene* s, const rt_camera* cam, rt_v
             for (hsa_signal_t& d : s->dma_done)
                 if (rt_dma::hsa().signal_create(0, 0, nullptr, &d) != HSA_STATUS_SUCCESS)
                     return set_error(RT_ERR_HIP, "hsa_signal_create failed");
-            s->dma = std::make_unique<rt_dma::DmaCopier>(ga, ca);
+            s->dma = std::make_unique<rt_dma::DmaCopier>(ga, ca, rt::tuning(RT_TUNE_HW1_COPY_WAIT, 1.0) != 0.0);
             s->copy_mode = 1;
         } else if (want == 1) {
             return set_error(RT_ERR_UNSUPPORTED, "SDMA delivery unavailable: " + rt_dma::hsa().err);
@@ -1019,7 +1215,7 @@ extern "C" int rt_hw1_list_info(const rt_hw1_scene* s, int64_t info[2]) {
         const int sl = int((s->frames - 1) % rt_hw1_scene::kRing);
         info[0] = s->lane[s->lane_of[sl]].list_cap;
         HIP_TRY(hipEventSynchronize(s->end_of(sl)));
-        info[1] = s->total_host[sl];
+        info[1] = uint32_t(s->total_host[sl]);
     }
     return RT_OK;
 }

@@ -55,6 +55,29 @@ def test_resident_hw1_frames_match_reference(name, cfg):
         sc.close()
 
 
+@pytest.mark.parametrize("fuse", [0, 1, 2, 3])
+def test_hw1_fused_passes_match_reference(fuse, tune):
+    """RT_TUNE_HW1_FUSE: the scan in the count pass's last block (bit 0) and the resolve in each
+    tile's last render item (bit 1), each on or off: the frames equal the reference's (AOVs and
+    P6), twice in a row on the same buffers (the passes leave the counters zeroed)."""
+    tune(hw1_fuse=fuse)
+    name, c = "c2_full", configs.HW1_CONFIGS["c2"]
+    meta = golden_meta(name)
+    W, H = meta["width"], meta["height"]
+    mesh = rt.MeshHW1(configs.MESHES / c["mesh"])
+    cam = rt.Camera(c["position"], c["look_at"], c["up"], c["focal_mm"], c["sensor_mm"], W, H, hw1=True)
+    sc = rt.HW1Scene(mesh.positions, mesh.normals, mesh.indices)
+    want = gzip.open(GOLDEN / "scenes" / name / "image.ppm.gz").read()
+    try:
+        for _ in range(2):
+            rgb, p6, hi, ht = _frame(sc, cam, c, c["spp"])
+            assert np.array_equal(hi, golden_array(name, "hits.i32.gz", np.int32))
+            assert np.array_equal(ht.view(np.uint32), golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
+            assert rt.p6_header(W, H) + p6.tobytes() == want
+    finally:
+        sc.close()
+
+
 @pytest.mark.parametrize("name,cfg,lanes,engine", [("c1_full", "c1", 2, -1), ("c2_full", "c2", 2, -1),
                                                    ("c2_full", "c2", 1, -1), ("c2_full", "c2", 2, 0),
                                                    ("c2_full", "c2", 1, 0)])

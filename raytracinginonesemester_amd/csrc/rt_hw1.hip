@@ -1060,7 +1060,7 @@ static int render_frame(rt_hw1_scene* s, int li, const rt_camera* cam, rt_vec3 l
             const int rgrid = (std::max(W * H, 2 * ntiles) + BLOCK - 1) / BLOCK;
             hipExtLaunchKernelGGL(hw1_resolve_kernel, dim3(rgrid), dim3(BLOCK), 0, st, nullptr, t1, 0, hp);
         }
-        s->last_kernel = "render_hw1_chunks_kernel";
+        s->last_kernel = (fuse & 2) ? "render_hw1_chunks_kernel<true>" : "render_hw1_chunks_kernel<false>";
     }
     HIP_TRY(hipGetLastError());
     L.used = true;

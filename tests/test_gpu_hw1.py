@@ -49,7 +49,7 @@ def test_resident_hw1_frames_match_reference(name, cfg):
             assert np.array_equal(ht.view(np.uint32), golden_array(name, "hitt.f32.gz", np.float32).view(np.uint32))
             want = gzip.open(GOLDEN / "scenes" / name / "image.ppm.gz").read()
             assert rt.p6_header(W, H) + p6.tobytes() == want
-        assert sc.kernel_name() == "render_hw1_chunks_kernel"
+        assert sc.kernel_name() == "render_hw1_chunks_kernel<true>"  # (as rocprofv3 names it; the resolve fused)
         assert (sc.kernel_times(3) > 0).all()
     finally:
         sc.close()

@@ -565,12 +565,15 @@ typedef enum {
                                     buffers + a stream each, 1..8; default 2): a lane
                                     overlaps the others only on a hardware queue of its own (HIP:
                                     GPU_MAX_HW_QUEUES per process, 4 by default) */
-    RT_TUNE_HW1_COPY_WAIT = 22,  /* rt_render_hw1_deliver's SDMA copier thread: 1 (default) waits for a frame with
-                                    hipEventSynchronize, 0 polls hipEventQuery; at the scene's first delivery */
+    RT_TUNE_COPY_WAIT = 22,      /* the SDMA copier threads (rt_renderer's and rt_hw1_scene's deliveries): 1 waits
+                                    for a frame with hipEventSynchronize, 0 polls hipEventQuery; default
+                                    -1: the renderer polls, the HW1 scene waits; at the copier's creation */
     RT_TUNE_HW1_FUSE = 23,       /* the HW1 scene's frames: bit 0 the scan fused into the count pass (its last
                                     block, up to 5,120 tiles), bit 1 the resolve fused into the render pass
                                     (each tile's last item); default 2 */
-    RT_TUNE_COUNT = 24
+    RT_TUNE_HW1_CHUNK = 24,      /* the HW1 scene's render work items: list entries per item, 16..256, a power of two
+                                    (32) */
+    RT_TUNE_COUNT = 25
 } rt_tune_id;
 /* Set knob id (NaN restores the default).  RT_ERR_ARG for an unknown id. */
 int rt_tuning_set(int id, double value);

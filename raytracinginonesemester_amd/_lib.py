@@ -34,7 +34,7 @@ TUNE = {"frustum_arity": 0, "half_waves": 1, "paired_only": 2, "heavy_frac": 3, 
         "quant_records": 12, "prepass_gate": 13,
         "overlap_frames": 14, "kernel_timing_every": 15,
         "record_greedy": 16, "wide4_greedy": 17, "pair_frames": 18, "pair_reserve": 19,
-        "cut_sub": 20, "hw1_lanes": 21, "hw1_copy_wait": 22, "hw1_fuse": 23}
+        "cut_sub": 20, "hw1_lanes": 21, "copy_wait": 22, "hw1_fuse": 23, "hw1_chunk": 24}
 
 
 class RTError(RuntimeError):

@@ -47,7 +47,7 @@ struct Hw1Params {
     uint8_t* __restrict__ p6;         // optional: write_p6-default samples (W*H*3 bytes)
     uint32_t list_cap;                // binned path: entries bin_list holds; a tile whose list would
                                       // reach past it takes the brute-force loop (exact, slower)
-    // chunked path (rt_render_hw1_device): work items of at most HW1_CHUNK list entries
+    // chunked path (rt_render_hw1_device): work items of at most 2^chunk_log2 list entries
     const uint32_t* __restrict__ chunk_tile;   // per chunk: its tile
     const uint32_t* __restrict__ chunk_first;  // per tile: its first chunk (exclusive prefix; [ntiles] = total)
     uint32_t chunk_cap;                         // chunk_tile's entries
@@ -55,6 +55,7 @@ struct Hw1Params {
     uint32_t* zero_counts;  // counts | cursor | done (3 * ntiles): each tile's resolving item zeroes its own
                             // entries for the lane's next frame (after every item of the tile read them)
     int32_t ntiles;
+    int32_t chunk_log2;  // work item size (RT_TUNE_HW1_CHUNK)
 };
 
 // The scan's outputs (hw1_scan_chunks_kernel's arguments, for the scan fused into the count pass).
@@ -68,6 +69,7 @@ struct Hw1Scan {
     unsigned long long* total_out;  // host: tag << 32 | list total
     uint32_t tag;
     uint32_t* arrive;        // blocks done counting (zeroed again by the last)
+    int32_t chunk_log2;
 };
 
 // HW1 shade (HW1/include/raytracer.h:21-48), material hard-coded at ray.h:111-114.
@@ -395,13 +397,15 @@ __global__ __launch_bounds__(64) void hw1_fill_kernel(Hw1Params P, uint32_t* __r
 // The chunked pass: a tile's list is cut into work items of at most HW1_CHUNK entries (a tile
 // whose list does not fit the capacity is one item over every triangle), so a long list no
 // longer makes one wave the kernel's tail.
-constexpr uint32_t HW1_CHUNK = 64;
+// 32 entries (the default; RT_TUNE_HW1_CHUNK): c2 0.0399-0.0411 ms per step against 0.0420-0.0422
+// with 64, 0.0426 with 16, 0.0465 with 128 (profiles/r06/exp/hw1_chunk/)
+constexpr int HW1_CHUNK_LOG2 = 5;
 
-// A tile's work items: one per HW1_CHUNK listed entries, or one brute-force item for a list that
-// does not fit the capacity; one item with no triangles for an empty tile (no triangle's
-// rectangle meets it: every sample misses, and the item resolves the tile).
-__device__ __forceinline__ uint32_t hw1_tile_chunks(uint32_t off, uint32_t c, uint32_t list_cap) {
-    return c == 0 ? 1u : (off + c > list_cap ? 1u : (c + HW1_CHUNK - 1) / HW1_CHUNK);
+// A tile's work items: one per 2^lg listed entries, or one brute-force item for a list that does
+// not fit the capacity; one item with no triangles for an empty tile (no triangle's rectangle
+// meets it: every sample misses, and the item resolves the tile).
+__device__ __forceinline__ uint32_t hw1_tile_chunks(uint32_t off, uint32_t c, uint32_t list_cap, int lg) {
+    return c == 0 ? 1u : (off + c > list_cap ? 1u : (c + (1u << lg) - 1) >> lg);
 }
 
 // Inclusive sum of v over a 1024-thread block: a shuffle scan per wave, then the 16 wave totals
@@ -444,7 +448,8 @@ __global__ __launch_bounds__(1024) void hw1_scan_chunks_kernel(const uint32_t* _
                                                                uint32_t* __restrict__ offsets, int n, uint32_t list_cap,
                                                                uint32_t* __restrict__ chunk_first,
                                                                uint32_t* __restrict__ chunk_tile, uint32_t chunk_cap,
-                                                               unsigned long long* total_out, uint32_t tag) {
+                                                               unsigned long long* total_out, uint32_t tag,
+                                                               int chunk_log2) {
     __shared__ uint32_t wsum[16];
     const int t = (int)threadIdx.x;
     const int per = PER > 0 ? PER : (n + 1023) / 1024;
@@ -473,7 +478,7 @@ __global__ __launch_bounds__(1024) void hw1_scan_chunks_kernel(const uint32_t* _
         if (lo + j < hi) {
             const uint32_t cj = cnt(j);
             offsets[lo + j] = run;
-            csum += hw1_tile_chunks(run, cj, list_cap);
+            csum += hw1_tile_chunks(run, cj, list_cap, chunk_log2);
             run += cj;
         }
     }
@@ -491,7 +496,7 @@ __global__ __launch_bounds__(1024) void hw1_scan_chunks_kernel(const uint32_t* _
         if (lo + j < hi) {
             const uint32_t cj = cnt(j);
             chunk_first[lo + j] = crun;
-            const uint32_t nc = hw1_tile_chunks(run, cj, list_cap);
+            const uint32_t nc = hw1_tile_chunks(run, cj, list_cap, chunk_log2);
             for (uint32_t k = 0; k < nc; ++k)
                 if (crun + k < chunk_cap) chunk_tile[crun + k] = (uint32_t)(lo + j);
             crun += nc;
@@ -519,7 +524,7 @@ __device__ __forceinline__ void hw1_wave_scan_tiles(const uint32_t* counts, cons
     for (int j = 0; j < PER; ++j) {
         if (lo + j < hi) {
             S.offsets[lo + j] = run;
-            csum += hw1_tile_chunks(run, c[j], S.list_cap);
+            csum += hw1_tile_chunks(run, c[j], S.list_cap, S.chunk_log2);
             run += c[j];
         }
     }
@@ -536,7 +541,7 @@ __device__ __forceinline__ void hw1_wave_scan_tiles(const uint32_t* counts, cons
     for (int j = 0; j < PER; ++j) {
         if (lo + j < hi) {
             S.chunk_first[lo + j] = crun;
-            const uint32_t nc = hw1_tile_chunks(run, c[j], S.list_cap);
+            const uint32_t nc = hw1_tile_chunks(run, c[j], S.list_cap, S.chunk_log2);
             for (uint32_t k = 0; k < nc; ++k)
                 if (crun + k < S.chunk_cap) S.chunk_tile[crun + k] = (uint32_t)(lo + j);
             crun += nc;
@@ -644,8 +649,8 @@ __global__ __launch_bounds__(BLOCK) void render_hw1_chunks_kernel(Hw1Params P) {
         const uint32_t cnt = uni(P.bin_count[tidx]);
         const uint32_t off = uni(P.bin_offset[tidx]);
         const bool all = cnt > 0 && off + cnt > P.list_cap;  // the list was not written: every triangle, in order
-        const uint32_t b = all ? 0u : c * HW1_CHUNK;
-        const uint32_t e = all ? (uint32_t)P.num_tris : min(cnt, b + HW1_CHUNK);
+        const uint32_t b = all ? 0u : c << P.chunk_log2;
+        const uint32_t e = all ? (uint32_t)P.num_tris : min(cnt, b + (1u << P.chunk_log2));
         const int x = (int)(tidx % tiles_x) * HW1_TW + (int)(lane % HW1_TW);
         const int y = (int)(tidx / tiles_x) * HW1_TH + (int)(lane / HW1_TW);
         const bool valid = x < P.W && y < P.H;
@@ -777,6 +782,7 @@ struct rt_hw1_scene {
         hipStream_t last_stream = nullptr;  // the stream of the lane's latest frame
         uint64_t last_frame = 0;
         bool used = false;
+        int chunk_log2 = -1;       // the item size the chunk table is laid out for
     };
     static constexpr int kLanes = 8;
     Lane lane[kLanes];
@@ -957,7 +963,14 @@ static int render_frame(rt_hw1_scene* s, int li, const rt_camera* cam, rt_vec3 l
         break;
     }
     const size_t nsamples = size_t(W) * size_t(H) * size_t(spp);
-    if (!brute && (L.bins_tiles != ntiles || L.keys_n != nsamples)) {
+    // work items of 2^lg list entries (RT_TUNE_HW1_CHUNK: 16..256, a power of two)
+    int lg = HW1_CHUNK_LOG2;
+    {
+        const double want = rt::tuning(RT_TUNE_HW1_CHUNK, double(1 << HW1_CHUNK_LOG2));
+        while (lg > 4 && double(1 << lg) > want) --lg;
+        while (lg < 8 && double(1 << lg) < want) ++lg;
+    }
+    if (!brute && (L.bins_tiles != ntiles || L.keys_n != nsamples || L.chunk_log2 != lg)) {
         HIP_TRY(s->sync_lane(L));
         // counts | cursor | done (finished items) | arrive | offsets (ntiles + 1): the first four
         // zeroed here, then by every frame's passes (each tile's resolving item, the count pass's
@@ -966,8 +979,9 @@ static int render_frame(rt_hw1_scene* s, int li, const rt_camera* cam, rt_vec3 l
         // (on the frame's stream: a null-stream memset is not ordered before a non-blocking
         // stream's kernels)
         HIP_TRY(hipMemsetAsync(L.bins.p, 0, size_t(3 * ntiles + 1) * sizeof(uint32_t), st));
-        // chunks: at most one per HW1_CHUNK listed entries plus one per tile
-        L.chunk_cap = uint32_t(std::min<uint64_t>(uint64_t(L.list_cap) / HW1_CHUNK + uint64_t(ntiles) + 1, 0x7FFFFFFFull));
+        // items: at most one per 2^lg listed entries plus one per tile
+        L.chunk_cap = uint32_t(std::min<uint64_t>((uint64_t(L.list_cap) >> lg) + uint64_t(ntiles) + 1, 0x7FFFFFFFull));
+        L.chunk_log2 = lg;
         if ((rc = L.chunks.alloc((size_t(ntiles) + 1 + L.chunk_cap) * sizeof(uint32_t))) != RT_OK) return rc;
         if ((rc = L.keys.alloc(nsamples * sizeof(unsigned long long))) != RT_OK) return rc;
         HIP_TRY(hipMemsetAsync(L.keys.p, 0xFF, nsamples * sizeof(unsigned long long), st));
@@ -1000,6 +1014,7 @@ static int render_frame(rt_hw1_scene* s, int li, const rt_camera* cam, rt_vec3 l
     hp.keys = static_cast<unsigned long long*>(L.keys.p);
     hp.zero_counts = static_cast<uint32_t*>(L.bins.p);
     hp.ntiles = ntiles;
+    hp.chunk_log2 = lg;
     const int sl = int(s->frames % rt_hw1_scene::kRing);
     // the lane's buffers are shared by its frames: a frame on another stream waits for the last
     if (L.used && st != L.last_stream) HIP_TRY(hipStreamWaitEvent(st, s->frame_end(L.last_frame), 0));
@@ -1030,6 +1045,7 @@ static int render_frame(rt_hw1_scene* s, int li, const rt_camera* cam, rt_vec3 l
         sc.chunk_cap = L.chunk_cap;
         sc.total_out = s->total_host + sl;
         sc.tag = uint32_t(s->frames);
+        sc.chunk_log2 = lg;
         // the scan fused into the count pass up to 64 x 80 tiles (c2: 4800), else its own
         // 1024-thread kernel (PER tiles per thread in registers: 8 up to 8192 tiles, 32 up to
         // 1080p's 32400); the first launch carries the start event only on timed frames
@@ -1043,7 +1059,7 @@ static int render_frame(rt_hw1_scene* s, int li, const rt_camera* cam, rt_vec3 l
             auto scan = ntiles <= 8 * 1024 ? hw1_scan_chunks_kernel<8>
                         : ntiles <= 32 * 1024 ? hw1_scan_chunks_kernel<32> : hw1_scan_chunks_kernel<0>;
             hipLaunchKernelGGL(scan, dim3(1), dim3(1024), 0, st, counts, sc.offsets, ntiles, L.list_cap,
-                               sc.chunk_first, sc.chunk_tile, L.chunk_cap, sc.total_out, sc.tag);
+                               sc.chunk_first, sc.chunk_tile, L.chunk_cap, sc.total_out, sc.tag, lg);
         }
         hp.bin_count = counts;
         hp.bin_offset = sc.offsets;
@@ -1051,12 +1067,14 @@ static int render_frame(rt_hw1_scene* s, int li, const rt_camera* cam, rt_vec3 l
         hp.chunk_first = sc.chunk_first;
         hp.chunk_tile = sc.chunk_tile;
         hipLaunchKernelGGL(hw1_fill_kernel, tgrid, dim3(64), 0, st, hp, cursor, static_cast<uint32_t*>(L.list.p));
-        // items grid-stride over a grid of every CU's worth of waves (the count is on the device);
-        // the resolve fused in, or its own pass
+        // items grid-stride over a grid of every CU's worth of waves (the count is on the device),
+        // 4,096 waves for 64-entry items and as many more as the items are smaller; the resolve
+        // fused in, or its own pass
+        const int rblocks = 1024 << std::max(0, 6 - lg);
         if (fuse & 2) {
-            hipExtLaunchKernelGGL(render_hw1_chunks_kernel<true>, dim3(1024), dim3(BLOCK), 0, st, nullptr, t1, 0, hp);
+            hipExtLaunchKernelGGL(render_hw1_chunks_kernel<true>, dim3(rblocks), dim3(BLOCK), 0, st, nullptr, t1, 0, hp);
         } else {
-            hipLaunchKernelGGL(render_hw1_chunks_kernel<false>, dim3(1024), dim3(BLOCK), 0, st, hp);
+            hipLaunchKernelGGL(render_hw1_chunks_kernel<false>, dim3(rblocks), dim3(BLOCK), 0, st, hp);
             const int rgrid = (std::max(W * H, 2 * ntiles) + BLOCK - 1) / BLOCK;
             hipExtLaunchKernelGGL(hw1_resolve_kernel, dim3(rgrid), dim3(BLOCK), 0, st, nullptr, t1, 0, hp);
         }
@@ -1105,7 +1123,7 @@ extern "C" int rt_render_hw1_deliver(rt_hw1_scene* s, const rt_camera* cam, rt_v
             for (hsa_signal_t& d : s->dma_done)
                 if (rt_dma::hsa().signal_create(0, 0, nullptr, &d) != HSA_STATUS_SUCCESS)
                     return set_error(RT_ERR_HIP, "hsa_signal_create failed");
-            s->dma = std::make_unique<rt_dma::DmaCopier>(ga, ca, rt::tuning(RT_TUNE_HW1_COPY_WAIT, 1.0) != 0.0);
+            s->dma = std::make_unique<rt_dma::DmaCopier>(ga, ca, rt::tuning(RT_TUNE_COPY_WAIT, -1.0) != 0.0);
             s->copy_mode = 1;
         } else if (want == 1) {
             return set_error(RT_ERR_UNSUPPORTED, "SDMA delivery unavailable: " + rt_dma::hsa().err);

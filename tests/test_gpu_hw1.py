@@ -55,12 +55,13 @@ def test_resident_hw1_frames_match_reference(name, cfg):
         sc.close()
 
 
-@pytest.mark.parametrize("fuse", [0, 1, 2, 3])
-def test_hw1_fused_passes_match_reference(fuse, tune):
+@pytest.mark.parametrize("fuse,chunk", [(0, 64), (1, 64), (2, 64), (3, 64), (2, 16), (2, 32), (3, 128), (0, 256)])
+def test_hw1_fused_passes_match_reference(fuse, chunk, tune):
     """RT_TUNE_HW1_FUSE: the scan in the count pass's last block (bit 0) and the resolve in each
-    tile's last render item (bit 1), each on or off: the frames equal the reference's (AOVs and
-    P6), twice in a row on the same buffers (the passes leave the counters zeroed)."""
-    tune(hw1_fuse=fuse)
+    tile's last render item (bit 1), each on or off, over work items of 16 to 256 list entries
+    (RT_TUNE_HW1_CHUNK): the frames equal the reference's (AOVs and P6), twice in a row on the
+    same buffers (the passes leave the counters zeroed)."""
+    tune(hw1_fuse=fuse, hw1_chunk=chunk)
     name, c = "c2_full", configs.HW1_CONFIGS["c2"]
     meta = golden_meta(name)
     W, H = meta["width"], meta["height"]

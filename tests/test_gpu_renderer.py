@@ -128,6 +128,33 @@ def test_pipelined_frames_all_identical(frog, golden):
         r.close()
 
 
+def test_overlapped_frames_long_pipelined_run(frog, golden, tune):
+    """RT_TUNE_OVERLAP_FRAMES=1 over a long pipelined run (consecutive render kernels
+    overlap on different render streams, so the pre-pass gate is off; a gate word overwritten by
+    a late frame would hang the prep stream within a few hundred frames): 400 frames at depth 3,
+    every 50th checked against the reference's frame."""
+    tune(overlap_frames=1)
+    r = rt.Renderer.from_host(frog, devices=(0,), depth=3, deliver=rt.RT_DELIVER_P6)
+    try:
+        cam = frog.camera(W, H)
+        o, _j = _opts(frog)
+        want = golden[1].tobytes()
+        pend, checked = [], 0
+        for k in range(400):
+            pend.append((k, r.submit(cam, o)))
+            if len(pend) >= 3:
+                kk, t = pend.pop(0)
+                addr, n = r.wait(t)
+                if kk % 50 == 0:
+                    assert bytes((C.c_uint8 * n).from_address(addr)) == want, kk
+                    checked += 1
+        for kk, t in pend:
+            r.wait(t)
+        assert checked == 8
+    finally:
+        r.close()
+
+
 @pytest.mark.parametrize("engine,overlap", [(None, 0), (0, 0), (1, 0), (None, 1), (0, 1)])
 @pytest.mark.parametrize("depth", [2, 3])
 def test_copy_engines_deliver_the_reference_frame(frog, golden, engine, overlap, depth, tune):

@@ -566,8 +566,9 @@ typedef enum {
                                     overlaps the others only on a hardware queue of its own (HIP:
                                     GPU_MAX_HW_QUEUES per process, 4 by default) */
     RT_TUNE_COPY_WAIT = 22,      /* the SDMA copier threads (rt_renderer's and rt_hw1_scene's deliveries): 1 waits
-                                    for a frame with hipEventSynchronize, 0 polls hipEventQuery; default
-                                    -1: the renderer polls, the HW1 scene waits; at the copier's creation */
+                                    for a frame with hipEventSynchronize, 0 polls hipEventQuery spinning,
+                                    2..1000 polls every that many microseconds; default -1: the renderer
+                                    spins, the HW1 scene waits; at the copier's creation */
     RT_TUNE_HW1_FUSE = 23,       /* the HW1 scene's frames: bit 0 the scan fused into the count pass (its last
                                     block, up to 5,120 tiles), bit 1 the resolve fused into the render pass
                                     (each tile's last item); default 2 */

@@ -9,6 +9,7 @@
 
 #include <dlfcn.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -151,7 +152,9 @@ class DmaCopier {
     // block: wait for a job's event with hipEventSynchronize (one runtime call per job) instead of
     // polling it with hipEventQuery (each poll takes the runtime's locks the submitting thread
     // needs for its launches; polling reacts sooner)
-    DmaCopier(hsa_agent_t gpu, hsa_agent_t cpu, bool block = false) : gpu_(gpu), cpu_(cpu), block_(block) {
+    // poll_us > 0: poll every poll_us microseconds (sleeping between polls) instead of spinning
+    DmaCopier(hsa_agent_t gpu, hsa_agent_t cpu, bool block = false, int poll_us = 0)
+        : gpu_(gpu), cpu_(cpu), block_(block), poll_us_(poll_us) {
         th_ = std::thread([this] { loop(); });
     }
     ~DmaCopier() {
@@ -192,7 +195,8 @@ class DmaCopier {
                 e = hipEventSynchronize(j.ready);
             } else {
                 for (uint32_t i = 0; (e = hipEventQuery(j.ready)) == hipErrorNotReady; ++i) {
-                    if (i < 4096) _mm_pause();
+                    if (poll_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(poll_us_));
+                    else if (i < 4096) _mm_pause();
                     else std::this_thread::yield();
                 }
             }
@@ -212,6 +216,7 @@ class DmaCopier {
     }
     hsa_agent_t gpu_, cpu_;
     bool block_ = false;
+    int poll_us_ = 0;
     std::thread th_;
     std::mutex m_;
     std::condition_variable cv_;

@@ -1123,7 +1123,9 @@ extern "C" int rt_render_hw1_deliver(rt_hw1_scene* s, const rt_camera* cam, rt_v
             for (hsa_signal_t& d : s->dma_done)
                 if (rt_dma::hsa().signal_create(0, 0, nullptr, &d) != HSA_STATUS_SUCCESS)
                     return set_error(RT_ERR_HIP, "hsa_signal_create failed");
-            s->dma = std::make_unique<rt_dma::DmaCopier>(ga, ca, rt::tuning(RT_TUNE_COPY_WAIT, -1.0) != 0.0);
+            const double cw = rt::tuning(RT_TUNE_COPY_WAIT, -1.0);
+            s->dma = std::make_unique<rt_dma::DmaCopier>(ga, ca, cw == 1.0 || cw < 0.0,
+                                                         cw >= 2.0 ? int(std::min(cw, 1000.0)) : 0);
             s->copy_mode = 1;
         } else if (want == 1) {
             return set_error(RT_ERR_UNSUPPORTED, "SDMA delivery unavailable: " + rt_dma::hsa().err);

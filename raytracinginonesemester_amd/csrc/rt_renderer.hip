@@ -787,7 +787,8 @@ extern "C" int rt_renderer_create(size_t P, const rt_bvh_node* nodes, const rt_a
                     return set_error(RT_ERR_HIP, "hsa_signal_create failed");
             r->dma_submit_ts.assign(depth, 0);
             r->dma_pending.assign(depth, false);
-            r->dma = std::make_unique<DmaCopier>(ga, ca, rt::tuning(RT_TUNE_COPY_WAIT, -1.0) > 0.0);
+            const double cw = rt::tuning(RT_TUNE_COPY_WAIT, -1.0);
+            r->dma = std::make_unique<DmaCopier>(ga, ca, cw == 1.0, cw >= 2.0 ? int(std::min(cw, 1000.0)) : 0);
         } else if (engine > 0.0) {
             return set_error(RT_ERR_UNSUPPORTED, "SDMA delivery unavailable: " + hsa().err);
         }

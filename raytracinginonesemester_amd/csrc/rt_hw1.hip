@@ -29,6 +29,48 @@ constexpr int BLOCK = 256;  // threads per block (rt_device.hip's render blocks 
 #include "rt_wave.hpp"
 
 // ---- HW1 brute force (HW1/src/render.cpp:72-116) ----------------------------------------
+// The camera-only half of hw1_rect's bounds: the ray direction D = pixel00 + ix du + iy dv -
+// center over the image's (ix, iy) range per axis, padded for its float evaluation, and |D|'s
+// bounds.  The same for every triangle of a frame, so the host makes it once per frame; the same
+// double operations in the same order (-ffp-contract=off on both sides) as the device made them
+// per triangle before round 6.
+struct Hw1Cam {
+    double du[3], dv[3], D00[3], Dl[3], Dh[3], pad[3], nmin, nmax;
+};
+__host__ __device__ inline Hw1Cam hw1_cam_bounds(const float center[3], const float p00[3], const float pdu[3],
+                                                 const float pdv[3], int W, int H) {
+    Hw1Cam o;
+    const int X0 = -2, X1 = W + 1, Y0 = -2, Y1 = H + 1;  // ix in [x, x+1] (truncation)
+    const double cc[3] = {center[0], center[1], center[2]}, p0[3] = {p00[0], p00[1], p00[2]};
+    for (int a = 0; a < 3; ++a) {
+        o.du[a] = pdu[a];
+        o.dv[a] = pdv[a];
+    }
+    const double xm = fmax(fabs((double)X0), fabs((double)X1)), ym = fmax(fabs((double)Y0), fabs((double)Y1));
+    double scale = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        o.D00[a] = p0[a] - cc[a];
+        const double u0 = X0 * o.du[a], u1 = X1 * o.du[a], w0 = Y0 * o.dv[a], w1 = Y1 * o.dv[a];
+        o.Dl[a] = o.D00[a] + fmin(u0, u1) + fmin(w0, w1);
+        o.Dh[a] = o.D00[a] + fmax(u0, u1) + fmax(w0, w1);
+        o.pad[a] = 8.0 * 0x1p-23 * (fabs(cc[a]) + fabs(p0[a]) + xm * fabs(o.du[a]) + ym * fabs(o.dv[a]));
+        scale = fmax(scale, fmax(fabs(o.Dl[a]), fabs(o.Dh[a])));
+    }
+    double nmin2 = 0.0, nmax2 = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        o.pad[a] += 1e-5 * scale;
+        o.Dl[a] -= o.pad[a];
+        o.Dh[a] += o.pad[a];
+        const double near = o.Dl[a] > 0 ? o.Dl[a] : (o.Dh[a] < 0 ? o.Dh[a] : 0.0);
+        const double far = fmax(fabs(o.Dl[a]), fabs(o.Dh[a]));
+        nmin2 += near * near;
+        nmax2 += far * far;
+    }
+    o.nmin = sqrt(nmin2) * (1 - 1e-12);
+    o.nmax = sqrt(nmax2) * (1 + 1e-12);
+    return o;
+}
+
 struct Hw1Params {
     const float4* __restrict__ tri;   // 3 float4 per triangle: v0, e1, e2
     const float4* __restrict__ nrm;   // 3 float4 per triangle: n0, n1, n2
@@ -56,6 +98,7 @@ struct Hw1Params {
                             // entries for the lane's next frame (after every item of the tile read them)
     int32_t ntiles;
     int32_t chunk_log2;  // work item size (RT_TUNE_HW1_CHUNK)
+    Hw1Cam cb;           // the frame's camera bounds for hw1_rect (binned path)
 };
 
 // The scan's outputs (hw1_scan_chunks_kernel's arguments, for the scan fused into the count pass).
@@ -239,30 +282,14 @@ __device__ int4 hw1_rect(const Hw1Params& P, int k) {
     w[1] = -(Ev + tiny);
     w[2] = -(4 * uu * dmax + Eu + Ev + Ed + tiny);
     w[3] = (double)FLT_EPSILON - Ed;
-    // D over the image, per axis, padded as in tile_dirs
-    const double cc[3] = {P.center.x, P.center.y, P.center.z}, p0[3] = {P.p00.x, P.p00.y, P.p00.z},
-                 du[3] = {P.du.x, P.du.y, P.du.z}, dv[3] = {P.dv.x, P.dv.y, P.dv.z};
-    const double xm = fmax(fabs((double)X0), fabs((double)X1)), ym = fmax(fabs((double)Y0), fabs((double)Y1));
-    double D00[3], Dl[3], Dh[3], pad[3], scale = 0.0;
-    for (int a = 0; a < 3; ++a) {
-        D00[a] = p0[a] - cc[a];
-        const double u0 = X0 * du[a], u1 = X1 * du[a], w0 = Y0 * dv[a], w1 = Y1 * dv[a];
-        Dl[a] = D00[a] + fmin(u0, u1) + fmin(w0, w1);
-        Dh[a] = D00[a] + fmax(u0, u1) + fmax(w0, w1);
-        pad[a] = 8.0 * 0x1p-23 * (fabs(cc[a]) + fabs(p0[a]) + xm * fabs(du[a]) + ym * fabs(dv[a]));
-        scale = fmax(scale, fmax(fabs(Dl[a]), fabs(Dh[a])));
-    }
-    double nmin2 = 0.0, nmax2 = 0.0;
-    for (int a = 0; a < 3; ++a) {
-        pad[a] += 1e-5 * scale;
-        Dl[a] -= pad[a];
-        Dh[a] += pad[a];
-        const double near = Dl[a] > 0 ? Dl[a] : (Dh[a] < 0 ? Dh[a] : 0.0);
-        const double far = fmax(fabs(Dl[a]), fabs(Dh[a]));
-        nmin2 += near * near;
-        nmax2 += far * far;
-    }
-    const double nmin = sqrt(nmin2) * (1 - 1e-12), nmax = sqrt(nmax2) * (1 + 1e-12);
+    // D over the image, per axis, padded as in tile_dirs: the frame's own (hw1_cam_bounds)
+    const double* D00 = P.cb.D00;
+    const double* Dl = P.cb.Dl;
+    const double* Dh = P.cb.Dh;
+    const double* pad = P.cb.pad;
+    const double* du = P.cb.du;
+    const double* dv = P.cb.dv;
+    const double nmin = P.cb.nmin, nmax = P.cb.nmax;
     if (!(nmin > 0.0) || !(nmax < 1e300)) {
         return all;
     }
@@ -996,6 +1023,13 @@ static int render_frame(rt_hw1_scene* s, int li, const rt_camera* cam, rt_vec3 l
     hp.p00 = f3{cam->pixel00_loc.x, cam->pixel00_loc.y, cam->pixel00_loc.z};
     hp.du = f3{cam->pixel_delta_u.x, cam->pixel_delta_u.y, cam->pixel_delta_u.z};
     hp.dv = f3{cam->pixel_delta_v.x, cam->pixel_delta_v.y, cam->pixel_delta_v.z};
+    {
+        const float c3[3] = {cam->center.x, cam->center.y, cam->center.z};
+        const float p3[3] = {cam->pixel00_loc.x, cam->pixel00_loc.y, cam->pixel00_loc.z};
+        const float u3[3] = {cam->pixel_delta_u.x, cam->pixel_delta_u.y, cam->pixel_delta_u.z};
+        const float v3[3] = {cam->pixel_delta_v.x, cam->pixel_delta_v.y, cam->pixel_delta_v.z};
+        hp.cb = hw1_cam_bounds(c3, p3, u3, v3, W, H);
+    }
     hp.W = W;
     hp.H = H;
     hp.spp = spp;

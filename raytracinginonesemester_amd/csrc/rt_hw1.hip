@@ -687,12 +687,20 @@ __global__ __launch_bounds__(BLOCK) void render_hw1_chunks_kernel(Hw1Params P) {
         for (int s = 0; s < P.spp; ++s) {
             const f3 d = hw1_dir(P, x, y, s);
             unsigned long long best = ~0ull;
+            // the item's triangle indices, 64 at a time, lane l holding entry ib + l (one
+            // coalesced load, then v_readlane: the triangles' scalar loads wait on no second
+            // round trip)
+            uint32_t idx = 0, ib = b;
             for (uint32_t i = b; i < e; i += 4) {
+                if (((i - b) & 63u) == 0) {
+                    ib = i;
+                    const uint32_t j = i + lane;
+                    idx = all ? j : (j < e ? P.bin_list[off + j] : 0u);
+                }
                 int kk[4];
                 float4 tq[12];
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    kk[q] = i + q < e ? (all ? (int)(i + q) : (int)ldc_u32(P.bin_list + off + i + q)) : -1;
+                for (int q = 0; q < 4; ++q) kk[q] = i + q < e ? (int)rdlane(idx, i + q - ib) : -1;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const float4* T = P.tri + 3 * (size_t)(kk[q] < 0 ? kk[0] : kk[q]);
